@@ -1,0 +1,145 @@
+/*
+ * maleague.h -- C ABI of the MI355X-native hot path of PMatthaei/ma-league (libmaleague.so, gfx950).
+ *
+ * Every entry point takes plain device pointers (HBM, allocated by the caller: PyTorch's caching
+ * allocator in the Python host package), sizes, and a hipStream_t passed as void*. Kernels are
+ * enqueued on that stream; no call allocates, frees or synchronises (graph-capturable), except
+ * where noted. Return value: 0 on success, nonzero on error; mlg_last_error() holds the message.
+ *
+ * Reference interfaces each entry point replaces (file:line in /root/reference):
+ *   mlg_rollout        ParallelStepper.run / reset  src/steppers/parallel_stepper.py:82-216
+ *                      + EnvWorker step/reset       src/steppers/utils/env_worker_process.py:27-71
+ *                      + BasicMAC.select_actions    src/marl/controllers/basic_controller.py:29-36
+ *                      + EpsilonGreedy.select       src/marl/components/action_selectors.py:44-62
+ *                      + maenv TeamsEnv.step/get_obs/get_state/get_avail_actions (external)
+ *   mlg_env_reset      EnvWorker "reset" command    src/steppers/utils/env_worker_process.py:54-60
+ *   mlg_env_step       EnvWorker "step" command     src/steppers/utils/env_worker_process.py:32-53
+ *   mlg_env_observe    TeamsEnv get_obs/get_state/get_avail_actions (env_worker_process.py:41-42)
+ *   mlg_agent_forward  DRQNAgentNetwork.forward     src/marl/modules/agents/drqn_agent.py:29-35
+ *   mlg_mac_forward    BasicMAC.forward + _build_inputs  src/marl/controllers/basic_controller.py:38-50,80-92
+ *   mlg_select_actions EpsilonGreedyActionSelector.select src/marl/components/action_selectors.py:44-62
+ *   mlg_pack_agent     (layout step feeding the above; no reference counterpart)
+ *   mlg_qmix_forward   QMixer.forward               src/marl/modules/mixers/qmix.py:41-59
+ *   mlg_qlearner_*     QLearner.train               src/marl/learners/q_learner.py:34-131
+ *                      + clip_grad_norm_ + RMSprop.step (q_learner.py:104-105, learner.py:25-31)
+ */
+#ifndef MALEAGUE_H
+#define MALEAGUE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MLG_MAXU 64 /* max units per env (large.json has 50) */
+
+/* Frozen synthetic TeamsEnv spec v1. Built on the host from env_args. */
+typedef struct {
+    int32_t U;             /* total units (both teams) */
+    int32_t n_agents;      /* policy-controlled units = env_info["n_agents"] */
+    int32_t n_actions;     /* 5 + U */
+    int32_t grid;          /* env_args.grid_size */
+    int32_t episode_limit; /* env_info["episode_limit"] */
+    int32_t stochastic;    /* env_args.stochastic_spawns */
+    int32_t policy_team;   /* first non-scripted plan team (stepper_utils.py:48-55) */
+    int32_t n_policy_teams;
+    int32_t team[MLG_MAXU];
+    int32_t role[MLG_MAXU];  /* TANK 0, HEALER 1, ADC 2 */
+    int32_t melee[MLG_MAXU]; /* RANGED 0, MELEE 1 */
+    int32_t agent_unit[MLG_MAXU];
+    int32_t scripted[2];
+    uint64_t seed; /* per-env key = seed * 2^32 + env_index */
+} MlgEnvSpec;
+
+/* Device-resident env state, SoA, [B][U] int32 + per-env counters. */
+typedef struct {
+    int32_t *x, *y, *hp;   /* [B*U] */
+    int32_t *t;            /* [B] step index within episode */
+    uint32_t *episode;     /* [B] episodes started (RNG stream counter) */
+    int32_t B;
+} MlgEnvState;
+
+/* EpisodeBatch transition tensors (scheme of ma_experiment.py:99-118), all [B][T1][...] row-major. */
+typedef struct {
+    float *state;          /* [B][T1][S] */
+    float *obs;            /* [B][T1][N][d_obs] */
+    int64_t *actions;      /* [B][T1][N][1] */
+    int32_t *avail;        /* [B][T1][N][A] */
+    float *reward;         /* [B][T1][1] */
+    uint8_t *terminated;   /* [B][T1][1] */
+    float *actions_onehot; /* [B][T1][N][A] */
+    int64_t *filled;       /* [B][T1][1] */
+    int32_t B, T1;
+} MlgBatch;
+
+/* Per-run episode summary written by mlg_rollout. */
+typedef struct {
+    int32_t *ep_len;   /* [B] env steps taken (t_env increment per env) */
+    float *ret;        /* [B] episode return of the policy team (reward[0]) */
+    int32_t *won;      /* [B][2] battle_won, policy team first */
+    int32_t *draw;     /* [B] */
+} MlgRunInfo;
+
+/* Agent weights in canonical nn.Module layout (state_dict of DRQNAgentNetwork). */
+typedef struct {
+    const float *fc1_w, *fc1_b;     /* [H][d_in], [H] */
+    const float *w_ih, *b_ih;       /* [3H][H], [3H] */
+    const float *w_hh, *b_hh;       /* [3H][H], [3H] */
+    const float *fc2_w, *fc2_b;     /* [A][H], [A] */
+} MlgAgentParams;
+
+typedef struct {
+    int32_t d_obs, n_actions, n_agents, hidden, d_in;
+    int32_t obs_last_action, obs_agent_id;
+} MlgAgentDims;
+
+/* Size in floats of the packed agent weight block used by the kernels. */
+int64_t mlg_packed_agent_size(const MlgAgentDims *d);
+int mlg_pack_agent(const MlgAgentDims *d, const MlgAgentParams *p, float *packed, void *stream);
+
+int mlg_env_reset(const MlgEnvSpec *spec, MlgEnvState *st, void *stream);
+int mlg_env_step(const MlgEnvSpec *spec, MlgEnvState *st, const int64_t *actions /*[B][N]*/,
+                 float *reward /*[B][n_policy_teams]*/, int32_t *done /*[B]*/, int32_t *won /*[B][2]*/,
+                 int32_t *draw /*[B]*/, void *stream);
+int mlg_env_observe(const MlgEnvSpec *spec, const MlgEnvState *st, float *obs /*[B][N][8U]*/,
+                    float *state /*[B][6U]*/, int32_t *avail /*[B][N][A]*/, void *stream);
+
+/* One full ParallelStepper.run: reset all B envs, step until every env terminated, filling `batch`
+ * (caller zero-initialised, like EpisodeBatch construction). epsilon already evaluated on the host
+ * (DecayThenFlatSchedule.eval(t_env)); test_mode forces epsilon 0. */
+int mlg_rollout(const MlgEnvSpec *spec, MlgEnvState *st, const MlgAgentDims *dims, const float *packed,
+                MlgBatch *batch, MlgRunInfo *info, float epsilon, int32_t test_mode, void *stream);
+
+/* DRQN forward over R rows: q[R][A], h_out[R][H] from inputs[R][d_in], h_in[R][H]. */
+int mlg_agent_forward(const MlgAgentDims *d, const float *packed, const float *inputs, const float *h_in,
+                      float *q, float *h_out, int32_t R, void *stream);
+
+/* BasicMAC.forward(ep_batch, t): builds inputs from the batch at t (obs, onehot(a_{t-1}), agent id). */
+int mlg_mac_forward(const MlgAgentDims *d, const float *packed, const MlgBatch *batch, int32_t t,
+                    const float *h_in, float *q /*[B][N][A]*/, float *h_out, void *stream);
+
+/* Epsilon-greedy over rows r of q[R][A] with avail[R][A] (int32). rng key per row:
+ * keys[r / n_agents] with ctr(episode[r / n_agents], t, purpose, r % n_agents). */
+int mlg_select_actions(const float *q, const int32_t *avail, int32_t R, int32_t A, int32_t n_agents,
+                       const uint64_t *keys, const uint32_t *episodes, int32_t t, float epsilon,
+                       int64_t *actions, int64_t *is_greedy, void *stream);
+
+/* QMixer forward (hypernet_layers 1 or 2). */
+typedef struct {
+    const float *hw1_0w, *hw1_0b, *hw1_2w, *hw1_2b; /* hyper_w_1 (2 layers) or hyper_w_1 (1 layer: 0w/0b) */
+    const float *hwf_0w, *hwf_0b, *hwf_2w, *hwf_2b;
+    const float *hb1_w, *hb1_b;
+    const float *v0_w, *v0_b, *v2_w, *v2_b;
+    int32_t n_agents, state_dim, embed_dim, hypernet_embed, hypernet_layers;
+} MlgQMixParams;
+int mlg_qmix_forward(const MlgQMixParams *p, const float *agent_qs /*[R][N]*/, const float *states /*[R][S]*/,
+                     float *q_tot /*[R]*/, int32_t R, void *stream);
+
+const char *mlg_last_error(void);
+const char *mlg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

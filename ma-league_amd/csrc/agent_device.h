@@ -1,0 +1,219 @@
+// agent_device.h -- the DRQN agent cell (fc1 -> ReLU -> GRUCell -> fc2) on one 16-row tile per wave,
+// f32 MFMA (16x16x4), register resident.  Restates DRQNAgentNetwork.forward
+// (src/marl/modules/agents/drqn_agent.py:29-35) with BasicMAC._build_inputs folded in
+// (src/marl/controllers/basic_controller.py:80-92): the one-hot last action and the agent id
+// columns of fc1 are added as weight-column gathers instead of dense K (identical sum, no zeros).
+//
+// Packed weight block (floats; every offset 16-byte aligned; H % 16 == 0):
+//   w1d [H][Dip]  fc1.weight dense (Dip = d_in rounded up to 16, zero padded) for arbitrary inputs
+//   w1o [H][Dob]  fc1.weight obs columns (Dob = d_obs rounded up to 16, zero padded)
+//   w1a [A][H]    fc1.weight last-action columns, transposed   (present iff obs_last_action)
+//   w1n [N][H]    fc1.weight agent-id columns, transposed       (present iff obs_agent_id)
+//   b1  [H]
+//   wih [3H][H], bih [3H], whh [3H][H], bhh [3H]   (PyTorch GRUCell gate order r, z, n)
+//   brz [2H]      b_ih + b_hh for the r,z gates (pre-summed)
+//   w2  [Ap][H]   fc2.weight zero padded to Ap = A rounded up to 16 rows
+//   b2  [Ap]
+#pragma once
+#include "mlg_device.h"
+
+struct AgentLayout {
+    int H, A, Ap, N, d_obs, Dob, d_in, Dip, last_action, agent_id;
+    int64_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;
+};
+
+__host__ __device__ inline int64_t mlg_align4(int64_t v) { return (v + 3) & ~int64_t(3); }
+
+__host__ __device__ inline AgentLayout make_agent_layout(const MlgAgentDims& d) {
+    AgentLayout L;
+    L.H = d.hidden;
+    L.A = d.n_actions;
+    L.Ap = (d.n_actions + 15) / 16 * 16;
+    L.N = d.n_agents;
+    L.d_obs = d.d_obs;
+    L.Dob = (d.d_obs + 15) / 16 * 16;
+    L.d_in = d.d_in;
+    L.Dip = (d.d_in + 15) / 16 * 16;
+    L.last_action = d.obs_last_action;
+    L.agent_id = d.obs_agent_id;
+    int64_t o = 0;
+    L.w1d = o; o += (int64_t)L.H * L.Dip;
+    L.w1o = o; o += (int64_t)L.H * L.Dob;
+    L.w1a = o; o += L.last_action ? (int64_t)L.A * L.H : 0;
+    L.w1n = o; o += L.agent_id ? (int64_t)L.N * L.H : 0;
+    L.b1 = o; o += L.H;
+    L.wih = o; o += (int64_t)3 * L.H * L.H;
+    L.bih = o; o += 3 * L.H;
+    L.whh = o; o += (int64_t)3 * L.H * L.H;
+    L.bhh = o; o += 3 * L.H;
+    L.brz = o; o += 2 * L.H;
+    L.w2 = o; o += (int64_t)L.Ap * L.H;
+    L.b2 = o; o += L.Ap;
+    L.total = mlg_align4(o);
+    return L;
+}
+
+// Per-lane inputs of a 16-row tile: this lane's row (col = lane & 15) data.
+//   DENSE:      x = full input row [d_in] (DRQNAgentNetwork.forward on arbitrary inputs)
+//   structured: x = obs row [d_obs]; last action from `onehot` (A floats, added as v * column) or,
+//               when onehot == nullptr, from `prev_action` (-1: zeros, t == 0); agent id column `agent`.
+struct RowIn {
+    const float* x;
+    const float* onehot;
+    int prev_action;
+    int agent;
+};
+
+__device__ __forceinline__ floatx4 load_chunk(const float* x, int k0, int n) {
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (x) {
+        if (k0 + 3 < n) {
+            v = floatx4{x[k0], x[k0 + 1], x[k0 + 2], x[k0 + 3]};
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (k0 + r < n) ? x[k0 + r] : 0.f;
+        }
+    }
+    return v;
+}
+
+// fc1 (pre-activation, bias included) for one tile -> x (HC chunks, D layout).
+template <int H, bool DENSE>
+__device__ __forceinline__ void agent_fc1(const float* __restrict__ P, const AgentLayout& L, const RowIn& in,
+                                          floatx4 (&x)[H / 16], int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int mt = 0; mt < HC; ++mt) {
+        floatx4 b = ld4(P + L.b1 + mt * 16 + 4 * g);
+        if (!DENSE) {
+            if (L.last_action) {
+                if (in.onehot) {
+                    for (int a = 0; a < L.A; ++a) {
+                        const float v = in.onehot[a];
+                        if (v != 0.f) b += v * ld4(P + L.w1a + (int64_t)a * H + mt * 16 + 4 * g);
+                    }
+                } else if (in.prev_action >= 0) {
+                    b += ld4(P + L.w1a + (int64_t)in.prev_action * H + mt * 16 + 4 * g);
+                }
+            }
+            if (L.agent_id) b += ld4(P + L.w1n + (int64_t)in.agent * H + mt * 16 + 4 * g);
+        }
+        x[mt] = b;
+    }
+    const int K = DENSE ? L.d_in : L.d_obs;
+    const int KP = DENSE ? L.Dip : L.Dob;
+    const int64_t base = DENSE ? L.w1d : L.w1o;
+    for (int kc = 0; kc < KP / 16; ++kc) {
+        const int k0 = kc * 16 + 4 * g;
+        const floatx4 xin = load_chunk(in.x, k0, K);
+#pragma unroll
+        for (int mt = 0; mt < HC; ++mt) x[mt] = mfma_chunk(ld4(P + base + (int64_t)(mt * 16 + col) * KP + k0), xin, x[mt]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// fc1 + ReLU + GRUCell for one tile; h (HC chunks, D layout) updated in place.
+template <int H, bool DENSE = false>
+__device__ __forceinline__ void agent_cell_hidden(const float* __restrict__ P, const AgentLayout& L, const RowIn& in,
+                                                  floatx4 (&h)[H / 16], int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4;
+    floatx4 x[HC];
+    agent_fc1<H, DENSE>(P, L, in, x, lane);
+#pragma unroll
+    for (int mt = 0; mt < HC; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[mt][r] = fmaxf(x[mt][r], 0.f);
+    // ---- GRUCell, one 16-feature output chunk at a time (4 live accumulators):
+    //   r = sig(W_ir x + W_hr h + b_ir + b_hr), z likewise, n = tanh(W_in x + b_in + r (W_hn h + b_hn)),
+    //   h' = (h - n) z + n   (PyTorch GRUCell gate order and formula)
+    floatx4 hn[HC];
+#pragma unroll
+    for (int mt = 0; mt < HC; ++mt) {
+        floatx4 ar = ld4(P + L.brz + mt * 16 + 4 * g);
+        floatx4 az = ld4(P + L.brz + H + mt * 16 + 4 * g);
+        floatx4 ain = ld4(P + L.bih + 2 * H + mt * 16 + 4 * g);
+        floatx4 ahn = ld4(P + L.bhh + 2 * H + mt * 16 + 4 * g);
+        const float* wr_i = P + L.wih + (int64_t)(mt * 16 + col) * H + 4 * g;
+        const float* wr_h = P + L.whh + (int64_t)(mt * 16 + col) * H + 4 * g;
+#pragma unroll
+        for (int kc = 0; kc < HC; ++kc) {
+            const int k0 = kc * 16;
+            ar = mfma_chunk(ld4(wr_i + k0), x[kc], ar);
+            az = mfma_chunk(ld4(wr_i + (int64_t)H * H + k0), x[kc], az);
+            ain = mfma_chunk(ld4(wr_i + (int64_t)2 * H * H + k0), x[kc], ain);
+            ar = mfma_chunk(ld4(wr_h + k0), h[kc], ar);
+            az = mfma_chunk(ld4(wr_h + (int64_t)H * H + k0), h[kc], az);
+            ahn = mfma_chunk(ld4(wr_h + (int64_t)2 * H * H + k0), h[kc], ahn);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float rg = 1.f / (1.f + expf(-ar[r]));
+            const float zg = 1.f / (1.f + expf(-az[r]));
+            const float ng = tanhf(ain[r] + rg * ahn[r]);
+            hn[mt][r] = ng + zg * (h[mt][r] - ng);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the next chunk's weight loads from being hoisted (VGPR budget)
+    }
+#pragma unroll
+    for (int mt = 0; mt < HC; ++mt) h[mt] = hn[mt];
+}
+
+// fc2 for action tile at (16 actions starting at 16*at): q (D layout) for this lane's row.
+template <int H>
+__device__ __forceinline__ floatx4 agent_q_tile(const float* __restrict__ P, const AgentLayout& L, const floatx4 (&h)[H / 16],
+                                                int at, int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4;
+    floatx4 q = ld4(P + L.b2 + at * 16 + 4 * g);
+#pragma unroll
+    for (int kc = 0; kc < HC; ++kc)
+        q = mfma_chunk(ld4(P + L.w2 + (int64_t)(at * 16 + col) * H + kc * 16 + 4 * g), h[kc], q);
+    return q;
+}
+
+// Masked greedy argmax + epsilon-greedy pick for the lane's row (EpsilonGreedyActionSelector.select,
+// action_selectors.py:44-62). q tile values for actions 16*at + 4*g + r. Returns, in every lane of the
+// row group, the chosen action.  avail: this row's A ints (nullptr -> all available).
+struct ArgmaxState {
+    float bv;
+    int bi;
+};
+
+__device__ __forceinline__ void argmax_accumulate(ArgmaxState& s, const floatx4 q, const int32_t* avail, int at, int A, int lane) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int a = at * 16 + 4 * g + r;
+        if (a >= A) continue;
+        const float v = (avail && avail[a] == 0) ? -INFINITY : q[r];
+        if (amax_better(v, a, s.bv, s.bi)) { s.bv = v; s.bi = a; }
+    }
+}
+
+__device__ __forceinline__ int argmax_reduce(ArgmaxState s) {
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+        const float ov = __shfl_xor(s.bv, m);
+        const int oi = __shfl_xor(s.bi, m);
+        if (amax_better(ov, oi, s.bv, s.bi)) { s.bv = ov; s.bi = oi; }
+    }
+    return s.bi;
+}
+
+// Random available action: k-th available with k = floor(u * n_avail), integer form (spec §3.7).
+__device__ __forceinline__ int random_available(const int32_t* avail, int A, uint64_t r) {
+    int n = 0;
+    for (int a = 0; a < A; ++a) n += (avail == nullptr || avail[a] != 0);
+    if (n == 0) return 0;
+    const int k = (int)(((r >> 40) * (uint64_t)n) >> 24);
+    int c = 0;
+    for (int a = 0; a < A; ++a) {
+        if (avail == nullptr || avail[a] != 0) {
+            if (c == k) return a;
+            ++c;
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,213 @@
+// mlg_device.h -- shared device helpers for the gfx950 kernels of libmaleague.
+//
+// * f32 MFMA (v_mfma_f32_16x16x4_f32) fragment helpers for the 16-row agent tiles
+// * the counter-based RNG of the env spec (splitmix64)
+// * the synthetic TeamsEnv spec v1 as device functions (bit-exact restatement checked against
+//   oracle/env_ref.c; the reference env itself -- external maenv -- is not available)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/maleague.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+#define MLG_ACT_BASE 5
+#define MLG_SIGHT2 36
+
+// ------------------------------------------------------------------------------------------------
+// MFMA: D[16x16] += A[16x4] * B[4x16]; lane l supplies A[l&15][l>>4], B[l>>4][l&15];
+// D lane l, reg r = D[4*(l>>4)+r][l&15].  Orientation used everywhere below: A = weights
+// (rows = output features), B = activations (cols = agent rows), so a result tile is already the
+// B operand of the next layer with the K index permuted (feature 16c + 4*(l>>4) + r at step (c, r)),
+// and the weight operand is read with the same permutation as one float4 per 4 MFMAs.
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+
+__device__ __forceinline__ floatx4 mfma_chunk(const floatx4 w, const floatx4 x, floatx4 acc) {
+    acc = mfma4(w.x, x.x, acc);
+    acc = mfma4(w.y, x.y, acc);
+    acc = mfma4(w.z, x.z, acc);
+    acc = mfma4(w.w, x.w, acc);
+    return acc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// RNG (spec §3.7): rng(key, ctr) = splitmix64(key ^ splitmix64(ctr))
+__device__ __forceinline__ uint64_t mlg_splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t mlg_rng(uint64_t key, uint64_t ctr) { return mlg_splitmix64(key ^ mlg_splitmix64(ctr)); }
+__device__ __forceinline__ uint64_t mlg_ctr(uint32_t episode, uint32_t t, uint32_t purpose, uint32_t idx) {
+    return ((uint64_t)episode << 32) | ((uint64_t)(t & 0xFFFFu) << 16) | ((uint64_t)(purpose & 0xFu) << 12) |
+           (uint64_t)(idx & 0xFFFu);
+}
+__device__ __forceinline__ float mlg_u01(uint64_t r) { return (float)(r >> 40) * (1.0f / 16777216.0f); }
+__device__ __forceinline__ uint64_t mlg_env_key(uint64_t seed, int env) { return (seed << 32) + (uint64_t)env; }
+
+enum { MLG_PURPOSE_SPAWN = 1, MLG_PURPOSE_EPS = 2, MLG_PURPOSE_RAND = 3 };
+
+// ------------------------------------------------------------------------------------------------
+// Env spec v1. Unit tables live in LDS, copied from the MlgEnvSpec kernel argument.
+struct EnvTables {
+    const int* team;   // [U]
+    const int* role;   // [U]
+    const int* melee;  // [U]
+    const int* agent;  // [U] agent index + 1, 0 for scripted units
+    int U, grid, episode_limit, stochastic;
+};
+
+__device__ __forceinline__ int role_maxhp(int r) { return r == 0 ? 64 : 32; }
+__device__ __forceinline__ int role_power(int r) { return r == 0 ? 3 : (r == 1 ? 4 : 6); }
+__device__ __forceinline__ int atk_range2(int melee) { return melee ? 2 : 9; }
+__device__ __forceinline__ float inv_maxhp(int r) { return r == 0 ? (1.0f / 64.0f) : (1.0f / 32.0f); }
+
+__device__ __forceinline__ int pow2_at_least(int g) {
+    int p = 1;
+    while (p < g) p <<= 1;
+    return p;
+}
+
+__device__ __forceinline__ int env_dist2(const int* x, const int* y, int i, int j) {
+    int dx = x[j] - x[i], dy = y[j] - y[i];
+    return dx * dx + dy * dy;
+}
+
+// Availability of action a for unit i (spec §3.2).
+__device__ __forceinline__ int env_avail_one(const EnvTables& T, const int* x, const int* y, const int* hp, int i, int a) {
+    const int alive = hp[i] > 0;
+    if (a == 0) return !alive;
+    if (!alive) return 0;
+    if (a == 1) return y[i] + 1 < T.grid;
+    if (a == 2) return y[i] - 1 >= 0;
+    if (a == 3) return x[i] + 1 < T.grid;
+    if (a == 4) return x[i] - 1 >= 0;
+    const int j = a - MLG_ACT_BASE;
+    if (j < 0 || j >= T.U) return 0;
+    if (hp[j] <= 0) return 0;
+    if (env_dist2(x, y, i, j) > atk_range2(T.melee[i])) return 0;
+    if (T.role[i] == 1) return j != i && T.team[j] == T.team[i] && hp[j] < role_maxhp(T.role[j]);
+    return T.team[j] != T.team[i];
+}
+
+__device__ __forceinline__ int env_move_toward(const int* x, const int* y, int i, int j) {
+    const int dx = x[j] - x[i], dy = y[j] - y[i];
+    const int adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+    if (adx >= ady && dx != 0) return dx > 0 ? 3 : 4;
+    if (dy != 0) return dy > 0 ? 1 : 2;
+    return 0;
+}
+
+// Scripted "basic" AI (spec §3.3), decided on the pre-step state.
+__device__ int env_ai_action(const EnvTables& T, const int* x, const int* y, const int* hp, int i) {
+    if (hp[i] <= 0) return 0;
+    int best = -1;
+    for (int j = 0; j < T.U; ++j)
+        if (env_avail_one(T, x, y, hp, i, MLG_ACT_BASE + j) && (best < 0 || hp[j] < hp[best])) best = j;
+    if (best >= 0) return MLG_ACT_BASE + best;
+    if (T.role[i] == 1) {
+        int near = -1, nd = 0;
+        for (int j = 0; j < T.U; ++j) {
+            if (j == i || hp[j] <= 0 || T.team[j] != T.team[i]) continue;
+            const int d = env_dist2(x, y, i, j);
+            if (near < 0 || d < nd) { near = j; nd = d; }
+        }
+        if (near >= 0) return nd > 2 ? env_move_toward(x, y, i, near) : 0;
+    }
+    int near = -1, nd = 0;
+    for (int j = 0; j < T.U; ++j) {
+        if (hp[j] <= 0 || T.team[j] == T.team[i]) continue;
+        const int d = env_dist2(x, y, i, j);
+        if (near < 0 || d < nd) { near = j; nd = d; }
+    }
+    return near >= 0 ? env_move_toward(x, y, i, near) : 0;
+}
+
+__device__ __forceinline__ void env_spawn_unit(const EnvTables& T, uint64_t key, uint32_t episode, int u, int team_first,
+                                               int team_size, int* x, int* y, int* hp) {
+    const int G = T.grid, tm = T.team[u];
+    hp[u] = role_maxhp(T.role[u]);
+    if (T.stochastic) {
+        const uint64_t r = mlg_rng(key, mlg_ctr(episode, 0, MLG_PURPOSE_SPAWN, (uint32_t)u));
+        const int col = (int)(r % 4u);
+        x[u] = tm == 0 ? col : G - 1 - col;
+        y[u] = (int)((r >> 8) % (uint64_t)G);
+    } else {
+        const int k = u - team_first;
+        x[u] = tm == 0 ? 1 : G - 2;
+        y[u] = (k * G) / team_size + (G / team_size) / 2;
+    }
+}
+
+// Obs features of unit j seen by unit i (spec §3.5): writes 8 floats.
+__device__ __forceinline__ void env_obs_feat(const EnvTables& T, const int* x, const int* y, const int* hp, int i, int j,
+                                             float inv_p, float* o) {
+    if (hp[i] <= 0 || hp[j] <= 0 || env_dist2(x, y, i, j) > MLG_SIGHT2) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) o[f] = 0.0f;
+        return;
+    }
+    o[0] = 1.0f;
+    o[1] = (float)(x[j] - x[i]) * inv_p;
+    o[2] = (float)(y[j] - y[i]) * inv_p;
+    o[3] = (float)hp[j] * inv_maxhp(T.role[j]);
+    o[4] = (float)env_avail_one(T, x, y, hp, i, MLG_ACT_BASE + j);
+    o[5] = (float)(T.team[j] == T.team[i]);
+    o[6] = (float)T.role[j] * 0.5f;
+    o[7] = (float)T.melee[j];
+}
+
+__device__ __forceinline__ void env_state_feat(const EnvTables& T, const int* x, const int* y, const int* hp, int j,
+                                               float inv_p, float* o) {
+    o[0] = (float)(hp[j] > 0);
+    o[1] = (float)x[j] * inv_p;
+    o[2] = (float)y[j] * inv_p;
+    o[3] = (float)hp[j] * inv_maxhp(T.role[j]);
+    o[4] = (float)T.team[j];
+    o[5] = (float)T.role[j] * 0.5f;
+}
+
+// Action actually executed by unit u: validated policy action or scripted AI action (spec §3.4).
+__device__ __forceinline__ int env_exec_action(const EnvTables& T, const int* x, const int* y, const int* hp, int u,
+                                               int64_t policy_action) {
+    if (T.agent[u]) {
+        const int a = (int)policy_action;
+        return (a >= 0 && a < MLG_ACT_BASE + T.U && env_avail_one(T, x, y, hp, u, a)) ? a : 0;
+    }
+    return env_ai_action(T, x, y, hp, u);
+}
+
+// New hp of unit j given all executed actions (spec §3.4, simultaneous resolution). hp = pre-step.
+__device__ __forceinline__ int env_resolve_hp(const EnvTables& T, const int* act, const int* hp, int j) {
+    if (hp[j] <= 0) return hp[j];
+    int dmg = 0, heal = 0;
+    for (int i = 0; i < T.U; ++i) {
+        if (hp[i] <= 0 || act[i] != MLG_ACT_BASE + j) continue;
+        if (T.role[i] == 1) heal += role_power(1);
+        else dmg += role_power(T.role[i]);
+    }
+    int v = hp[j] - dmg + heal;
+    const int mx = role_maxhp(T.role[j]);
+    return v < 0 ? 0 : (v > mx ? mx : v);
+}
+
+__device__ __forceinline__ void env_apply_move(int a, int* xu, int* yu) {
+    if (a == 1) *yu += 1;
+    else if (a == 2) *yu -= 1;
+    else if (a == 3) *xu += 1;
+    else if (a == 4) *xu -= 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// argmax with torch.max semantics on CPU: NaN wins, ties -> lowest index.
+__device__ __forceinline__ bool amax_better(float v, int i, float bv, int bi) {
+    const bool vn = v != v, bn = bv != bv;
+    if (vn || bn) return vn && (!bn || i < bi);
+    return v > bv || (v == bv && i < bi);
+}

@@ -1,0 +1,54 @@
+"""EpisodeBatch -> MlgBatch (device pointers + sizes) for the C ABI."""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+
+KEYS = ("state", "obs", "actions", "avail_actions", "reward", "terminated", "actions_onehot", "filled")
+DTYPES = {"state": torch.float32, "obs": torch.float32, "actions": torch.int64, "avail_actions": torch.int32,
+          "reward": torch.float32, "terminated": torch.uint8, "actions_onehot": torch.float32, "filled": torch.int64}
+
+
+def _time_stride_ok(t: torch.Tensor, T1: int) -> bool:
+    """[B, T, *inner] view whose memory is [B][T1][*inner] with T <= T1 (a time slice starting at 0 is)."""
+    inner = 1
+    for s in t.shape[2:]:
+        inner *= s
+    want = [T1 * inner, inner]
+    exp = []
+    acc = 1
+    for d in range(t.dim() - 1, 1, -1):
+        exp.insert(0, acc)
+        acc *= t.shape[d]
+    return list(t.stride()[:2]) == want and all(
+        t.shape[d] == 1 or t.stride(d) == exp[d - 2] for d in range(2, t.dim()))
+
+
+def mlg_batch(batch, required=KEYS):
+    """Build an MlgBatch for `batch` (EpisodeBatch), making tensors contiguous when the layout is not
+    a plain [B][T1][...] array. Returns (MlgBatch, keepalive-list)."""
+    data = batch.data.transition_data
+    B = batch.batch_size
+    ref = data["obs"]
+    T1 = ref.stride(0) // max(1, ref.stride(1)) if ref.dim() > 1 and ref.stride(1) > 0 else ref.shape[1]
+    tensors = {}
+    for k in KEYS:
+        if k not in data:
+            if k in required:
+                raise KeyError(f"EpisodeBatch lacks {k!r} needed by the kernel")
+            tensors[k] = None
+            continue
+        t = data[k]
+        if t.dtype != DTYPES[k]:
+            raise TypeError(f"EpisodeBatch[{k!r}] has dtype {t.dtype}, kernel expects {DTYPES[k]}")
+        if not t.is_cuda:
+            raise _native.NativeError(f"EpisodeBatch[{k!r}] is on {t.device}; kernels need device tensors")
+        tensors[k] = t
+    if not all(t is None or _time_stride_ok(t, T1) for t in tensors.values()):
+        tensors = {k: (None if t is None else t.contiguous()) for k, t in tensors.items()}
+        T1 = batch.max_seq_length
+    p = lambda k: None if tensors[k] is None else tensors[k].data_ptr()  # noqa: E731
+    mb = _native.MlgBatch(p("state"), p("obs"), p("actions"), p("avail_actions"), p("reward"), p("terminated"),
+                          p("actions_onehot"), p("filled"), B, T1)
+    return mb, list(tensors.values())

@@ -1,0 +1,65 @@
+"""Circular episode replay buffer (API of src/marl/components/replay_buffers/replay_buffer.py:6-59).
+
+Lives on the training device (HBM) so sampling and training never cross PCIe.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .episode_batch import EpisodeBatch
+
+
+class ReplayBuffer(EpisodeBatch):
+    def __init__(self, scheme, groups, buffer_size: int, max_seq_length: int, preprocess=None, device="cpu"):
+        super().__init__(scheme, groups, buffer_size, max_seq_length, preprocess=preprocess, device=device)
+        self.buffer_size = buffer_size
+        self.buffer_index = 0
+        self.episodes_in_buffer = 0
+
+    def insert_episode_batch(self, ep_batch: EpisodeBatch):
+        room = self.buffer_size - self.buffer_index
+        if ep_batch.batch_size > room:
+            # split at the wrap point and insert both halves (replay_buffer.py:37-41)
+            self.insert_episode_batch(ep_batch[0:room, :])
+            self.insert_episode_batch(ep_batch[room:, :])
+            return
+        dst = slice(self.buffer_index, self.buffer_index + ep_batch.batch_size)
+        self._copy_in(ep_batch, dst)
+        self.buffer_index += ep_batch.batch_size
+        self.episodes_in_buffer = max(self.episodes_in_buffer, self.buffer_index)
+        self.buffer_index %= self.buffer_size
+        assert self.buffer_index < self.buffer_size
+
+    def _copy_in(self, ep_batch: EpisodeBatch, dst: slice):
+        """Same result as update(..., mark_filled=False) of every key: the preprocessed keys that the
+        source already carries are copied rather than recomputed (their recomputed value is overwritten
+        by the copy in the reference as well)."""
+        t = slice(0, ep_batch.max_seq_length)
+        src = ep_batch.data.transition_data
+        derived = {v[0] for v in self.preprocess.values()}
+        for key, value in src.items():
+            if key not in self.data.transition_data:
+                raise KeyError(f"{key} not found in transition or episode data")
+            if key in self.preprocess and self.preprocess[key][0] in src:
+                self.data.transition_data[key][dst, t] = value.to(self.data.transition_data[key].dtype)
+                continue
+            if key in derived or key not in self.preprocess:
+                self.data.transition_data[key][dst, t] = value.to(self.data.transition_data[key].dtype)
+            else:
+                self.update({key: value}, dst, t, mark_filled=False)
+        if ep_batch.data.episode_data:
+            self.update(ep_batch.data.episode_data, dst)
+
+    def can_sample(self, batch_size: int) -> bool:
+        return self.episodes_in_buffer >= batch_size
+
+    def sample(self, batch_size: int) -> EpisodeBatch:
+        assert self.can_sample(batch_size)
+        if self.episodes_in_buffer == batch_size:
+            return self[:batch_size]
+        ep_ids = np.random.choice(self.episodes_in_buffer, batch_size, replace=False)
+        return self[ep_ids]
+
+    def __repr__(self):
+        return (f"ReplayBuffer. {self.episodes_in_buffer}/{self.buffer_size} episodes. "
+                f"Keys:{self.scheme.keys()} Groups:{self.groups.keys()}")

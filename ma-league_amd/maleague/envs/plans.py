@@ -1,0 +1,37 @@
+"""Built-in match build plans, keyed like the reference's src/config/teams/<name>.json.
+
+A plan is two teams [scripted AI team, policy team]; each unit is (role, attack type). Compact codes:
+role T=TANK H=HEALER A=ADC; attack R=RANGED M=MELEE. A user's own config/teams/*.json files (the
+reference format with {"__enum__": "RoleTypes.X"} fields) are read directly by load_match_build_plan
+when a config directory is given; these built-ins make the package self-contained.
+"""
+from __future__ import annotations
+
+_ROLE = {"T": "TANK", "H": "HEALER", "A": "ADC"}
+_ATK = {"R": "RANGED", "M": "MELEE"}
+
+_COMPOSITIONS = {
+    "small": "TR TR TR",
+    "medium": "TR TR TR TR TR",
+    "medium_1h_4t": "TR TR HR TR TR",
+    "medium_1h_4a": "AR AR HR AR AR",
+    "medium_1h_2t_2a": "TR TR HR AR AR",
+    "medium_1h_2t_2a_melee": "TM TM HM AM AM",
+    "large": " ".join(["TR"] * 25),
+}
+
+
+def team_from_codes(codes: str, is_scripted: bool) -> dict:
+    units = [{"role": {"__enum__": f"RoleTypes.{_ROLE[c[0]]}"},
+              "attack_type": {"__enum__": f"UnitAttackTypes.{_ATK[c[1]]}"}} for c in codes.split()]
+    return {"is_scripted": is_scripted, "units": units}
+
+
+def builtin_plan(name: str, self_play: bool = False):
+    """Team plan list for a built-in name; self_play makes both teams policy-controlled."""
+    codes = _COMPOSITIONS[name]
+    return [team_from_codes(codes, not self_play), team_from_codes(codes, False)]
+
+
+def available() -> list:
+    return sorted(_COMPOSITIONS)

@@ -1,0 +1,95 @@
+"""DRQN agent: fc1 -> ReLU -> GRUCell -> fc2 (API + state_dict keys of src/marl/modules/agents/drqn_agent.py:7-35).
+
+Parameters are ordinary nn.Linear / nn.GRUCell tensors (so ``{name}agent.th`` checkpoints interoperate with
+the reference); the forward pass runs in the gfx950 kernel (mlg_agent_forward) from a packed copy of the
+weights that is refreshed whenever the parameters change.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ... import _native
+
+
+class AgentNetwork(nn.Module):
+    def __init__(self, input_shape, args):
+        super().__init__()
+        self.args = args
+        self.input_shape = input_shape
+        self.trained_steps = 0
+
+    def init_hidden(self):
+        raise NotImplementedError()
+
+    def forward(self, inputs, hidden_state):
+        raise NotImplementedError()
+
+    def count_parameters(self):
+        return sum(p.numel() for p in self.parameters() if p.requires_grad)
+
+
+class DRQNAgentNetwork(AgentNetwork):
+    def __init__(self, input_shape, args):
+        super().__init__(input_shape, args)
+        dev = getattr(args, "device", "cpu")
+        self.fc1 = nn.Linear(input_shape, args.rnn_hidden_dim, device=dev)
+        self.gru = nn.GRUCell(args.rnn_hidden_dim, args.rnn_hidden_dim, device=dev)
+        self.fc2 = nn.Linear(args.rnn_hidden_dim, args.n_actions, device=dev)
+        self._packed = None
+        self._packed_key = None
+        self._dirty = 0
+
+    # ---- kernel plumbing --------------------------------------------------------------------
+    def dims(self) -> _native.MlgAgentDims:
+        a = self.args
+        return _native.MlgAgentDims(d_obs=self.input_shape - (a.n_actions if a.obs_last_action else 0)
+                                    - (a.n_agents if a.obs_agent_id else 0),
+                                    n_actions=a.n_actions, n_agents=a.n_agents, hidden=a.rnn_hidden_dim,
+                                    d_in=self.input_shape, obs_last_action=int(bool(a.obs_last_action)),
+                                    obs_agent_id=int(bool(a.obs_agent_id)))
+
+    def mark_dirty(self):
+        """Call after parameters were modified outside torch (e.g. by the fused optimizer kernel)."""
+        self._dirty += 1
+
+    def packed(self) -> torch.Tensor:
+        """Packed weight block (agent_device.h layout); rebuilt when any parameter changed."""
+        params = [self.fc1.weight, self.fc1.bias, self.gru.weight_ih, self.gru.bias_ih, self.gru.weight_hh,
+                  self.gru.bias_hh, self.fc2.weight, self.fc2.bias]
+        key = (self._dirty,) + tuple((p.data_ptr(), p._version) for p in params)
+        if self._packed is None or key != self._packed_key:
+            d = self.dims()
+            n = _native.load().mlg_packed_agent_size(_native.byref(d))
+            if n < 0:
+                raise _native.NativeError(_native.load().mlg_last_error().decode())
+            dev = self.fc1.weight.device
+            if self._packed is None or self._packed.numel() != n or self._packed.device != dev:
+                self._packed = torch.empty(n, dtype=torch.float32, device=dev)
+            with torch.no_grad():
+                cp = [p.detach().float().contiguous() for p in params]
+            cparams = _native.MlgAgentParams(*[_native.ptr(p) for p in cp])
+            _native.call("mlg_pack_agent", _native.byref(d), _native.byref(cparams), _native.ptr(self._packed),
+                         _native.stream_ptr())
+            self._packed_key = key
+        return self._packed
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self.mark_dirty()
+
+    # ---- reference API -------------------------------------------------------------------------
+    def init_hidden(self):
+        return self.fc1.weight.new(1, self.args.rnn_hidden_dim).zero_()
+
+    def forward(self, inputs, hidden_state):
+        H = self.args.rnn_hidden_dim
+        x = inputs.float().contiguous()
+        h_in = hidden_state.reshape(-1, H).float().contiguous()
+        R = x.shape[0]
+        q = torch.empty(R, self.args.n_actions, device=x.device)
+        h_out = torch.empty(R, H, device=x.device)
+        d = self.dims()
+        _native.call("mlg_agent_forward", _native.byref(d), _native.ptr(self.packed()), _native.ptr(x),
+                     _native.ptr(h_in), _native.ptr(q), _native.ptr(h_out), R, _native.stream_ptr())
+        return q, h_out

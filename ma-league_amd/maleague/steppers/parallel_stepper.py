@@ -1,0 +1,149 @@
+"""Batched rollout of B envs (API of src/steppers/parallel_stepper.py:14-220).
+
+The reference forks one EnvWorker process per env and exchanges pickled dicts over Queues every step
+(env_worker_process.py:27-71); here one launch of the fused gfx950 kernel (mlg_rollout) runs a whole
+episode of all B envs: env step, observation, masks, the DRQN agent step and epsilon-greedy
+selection, writing the EpisodeBatch tensors in HBM directly. The host reads back one small per-env
+summary (episode length, return, won/draw) for t_env and the logger.
+"""
+from __future__ import annotations
+
+from functools import partial
+
+import torch
+
+from .. import _native
+from ..components.batch_view import mlg_batch
+from ..components.episode_batch import EpisodeBatch
+from ..custom_logging import Collectibles, Originator
+from ..envs.teams_env import TeamsEnvSpec, VecEnvState
+from ..exceptions import MultiAgentControllerNotInitialized
+
+
+class EnvStepper:
+    def __init__(self, args, logger, log_start_t=0):
+        self.args = args
+        self.logger = logger
+        self.batch_size = None
+        self.t_env = 0
+        self.is_initalized = False  # [sic] reference attribute name (ma_experiment.py:124)
+        self.log_start_t = log_start_t or 0
+
+    @property
+    def log_t(self):
+        return self.log_start_t + self.t_env
+
+
+class ParallelStepper(EnvStepper):
+    def __init__(self, args, logger, log_start_t=0):
+        super().__init__(args, logger, log_start_t)
+        self.batch_size = args.batch_size_run
+        self.device = torch.device(args.device)
+        env_args = dict(args.env_args)
+        env_args.setdefault("seed", getattr(args, "seed", 0))
+        self.spec = TeamsEnvSpec.from_env_args(env_args, getattr(args, "config_dir", None))
+        self.policy_team_id = self.spec.policy_team
+        self.env_info = self.spec.env_info()
+        self.episode_limit = self.env_info["episode_limit"]
+        self._cspec = self.spec.to_c()
+        self.envs = VecEnvState(self.spec, self.batch_size, self.device)
+        B = self.batch_size
+        # one int32 buffer for the per-run summary -> one D2H copy per run
+        self._info = torch.zeros(5 * B, dtype=torch.int32, device=self.device)
+        self.t = 0
+        self.env_steps_this_run = 0
+        self.new_batch_fn = None
+        self.home_mac = None
+        self.home_batch = None
+        self.last_run = None
+
+    def initialize(self, scheme, groups, preprocess, home_mac, away_mac=None):
+        if away_mac is not None:
+            raise NotImplementedError("self-play (away MAC) rollout is a next-round item (SURVEY §8f)")
+        self.new_batch_fn = partial(EpisodeBatch, scheme, groups, self.batch_size, self.episode_limit + 1,
+                                    preprocess=preprocess, device=self.device)
+        self.home_mac = home_mac
+        self.is_initalized = True
+
+    def get_env_info(self):
+        return self.env_info
+
+    def save_replay(self):
+        pass
+
+    def close_env(self):
+        pass
+
+    def reset(self):
+        self.home_batch = self.new_batch_fn()
+        self.t = 0
+        self.env_steps_this_run = 0
+
+    def _launch(self, batch: EpisodeBatch, epsilon: float, test_mode: bool):
+        B = self.batch_size
+        info = self._info
+        run_info = _native.MlgRunInfo(info[0:B].data_ptr(), info[4 * B:5 * B].data_ptr(),
+                                      info[B:3 * B].data_ptr(), info[3 * B:4 * B].data_ptr())
+        mb, keep = mlg_batch(batch)
+        agent = self.home_mac.agent
+        d = agent.dims()
+        st = self.envs.to_c()
+        _native.call("mlg_rollout", _native.byref(self._cspec), _native.byref(st), _native.byref(d),
+                     _native.ptr(agent.packed()), _native.byref(mb), _native.byref(run_info), float(epsilon),
+                     int(bool(test_mode)), _native.stream_ptr(self.device))
+        del keep
+
+    def run(self, test_mode=False):
+        if self.home_mac is None:
+            raise MultiAgentControllerNotInitialized()
+        self.reset()
+        self.logger.test_mode = test_mode
+        self.home_mac.init_hidden(batch_size=self.batch_size)
+        sel = self.home_mac.action_selector
+        sel.epsilon = sel.schedule.eval(self.t_env)
+        eps = 0.0 if test_mode else float(sel.epsilon)
+        if test_mode:
+            sel.epsilon = 0.0
+        self._launch(self.home_batch, eps, test_mode)
+        B = self.batch_size
+        host = self._info.cpu()
+        ep_len = host[0:B]
+        won = host[B:3 * B].view(B, 2)
+        draw = host[3 * B:4 * B]
+        ret = host[4 * B:5 * B].view(torch.float32)
+        self.t = int(ep_len.max())
+        if not test_mode:
+            self.env_steps_this_run = int(ep_len.sum())
+            self.t_env += self.env_steps_this_run
+        # env_infos in order of termination (parallel_stepper.py:124,183-184): by episode length, then env index
+        order = sorted(range(B), key=lambda i: (int(ep_len[i]), i))
+        won_l, draw_l = won.tolist(), draw.tolist()
+        env_infos = [{"battle_won": [bool(won_l[i][0]), bool(won_l[i][1])], "draw": bool(draw_l[i])} for i in order]
+        self.last_run = {"ep_len": ep_len, "returns": ret}
+        self.logger.collect(Collectibles.RETURN, ret.tolist(), origin=Originator.HOME, parallel=True)
+        self.logger.collect(Collectibles.WON, [e["battle_won"][0] for e in env_infos], origin=Originator.HOME,
+                            parallel=True)
+        self.logger.collect(Collectibles.WON, [e["battle_won"][1] for e in env_infos], origin=Originator.AWAY,
+                            parallel=True)
+        self.logger.collect(Collectibles.DRAW, [e["draw"] for e in env_infos], parallel=True)
+        self.logger.collect(Collectibles.STEPS, self.t, parallel=True)
+        self.logger.log(self.t_env)
+        return self.home_batch, env_infos
+
+
+class EpisodeStepper(ParallelStepper):
+    """Single-env stepper (src/steppers/episode_stepper.py:16-186): same kernel with B = 1; returns the
+    final env_info dict instead of a list."""
+
+    def __init__(self, args, logger, log_start_t=0):
+        assert args.batch_size_run == 1
+        super().__init__(args, logger, log_start_t)
+
+    @property
+    def epsilon(self):
+        return getattr(self.home_mac.action_selector, "epsilon", None)
+
+    def run(self, test_mode=False):
+        batch, infos = super().run(test_mode)
+        self.logger.log_stat("home_epsilon", self.epsilon, self.log_t)
+        return batch, infos[-1]
