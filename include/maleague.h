@@ -136,6 +136,36 @@ typedef struct {
 int mlg_qmix_forward(const MlgQMixParams *p, const float *agent_qs /*[R][N]*/, const float *states /*[R][S]*/,
                      float *q_tot /*[R]*/, int32_t R, void *stream);
 
+/* ---- QLearner.train (q_learner.py:34-131) as one fused device pipeline --------------------------
+ * Flat parameter vectors follow the nn.Module named_parameters() order:
+ *   agent: fc1.weight [H][d_in], fc1.bias [H], gru.weight_ih [3H][H], gru.weight_hh [3H][H],
+ *          gru.bias_ih [3H], gru.bias_hh [3H], fc2.weight [A][H], fc2.bias [A]
+ *   qmix (hypernet_layers 2): hyper_w_1.{0.weight [HE][S], 0.bias, 2.weight [N*E][HE], 2.bias},
+ *          hyper_w_final.{0.weight [HE][S], 0.bias, 2.weight [E][HE], 2.bias}, hyper_b_1.{weight [E][S], bias},
+ *          V.{0.weight [E][S], 0.bias, 2.weight [1][E], 2.bias}
+ * params/grads/square_avg = [agent | mixer]; target_params likewise (the target networks). */
+typedef struct {
+    int32_t B, T, N, A, d_obs, H, S, E, HE, hypernet_layers;
+    int32_t mixer; /* 0 none (IQL), 1 vdn, 2 qmix */
+    int32_t double_q, obs_last_action, obs_agent_id;
+    float gamma, lr, optim_alpha, optim_eps, grad_norm_clip;
+} MlgLearnerCfg;
+
+typedef struct {
+    MlgBatch batch;              /* the truncated sample: B episodes, T = max_t_filled timesteps (batch.T1 = stride) */
+    float *params;               /* [n_agent + n_mixer] updated in place (RMSprop) */
+    float *grads;                /* [n_agent + n_mixer] out: clipped gradients */
+    float *square_avg;           /* [n_agent + n_mixer] RMSprop state */
+    const float *target_params;  /* [n_agent + n_mixer] */
+    float *workspace;            /* mlg_qlearner_workspace_floats() floats */
+    float *stats;                /* [8] out: loss, grad_norm, td_error_abs, q_taken_mean, target_mean,
+                                    mask_sum, count_nonzero(mask), 0 */
+} MlgLearnerBufs;
+
+int64_t mlg_qlearner_param_counts(const MlgLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);
+int64_t mlg_qlearner_workspace_floats(const MlgLearnerCfg *c);
+int mlg_qlearner_train(const MlgLearnerCfg *c, const MlgLearnerBufs *b, void *stream);
+
 const char *mlg_last_error(void);
 const char *mlg_version(void);
 

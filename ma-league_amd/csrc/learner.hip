@@ -1,0 +1,1060 @@
+// learner.hip -- QLearner.train (src/marl/learners/q_learner.py:34-131) as one device pipeline on gfx950.
+//
+//   pack        online/target agent + mixer weights -> kernel layouts (+ transposes for backward)
+//   mask_sum    mask = filled[:, :-1] * (1 - terminated shifted) and its sum                (:36-42, :89-98)
+//   agent_fwd   online + target BPTT unroll, one workgroup per 16 sequence rows, wave w owns
+//               hidden chunk w; saves inputs/activations/gates for backward                  (:44-65)
+//   mix_td      per (b, t) row: gather chosen Q, double-Q target, QMixer fwd (online+target),
+//               TD error, masked MSE partials, QMixer backward -> dQ and mixer deltas         (:55-98)
+//   agent_bwd   reverse-time GRU backward (dh carried in registers, dGH exchanged in LDS)    (:103)
+//   wgrad       every weight/bias gradient as sum_rows delta^T x, split over row chunks
+//               (deterministic slab reduction; MFMA with the row index as K)
+//   finish      loss/stat reduction, clip_grad_norm_(10), RMSprop step                       (:104-105, learner.py:25-31)
+// Tensors saved for backward are t-major: [T][R][F] with R = B * N agent rows (r = b * N + n).
+#include "agent_device.h"
+#include "mlg_host.h"
+
+namespace {
+
+constexpr int WCH = 256;      // rows per wgrad chunk
+constexpr int MAX_JOBS = 16;
+
+// ---- canonical flat parameter offsets (nn.Module named_parameters order) ------------------------
+struct AgentOffs {
+    int64_t fc1w, fc1b, wih, whh, bih, bhh, fc2w, fc2b, total;
+};
+__host__ __device__ inline AgentOffs agent_offs(int H, int d_in, int A) {
+    AgentOffs o;
+    int64_t p = 0;
+    o.fc1w = p; p += (int64_t)H * d_in;
+    o.fc1b = p; p += H;
+    o.wih = p; p += (int64_t)3 * H * H;
+    o.whh = p; p += (int64_t)3 * H * H;
+    o.bih = p; p += 3 * H;
+    o.bhh = p; p += 3 * H;
+    o.fc2w = p; p += (int64_t)A * H;
+    o.fc2b = p; p += A;
+    o.total = p;
+    return o;
+}
+
+struct MixOffs {
+    int64_t w1_0w, w1_0b, w1_2w, w1_2b, wf_0w, wf_0b, wf_2w, wf_2b, b1w, b1b, v0w, v0b, v2w, v2b, total;
+};
+__host__ __device__ inline MixOffs mix_offs(int N, int S, int E, int HE) {
+    MixOffs o;
+    int64_t p = 0;
+    o.w1_0w = p; p += (int64_t)HE * S;
+    o.w1_0b = p; p += HE;
+    o.w1_2w = p; p += (int64_t)N * E * HE;
+    o.w1_2b = p; p += (int64_t)N * E;
+    o.wf_0w = p; p += (int64_t)HE * S;
+    o.wf_0b = p; p += HE;
+    o.wf_2w = p; p += (int64_t)E * HE;
+    o.wf_2b = p; p += E;
+    o.b1w = p; p += (int64_t)E * S;
+    o.b1b = p; p += E;
+    o.v0w = p; p += (int64_t)E * S;
+    o.v0b = p; p += E;
+    o.v2w = p; p += E;
+    o.v2b = p; p += 1;
+    o.total = p;
+    return o;
+}
+
+// ---- packed mixer block: m1 = [w1h | wfh | b1 | vh] rows over padded state, transposes, padded V.2 ----
+struct MixPack {
+    int L1, Sp, NE;
+    int64_t m1, mb1, a2T, f2T, v2p, bv2p, total;
+};
+__host__ __device__ inline MixPack mix_pack(int N, int S, int E, int HE) {
+    MixPack m;
+    m.L1 = 2 * HE + 2 * E;
+    m.Sp = (S + 15) / 16 * 16;
+    m.NE = N * E;
+    int64_t p = 0;
+    m.m1 = p; p += (int64_t)m.L1 * m.Sp;
+    m.mb1 = p; p += m.L1;
+    m.a2T = p; p += (int64_t)HE * m.NE;
+    m.f2T = p; p += (int64_t)HE * E;
+    m.v2p = p; p += (int64_t)16 * E;
+    m.bv2p = p; p += 16;
+    m.total = mlg_align4(p);
+    return m;
+}
+
+struct MixPtrs {
+    const float *m1, *mb1, *a2, *ba2, *a2T, *f2, *bf2, *f2T, *v2p, *bv2p;
+};
+
+// ---- device config ---------------------------------------------------------------------------------
+struct LCfg {
+    int B, T, T1, N, A, Ap, d_obs, d_in, H, S, E, HE, mixer, double_q, last_action, agent_id;
+    int R, RM;
+    float gamma;
+};
+
+// ---- workspace layout --------------------------------------------------------------------------------
+struct WsLayout {
+    int64_t p_on, p_tg, wihT, whhT, mix_on, mix_tg;
+    int64_t in, x, hs, gr, gz, gn, ghn, mac, tmac, dq, d2, dgi, dgh, da;
+    int64_t srow, l1act, d1, da2, df2, dv2;
+    int64_t part, msum, slab, total;
+    int n_mix_tiles, n_tasks;
+};
+
+__host__ __device__ inline int64_t a4(int64_t v) { return mlg_align4(v); }
+
+// ================================================================================================
+// packing
+__global__ void transpose_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols) {
+    // dst[c][r] = src[r][c]
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)rows * cols) return;
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    dst[(int64_t)c * rows + r] = src[i];
+}
+
+__global__ void pack_mixer_kernel(MixPack mp, MixOffs mo, const float* __restrict__ P, float* __restrict__ out, int N,
+                                  int S, int E, int HE) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= mp.total) return;
+    float v = 0.f;
+    if (i < mp.mb1) {
+        const int r = (int)(i / mp.Sp), c = (int)(i % mp.Sp);
+        if (c < S) {
+            if (r < HE) v = P[mo.w1_0w + (int64_t)r * S + c];
+            else if (r < 2 * HE) v = P[mo.wf_0w + (int64_t)(r - HE) * S + c];
+            else if (r < 2 * HE + E) v = P[mo.b1w + (int64_t)(r - 2 * HE) * S + c];
+            else v = P[mo.v0w + (int64_t)(r - 2 * HE - E) * S + c];
+        }
+    } else if (i < mp.a2T) {
+        const int r = (int)(i - mp.mb1);
+        if (r < HE) v = P[mo.w1_0b + r];
+        else if (r < 2 * HE) v = P[mo.wf_0b + r - HE];
+        else if (r < 2 * HE + E) v = P[mo.b1b + r - 2 * HE];
+        else v = P[mo.v0b + r - 2 * HE - E];
+    } else if (i < mp.f2T) {  // a2T [HE][NE] = w1_2w^T
+        const int64_t k = i - mp.a2T;
+        const int r = (int)(k / mp.NE), c = (int)(k % mp.NE);
+        v = P[mo.w1_2w + (int64_t)c * HE + r];
+    } else if (i < mp.v2p) {  // f2T [HE][E]
+        const int64_t k = i - mp.f2T;
+        const int r = (int)(k / E), c = (int)(k % E);
+        v = P[mo.wf_2w + (int64_t)c * HE + r];
+    } else if (i < mp.bv2p) {  // v2p [16][E], row 0 = V.2.weight
+        const int64_t k = i - mp.v2p;
+        if (k < E) v = P[mo.v2w + k];
+    } else if (i < mp.bv2p + 16) {
+        if (i == mp.bv2p) v = P[mo.v2b];
+    }
+    out[i] = v;
+}
+
+// ================================================================================================
+// mask: mask[b][t] = filled[b][t] * (t > 0 ? 1 - terminated[b][t-1] : 1), t < T-1
+__device__ __forceinline__ float mask_at(const MlgBatch& bt, int b, int t) {
+    const int64_t base = (int64_t)b * bt.T1;
+    float m = (float)bt.filled[base + t];
+    if (t > 0) m *= 1.f - (float)bt.terminated[base + t - 1];
+    return m;
+}
+
+__global__ void mask_sum_kernel(MlgBatch bt, int B, int T, float* __restrict__ msum) {
+    __shared__ float red[1024];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < B * (T - 1); i += blockDim.x) s += mask_at(bt, i / (T - 1), i % (T - 1));
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) msum[0] = red[0];
+}
+
+// ================================================================================================
+// 16-row x 16-feature tile product with the activation operand in LDS, row-major [16][lda]:
+// acc += W[m0 + col][kc*16 .. ] . act[row][kc*16 ..] over kchunks chunks.
+__device__ __forceinline__ floatx4 tile_mm_lds(const float* __restrict__ W, int64_t ldw, int m0, const float* act, int lda,
+                                               int kchunks, floatx4 acc, int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    const float* wrow = W + (int64_t)(m0 + col) * ldw + 4 * g;
+    const float* arow = act + col * lda + 4 * g;
+    for (int kc = 0; kc < kchunks; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), ld4(arow + kc * 16), acc);
+    return acc;
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+// ================================================================================================
+// forward unroll: blockIdx.x < ntiles -> online (saves), else target (q only)
+template <int H>
+__global__ void __launch_bounds__(512) agent_fwd_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ Pon,
+                                                        const float* __restrict__ Ptg, float* __restrict__ ws_in,
+                                                        float* __restrict__ ws_x, float* __restrict__ ws_hs,
+                                                        float* __restrict__ ws_gr, float* __restrict__ ws_gz,
+                                                        float* __restrict__ ws_gn, float* __restrict__ ws_ghn,
+                                                        float* __restrict__ mac, float* __restrict__ tmac) {
+    constexpr int HC = H / 16;
+    constexpr int LDA = H + 4;
+    __shared__ __attribute__((aligned(16))) float xs[16 * LDA];
+    __shared__ __attribute__((aligned(16))) float hs[2][16 * LDA];
+    const int ntiles = (c.R + 15) / 16;
+    const bool online = blockIdx.x < ntiles;
+    const int tile = online ? blockIdx.x : blockIdx.x - ntiles;
+    const float* P = online ? Pon : Ptg;
+    float* qout = online ? mac : tmac;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;  // wave w owns hidden chunk w
+    const int col = lane & 15, g = lane >> 4;
+    const int r = tile * 16 + col;
+    const bool valid = r < c.R;
+    const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
+    const int N = c.N, A = c.A, R = c.R;
+    for (int i = tid; i < 16 * LDA; i += blockDim.x) hs[0][i] = 0.f;
+    if (online && w == 0 && valid)
+        for (int k = 0; k < H; k += 4) *reinterpret_cast<floatx4*>(ws_hs + (int64_t)r * H + k) = floatx4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    int cur = 0;
+    for (int t = 0; t < c.T; ++t) {
+        const float* Pt = P;
+        asm volatile("" : "+s"(Pt));
+        const int64_t boff = ((int64_t)b * bt.T1 + t) * N + n;
+        // ---- fc1 chunk w ----
+        {
+            floatx4 acc = ld4(Pt + L.b1 + w * 16 + 4 * g);
+            if (valid) {
+                if (L.last_action && t > 0) {
+                    const float* oh = bt.actions_onehot + (boff - N) * A;
+                    for (int a = 0; a < A; ++a) {
+                        const float v = oh[a];
+                        if (v != 0.f) acc += v * ld4(Pt + L.w1a + (int64_t)a * H + w * 16 + 4 * g);
+                    }
+                }
+                if (L.agent_id) acc += ld4(Pt + L.w1n + (int64_t)n * H + w * 16 + 4 * g);
+            }
+            const float* orow = valid ? bt.obs + boff * c.d_obs : nullptr;
+            const float* wrow = Pt + L.w1o + (int64_t)(w * 16 + col) * L.Dob + 4 * g;
+            for (int kc = 0; kc < L.Dob / 16; ++kc)
+                acc = mfma_chunk(ld4(wrow + kc * 16), load_chunk(orow, kc * 16 + 4 * g, c.d_obs), acc);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = fmaxf(acc[q], 0.f);
+            *reinterpret_cast<floatx4*>(xs + col * LDA + w * 16 + 4 * g) = acc;
+            if (online && valid) *reinterpret_cast<floatx4*>(ws_x + ((int64_t)t * R + r) * H + w * 16 + 4 * g) = acc;
+        }
+        if (online) {  // dense input row for dW1 (basic_controller.py:80-92 layout)
+            for (int i = tid; i < 16 * c.d_in; i += blockDim.x) {
+                const int rr = tile * 16 + i / c.d_in, k = i % c.d_in;
+                if (rr >= R) continue;
+                const int bb = rr / N, nn = rr % N;
+                const int64_t bo = ((int64_t)bb * bt.T1 + t) * N + nn;
+                float v;
+                if (k < c.d_obs) v = bt.obs[bo * c.d_obs + k];
+                else if (L.last_action && k < c.d_obs + A) v = t > 0 ? bt.actions_onehot[(bo - N) * A + (k - c.d_obs)] : 0.f;
+                else v = (k - c.d_obs - (L.last_action ? A : 0)) == nn ? 1.f : 0.f;
+                ws_in[((int64_t)t * R + rr) * c.d_in + k] = v;
+            }
+        }
+        __syncthreads();
+        // ---- GRU chunk w ----
+        {
+            const float* hcur = hs[cur];
+            floatx4 ar = ld4(Pt + L.brz + w * 16 + 4 * g);
+            floatx4 az = ld4(Pt + L.brz + H + w * 16 + 4 * g);
+            floatx4 ain = ld4(Pt + L.bih + 2 * H + w * 16 + 4 * g);
+            floatx4 ahn = ld4(Pt + L.bhh + 2 * H + w * 16 + 4 * g);
+            ar = tile_mm_lds(Pt + L.wih, H, w * 16, xs, LDA, HC, ar, lane);
+            ar = tile_mm_lds(Pt + L.whh, H, w * 16, hcur, LDA, HC, ar, lane);
+            az = tile_mm_lds(Pt + L.wih, H, H + w * 16, xs, LDA, HC, az, lane);
+            az = tile_mm_lds(Pt + L.whh, H, H + w * 16, hcur, LDA, HC, az, lane);
+            ain = tile_mm_lds(Pt + L.wih, H, 2 * H + w * 16, xs, LDA, HC, ain, lane);
+            ahn = tile_mm_lds(Pt + L.whh, H, 2 * H + w * 16, hcur, LDA, HC, ahn, lane);
+            const floatx4 hp = ld4(hcur + col * LDA + w * 16 + 4 * g);
+            floatx4 rg, zg, ng, hn;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                rg[q] = sigm(ar[q]);
+                zg[q] = sigm(az[q]);
+                ng[q] = tanhf(ain[q] + rg[q] * ahn[q]);
+                hn[q] = ng[q] + zg[q] * (hp[q] - ng[q]);
+            }
+            *reinterpret_cast<floatx4*>(hs[cur ^ 1] + col * LDA + w * 16 + 4 * g) = hn;
+            if (online && valid) {
+                const int64_t o = ((int64_t)t * R + r) * H + w * 16 + 4 * g;
+                *reinterpret_cast<floatx4*>(ws_gr + o) = rg;
+                *reinterpret_cast<floatx4*>(ws_gz + o) = zg;
+                *reinterpret_cast<floatx4*>(ws_gn + o) = ng;
+                *reinterpret_cast<floatx4*>(ws_ghn + o) = ahn;
+                *reinterpret_cast<floatx4*>(ws_hs + o + (int64_t)R * H) = hn;  // HS[t + 1]
+            }
+        }
+        __syncthreads();
+        // ---- fc2: action tiles w, w + HC, ... ----
+        for (int at = w; at < L.Ap / 16; at += HC) {
+            floatx4 q = ld4(Pt + L.b2 + at * 16 + 4 * g);
+            q = tile_mm_lds(Pt + L.w2, H, at * 16, hs[cur ^ 1], LDA, HC, q, lane);
+            if (valid) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int a = at * 16 + 4 * g + k;
+                    if (a < A) qout[((int64_t)t * R + r) * A + a] = q[k];
+                }
+            }
+        }
+        cur ^= 1;
+    }
+}
+
+// ================================================================================================
+// QMixer on one 16-row tile (rows on lanes).  l1 = [w1h | wfh | b1 | vh] (post ReLU except b1).
+template <int HE, int E>
+struct Mixer {
+    static constexpr int T1H = HE / 16, TE = E / 16, L1T = (2 * HE + 2 * E) / 16;
+    static constexpr int OW1 = 0, OWF = T1H, OB1 = 2 * T1H, OVH = 2 * T1H + TE;
+
+    // first layer + ReLUs; s = this lane's state row (nullptr -> zeros)
+    __device__ static void layer1(const MixPtrs& M, const MixPack& mp, int S, const float* s, floatx4 (&l1)[L1T], int lane) {
+        const int col = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int mt = 0; mt < L1T; ++mt) l1[mt] = ld4(M.mb1 + mt * 16 + 4 * g);
+        for (int kc = 0; kc < mp.Sp / 16; ++kc) {
+            const floatx4 sv = load_chunk(s, kc * 16 + 4 * g, S);
+#pragma unroll
+            for (int mt = 0; mt < L1T; ++mt)
+                l1[mt] = mfma_chunk(ld4(M.m1 + (int64_t)(mt * 16 + col) * mp.Sp + kc * 16 + 4 * g), sv, l1[mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < L1T; ++mt) {
+            if (mt >= OB1 && mt < OVH) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) l1[mt][q] = fmaxf(l1[mt][q], 0.f);
+        }
+    }
+
+    // pre-abs hyper_w_1 output for agent n, chunk cc (features n*E + cc*16 ..)
+    __device__ static floatx4 w1pre(const MixPtrs& M, int n, int cc, const floatx4 (&l1)[L1T], int lane) {
+        const int col = lane & 15, g = lane >> 4;
+        floatx4 acc = ld4(M.ba2 + n * E + cc * 16 + 4 * g);
+        const float* wrow = M.a2 + (int64_t)(n * E + cc * 16 + col) * HE + 4 * g;
+#pragma unroll
+        for (int kc = 0; kc < T1H; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), l1[OW1 + kc], acc);
+        return acc;
+    }
+
+    __device__ static floatx4 wfpre(const MixPtrs& M, int cc, const floatx4 (&l1)[L1T], int lane) {
+        const int col = lane & 15, g = lane >> 4;
+        floatx4 acc = ld4(M.bf2 + cc * 16 + 4 * g);
+        const float* wrow = M.f2 + (int64_t)(cc * 16 + col) * HE + 4 * g;
+#pragma unroll
+        for (int kc = 0; kc < T1H; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), l1[OWF + kc], acc);
+        return acc;
+    }
+
+    __device__ static float vval(const MixPtrs& M, const floatx4 (&l1)[L1T], int lane) {
+        const int col = lane & 15, g = lane >> 4;
+        floatx4 acc = ld4(M.bv2p + 4 * g);
+        const float* wrow = M.v2p + (int64_t)col * E + 4 * g;
+#pragma unroll
+        for (int kc = 0; kc < TE; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), l1[OVH + kc], acc);
+        return __shfl(acc[0], col);  // feature 0 lives in lane group 0, reg 0
+    }
+
+    // forward: y per row (identical in the 4 lanes of a row). q(n) = this row's agent-n value.
+    __device__ static float forward(const MixPtrs& M, const MixPack& mp, int S, int N, const float* s, const float* qrow,
+                                    floatx4 (&l1)[L1T], floatx4 (&pre)[TE], floatx4 (&hid)[TE], floatx4 (&wfp)[TE], int lane) {
+        layer1(M, mp, S, s, l1, lane);
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) pre[cc] = l1[OB1 + cc];
+        for (int n = 0; n < N; ++n) {
+            const float qn = qrow[n];
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc) {
+                const floatx4 wp = w1pre(M, n, cc, l1, lane);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pre[cc][q] += qn * fabsf(wp[q]);
+            }
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) {
+            wfp[cc] = wfpre(M, cc, l1, lane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                hid[cc][q] = pre[cc][q] > 0.f ? pre[cc][q] : expm1f(pre[cc][q]);
+                part += hid[cc][q] * fabsf(wfp[cc][q]);
+            }
+        }
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        return part + vval(M, l1, lane);
+    }
+};
+
+__device__ __forceinline__ float row_sum16(float v) {  // sum over the 16 lanes of lane group 0
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    return v;
+}
+
+// chosen / target per-agent values of row (b, t) (q_learner.py:55, 68-75)
+__device__ __forceinline__ void gather_q(const LCfg& c, const MlgBatch& bt, const float* mac, const float* tmac, int b, int t,
+                                         float* cq, float* tq) {
+    const int N = c.N, A = c.A, R = c.R;
+    for (int n = 0; n < N; ++n) {
+        const int r = b * N + n;
+        const int a = (int)bt.actions[((int64_t)b * bt.T1 + t) * N + n];
+        cq[n] = mac[((int64_t)t * R + r) * A + a];
+        const int32_t* av = bt.avail + ((int64_t)b * bt.T1 + t + 1) * N * A + (int64_t)n * A;
+        const float* qn = mac + ((int64_t)(t + 1) * R + r) * A;
+        const float* tn = tmac + ((int64_t)(t + 1) * R + r) * A;
+        if (c.double_q) {
+            float bv = 0.f;
+            int bi = 0;
+            for (int k = 0; k < A; ++k) {
+                const float v = av[k] ? qn[k] : -9999999.f;
+                if (k == 0 || v > bv) { bv = v; bi = k; }
+            }
+            tq[n] = av[bi] ? tn[bi] : -9999999.f;
+        } else {
+            float bv = 0.f;
+            for (int k = 0; k < A; ++k) {
+                const float v = av[k] ? tn[k] : -9999999.f;
+                if (k == 0 || v > bv) bv = v;
+            }
+            tq[n] = bv;
+        }
+    }
+}
+
+constexpr int MAXN = 32;
+
+struct MixOut {
+    float *srow, *l1act, *d1, *da2, *df2, *dv2, *dq, *d2, *part;
+};
+
+template <int HE, int E>
+__global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs Mon, MixPtrs Mtg, MixPack mp,
+                                                    const float* __restrict__ mac, const float* __restrict__ tmac,
+                                                    const float* __restrict__ msum_p, MixOut o) {
+    using Mx = Mixer<HE, E>;
+    const int lane = threadIdx.x, col = lane & 15, g = lane >> 4;
+    const int rm = blockIdx.x * 16 + col;
+    const int Tm = c.T - 1;
+    const bool valid = rm < c.RM;
+    const int b = valid ? rm / Tm : 0, t = valid ? rm % Tm : 0;
+    const int N = c.N, S = c.S, L1 = 2 * HE + 2 * E, NE = N * E;
+    float cq[MAXN], tq[MAXN];
+    for (int n = 0; n < N; ++n) cq[n] = tq[n] = 0.f;
+    if (valid) gather_q(c, bt, mac, tmac, b, t, cq, tq);
+    const float m = valid ? mask_at(bt, b, t) : 0.f;
+    const float rwd = valid ? bt.reward[(int64_t)b * bt.T1 + t] : 0.f;
+    const float term = valid ? (float)bt.terminated[(int64_t)b * bt.T1 + t] : 0.f;
+    const float msum = msum_p[0];
+    const float* s0 = valid ? bt.state + ((int64_t)b * bt.T1 + t) * S : nullptr;
+    const float* s1 = valid ? bt.state + ((int64_t)b * bt.T1 + t + 1) * S : nullptr;
+    float qtot, tgt;
+    floatx4 l1[Mx::L1T], pre[Mx::TE], hid[Mx::TE], wfp[Mx::TE];
+    if (c.mixer == 2) {
+        {
+            floatx4 tl1[Mx::L1T], tpre[Mx::TE], thid[Mx::TE], twfp[Mx::TE];
+            tgt = Mx::forward(Mtg, mp, S, N, s1, tq, tl1, tpre, thid, twfp, lane);
+        }
+        qtot = Mx::forward(Mon, mp, S, N, s0, cq, l1, pre, hid, wfp, lane);
+    } else {  // VDN (vdn.py:9)
+        qtot = 0.f;
+        tgt = 0.f;
+        for (int n = 0; n < N; ++n) {
+            qtot += cq[n];
+            tgt += tq[n];
+        }
+    }
+    const float y = rwd + c.gamma * (1.f - term) * tgt;          // q_learner.py:86
+    const float mtd = (qtot - y) * m;                             // :89-95
+    const float dy = 2.f * mtd * m / msum;                        // d loss / d q_tot
+    // ---- loss / stat partials (one row per lane of group 0) ----
+    {
+        float p0 = g == 0 ? mtd * mtd : 0.f, p1 = g == 0 ? fabsf(mtd) : 0.f;
+        float p2 = g == 0 ? qtot * m : 0.f, p3 = g == 0 ? y * m : 0.f;
+        p0 = row_sum16(p0);
+        p1 = row_sum16(p1);
+        p2 = row_sum16(p2);
+        p3 = row_sum16(p3);
+        if (lane == 0) {
+            float* pp = o.part + (int64_t)blockIdx.x * 4;
+            pp[0] = p0;
+            pp[1] = p1;
+            pp[2] = p2;
+            pp[3] = p3;
+        }
+    }
+    float dq[MAXN];
+    if (c.mixer == 2) {
+        // ---- QMixer backward (autograd of qmix.py:41-59) ----
+        floatx4 dpre[Mx::TE], dwf[Mx::TE];
+#pragma unroll
+        for (int cc = 0; cc < Mx::TE; ++cc) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float dh = dy * fabsf(wfp[cc][q]);
+                const float sg = wfp[cc][q] > 0.f ? 1.f : (wfp[cc][q] < 0.f ? -1.f : 0.f);
+                dwf[cc][q] = dy * hid[cc][q] * sg;
+                dpre[cc][q] = pre[cc][q] > 0.f ? dh : dh * (hid[cc][q] + 1.f);
+            }
+        }
+        floatx4 dw1h[Mx::T1H];
+#pragma unroll
+        for (int mt = 0; mt < Mx::T1H; ++mt) dw1h[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < N; ++n) {
+            float part = 0.f;
+#pragma unroll
+            for (int cc = 0; cc < Mx::TE; ++cc) {
+                const floatx4 wp = Mx::w1pre(Mon, n, cc, l1, lane);
+                floatx4 dlt;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    part += fabsf(wp[q]) * dpre[cc][q];
+                    const float sg = wp[q] > 0.f ? 1.f : (wp[q] < 0.f ? -1.f : 0.f);
+                    dlt[q] = cq[n] * dpre[cc][q] * sg;
+                }
+                if (valid) *reinterpret_cast<floatx4*>(o.da2 + (int64_t)rm * NE + n * E + cc * 16 + 4 * g) = dlt;
+                // dw1h += W_a2^T[:, n*E + cc*16 ..] . dlt   (a2T is [HE][NE])
+#pragma unroll
+                for (int mt = 0; mt < Mx::T1H; ++mt)
+                    dw1h[mt] = mfma_chunk(ld4(Mon.a2T + (int64_t)(mt * 16 + col) * NE + n * E + cc * 16 + 4 * g), dlt, dw1h[mt]);
+            }
+            part += __shfl_xor(part, 16);
+            part += __shfl_xor(part, 32);
+            dq[n] = part;
+        }
+        // dwfh = W_f2^T . dwf -- MFMA needs every lane active, so it runs outside the store guard
+        floatx4 dwfh[Mx::T1H];
+#pragma unroll
+        for (int mt = 0; mt < Mx::T1H; ++mt) {
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int cc = 0; cc < Mx::TE; ++cc)
+                acc = mfma_chunk(ld4(Mon.f2T + (int64_t)(mt * 16 + col) * E + cc * 16 + 4 * g), dwf[cc], acc);
+            dwfh[mt] = acc;
+        }
+        if (valid) {
+            float* d1 = o.d1 + (int64_t)rm * L1;
+            float* la = o.l1act + (int64_t)rm * L1;
+#pragma unroll
+            for (int mt = 0; mt < Mx::T1H; ++mt) {  // w1h
+                floatx4 v;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = l1[Mx::OW1 + mt][q] > 0.f ? dw1h[mt][q] : 0.f;
+                *reinterpret_cast<floatx4*>(d1 + mt * 16 + 4 * g) = v;
+            }
+#pragma unroll
+            for (int mt = 0; mt < Mx::T1H; ++mt) {  // wfh
+                floatx4 acc = dwfh[mt];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = l1[Mx::OWF + mt][q] > 0.f ? acc[q] : 0.f;
+                *reinterpret_cast<floatx4*>(d1 + HE + mt * 16 + 4 * g) = acc;
+            }
+#pragma unroll
+            for (int cc = 0; cc < Mx::TE; ++cc) {  // b1, vh
+                *reinterpret_cast<floatx4*>(d1 + 2 * HE + cc * 16 + 4 * g) = dpre[cc];
+                const floatx4 wv = ld4(Mon.v2p + cc * 16 + 4 * g);
+                floatx4 v;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = l1[Mx::OVH + cc][q] > 0.f ? dy * wv[q] : 0.f;
+                *reinterpret_cast<floatx4*>(d1 + 2 * HE + E + cc * 16 + 4 * g) = v;
+                *reinterpret_cast<floatx4*>(o.df2 + (int64_t)rm * E + cc * 16 + 4 * g) = dwf[cc];
+            }
+#pragma unroll
+            for (int mt = 0; mt < Mx::L1T; ++mt) *reinterpret_cast<floatx4*>(la + mt * 16 + 4 * g) = l1[mt];
+            if (g == 0) {
+                o.dv2[rm] = dy;
+                for (int k = 0; k < S; ++k) o.srow[(int64_t)rm * S + k] = s0[k];
+            }
+        }
+    } else {
+        for (int n = 0; n < N; ++n) dq[n] = dy;
+    }
+    // ---- dQ per agent row (t-major) and its one-hot expansion for dW2 ----
+    if (valid && g == 0) {
+        for (int n = 0; n < N; ++n) {
+            const int r = b * N + n;
+            o.dq[(int64_t)t * c.R + r] = dq[n];
+            const int a = (int)bt.actions[((int64_t)b * bt.T1 + t) * N + n];
+            o.d2[((int64_t)t * c.R + r) * c.A + a] = dq[n];
+        }
+    }
+}
+
+// ================================================================================================
+// reverse-time GRU backward; wave w owns hidden chunk w (same ownership as agent_fwd_kernel)
+template <int H>
+__global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ P,
+                                                        const float* __restrict__ wihT, const float* __restrict__ whhT,
+                                                        const float* __restrict__ ws_x, const float* __restrict__ ws_hs,
+                                                        const float* __restrict__ ws_gr, const float* __restrict__ ws_gz,
+                                                        const float* __restrict__ ws_gn, const float* __restrict__ ws_ghn,
+                                                        const float* __restrict__ dqv, float* __restrict__ dgi,
+                                                        float* __restrict__ dgh, float* __restrict__ da) {
+    constexpr int LDG = 3 * H + 4;
+    __shared__ __attribute__((aligned(16))) float sgi[16 * LDG];
+    __shared__ __attribute__((aligned(16))) float sgh[16 * LDG];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int r = blockIdx.x * 16 + col;
+    const bool valid = r < c.R;
+    const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
+    const int R = c.R, N = c.N;
+    floatx4 dh = {0.f, 0.f, 0.f, 0.f};
+    const int f0 = w * 16 + 4 * g;  // this lane's 4 hidden features
+    for (int t = c.T - 1; t >= 0; --t) {
+        const int64_t o = ((int64_t)t * R + (valid ? r : 0)) * H + f0;
+        if (valid && t < c.T - 1) {
+            const float dq = dqv[(int64_t)t * R + r];
+            const int a = (int)bt.actions[((int64_t)b * bt.T1 + t) * N + n];
+            dh += dq * ld4(P + L.w2 + (int64_t)a * H + f0);
+        }
+        floatx4 rg = {0.f, 0.f, 0.f, 0.f}, zg = rg, ng = rg, ghn = rg, hp = rg;
+        if (valid) {
+            rg = ld4(ws_gr + o);
+            zg = ld4(ws_gz + o);
+            ng = ld4(ws_gn + o);
+            ghn = ld4(ws_ghn + o);
+            hp = ld4(ws_hs + o);  // HS[t] = h_{t-1}
+        }
+        floatx4 drp, dzp, dnp, dghn, dhd;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float dn = dh[q] * (1.f - zg[q]);
+            const float dz = dh[q] * (hp[q] - ng[q]);
+            dhd[q] = dh[q] * zg[q];
+            dnp[q] = dn * (1.f - ng[q] * ng[q]);
+            const float dr = dnp[q] * ghn[q];
+            drp[q] = dr * rg[q] * (1.f - rg[q]);
+            dzp[q] = dz * zg[q] * (1.f - zg[q]);
+            dghn[q] = dnp[q] * rg[q];
+        }
+        float* gi = sgi + col * LDG;
+        float* gh = sgh + col * LDG;
+        *reinterpret_cast<floatx4*>(gi + f0) = drp;
+        *reinterpret_cast<floatx4*>(gi + H + f0) = dzp;
+        *reinterpret_cast<floatx4*>(gi + 2 * H + f0) = dnp;
+        *reinterpret_cast<floatx4*>(gh + f0) = drp;
+        *reinterpret_cast<floatx4*>(gh + H + f0) = dzp;
+        *reinterpret_cast<floatx4*>(gh + 2 * H + f0) = dghn;
+        if (valid) {
+            const int64_t o3 = ((int64_t)t * R + r) * 3 * H + f0;
+            *reinterpret_cast<floatx4*>(dgi + o3) = drp;
+            *reinterpret_cast<floatx4*>(dgi + o3 + H) = dzp;
+            *reinterpret_cast<floatx4*>(dgi + o3 + 2 * H) = dnp;
+            *reinterpret_cast<floatx4*>(dgh + o3) = drp;
+            *reinterpret_cast<floatx4*>(dgh + o3 + H) = dzp;
+            *reinterpret_cast<floatx4*>(dgh + o3 + 2 * H) = dghn;
+        }
+        __syncthreads();
+        // dh_{t-1} = dh * z + W_hh^T dGH ;  dA = (W_ih^T dGI) * (x > 0)
+        floatx4 dprev = tile_mm_lds(whhT, 3 * H, w * 16, sgh, LDG, 3 * H / 16, dhd, lane);
+        floatx4 dx = tile_mm_lds(wihT, 3 * H, w * 16, sgi, LDG, 3 * H / 16, floatx4{0.f, 0.f, 0.f, 0.f}, lane);
+        if (valid) {
+            const floatx4 xv = ld4(ws_x + o);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dx[q] = xv[q] > 0.f ? dx[q] : 0.f;
+            *reinterpret_cast<floatx4*>(da + o) = dx;
+        }
+        dh = dprev;
+        __syncthreads();
+    }
+}
+
+// ================================================================================================
+// weight gradients: dW[M][K] = sum_rows delta[row][m] x[row][k], db[m] = sum_rows delta[row][m]
+struct WJob {
+    const float* delta;
+    const float* x;
+    float* dw;
+    float* db;
+    int64_t ldd, ldx;
+    int M, K, rows, mt, nt, chunks;
+    int task0;  // first task index
+    int64_t slab0;
+};
+struct WJobs {
+    WJob j[MAX_JOBS];
+    int n;
+};
+
+__device__ __forceinline__ int find_job(const WJobs& J, int task) {
+    int k = 0;
+    while (k + 1 < J.n && J.j[k + 1].task0 <= task) ++k;
+    return k;
+}
+
+// one wave per (job, m-tile, n-tile, row chunk); partial tile (+ bias partial when nt == 0) -> slab
+__global__ void __launch_bounds__(256) wgrad_kernel(WJobs J, float* __restrict__ slab) {
+    const int lane = threadIdx.x & 63;
+    const int task = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (task >= J.j[J.n - 1].task0 + J.j[J.n - 1].mt * J.j[J.n - 1].nt * J.j[J.n - 1].chunks) return;
+    const WJob jb = J.j[find_job(J, task)];
+    const int local = task - jb.task0;
+    const int ch = local % jb.chunks, tt = local / jb.chunks;
+    const int mt = tt / jb.nt, nt = tt % jb.nt;
+    const int col = lane & 15, g = lane >> 4;
+    const int m = mt * 16 + col, k = nt * 16 + col;
+    const int r0 = ch * WCH, r1 = min(jb.rows, r0 + WCH);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    const bool mv = m < jb.M, kv = k < jb.K;
+    for (int rr = r0; rr < r1; rr += 4) {
+        const int row = rr + g;
+        const bool rv = row < r1;
+        const float a = (mv && rv) ? jb.delta[(int64_t)row * jb.ldd + m] : 0.f;
+        const float xv = (kv && rv) ? jb.x[(int64_t)row * jb.ldx + k] : 0.f;
+        acc = mfma4(a, xv, acc);
+        bsum += a;
+    }
+    float* out = slab + jb.slab0 + ((int64_t)tt * jb.chunks + ch) * 272;
+    // D layout: reg q -> (m = mt*16 + 4g + q, k = nt*16 + col)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(4 * g + q) * 16 + col] = acc[q];
+    bsum += __shfl_xor(bsum, 16);
+    bsum += __shfl_xor(bsum, 32);
+    if (g == 0) out[256 + col] = bsum;
+}
+
+// fixed-order sum over chunks -> dW, db
+__global__ void wgrad_reduce_kernel(WJobs J, const float* __restrict__ slab) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (job, tile, 272)
+    int64_t acc = 0;
+    for (int q = 0; q < J.n; ++q) {
+        const WJob& jb = J.j[q];
+        const int64_t n_el = (int64_t)jb.mt * jb.nt * 272;
+        if (i >= acc && i < acc + n_el) {
+            const int64_t loc = i - acc;
+            const int tt = (int)(loc / 272), e = (int)(loc % 272);
+            const int mt = tt / jb.nt, nt = tt % jb.nt;
+            float s = 0.f;
+            const float* base = slab + jb.slab0 + (int64_t)tt * jb.chunks * 272 + e;
+            for (int ch = 0; ch < jb.chunks; ++ch) s += base[(int64_t)ch * 272];
+            if (e < 256) {
+                const int m = mt * 16 + e / 16, k = nt * 16 + e % 16;
+                if (m < jb.M && k < jb.K) jb.dw[(int64_t)m * jb.K + k] = s;
+            } else if (nt == 0 && jb.db) {
+                const int m = mt * 16 + (e - 256);
+                if (m < jb.M) jb.db[m] = s;
+            }
+            return;
+        }
+        acc += n_el;
+    }
+}
+
+// ================================================================================================
+// loss/stats, clip_grad_norm_, RMSprop (single workgroup; deterministic)
+__global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ part, int n_part,
+                                                      const float* __restrict__ msum_p, float* __restrict__ params,
+                                                      float* __restrict__ grads, float* __restrict__ sq, int64_t n_params,
+                                                      float lr, float alpha, float eps, float max_norm, int N,
+                                                      float* __restrict__ stats) {
+    __shared__ float red[1024];
+    __shared__ float s4[4];
+    const int tid = threadIdx.x;
+    for (int k = 0; k < 4; ++k) {
+        float s = 0.f;
+        for (int i = tid; i < n_part; i += blockDim.x) s += part[(int64_t)i * 4 + k];
+        red[tid] = s;
+        __syncthreads();
+        for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+            if (tid < w) red[tid] += red[tid + w];
+            __syncthreads();
+        }
+        if (tid == 0) s4[k] = red[0];
+        __syncthreads();
+    }
+    float s = 0.f;
+    for (int64_t i = tid; i < n_params; i += blockDim.x) s += grads[i] * grads[i];
+    red[tid] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (tid < w) red[tid] += red[tid + w];
+        __syncthreads();
+    }
+    const float norm = sqrtf(red[0]);
+    const float coef = fminf(max_norm / (norm + 1e-6f), 1.f);  // torch clip_grad_norm_ (clamped coef)
+    for (int64_t i = tid; i < n_params; i += blockDim.x) {
+        const float gi = grads[i] * coef;
+        grads[i] = gi;
+        const float a = alpha * sq[i] + (1.f - alpha) * gi * gi;  // RMSprop square_avg
+        sq[i] = a;
+        params[i] -= lr * gi / (sqrtf(a) + eps);
+    }
+    if (tid == 0) {
+        const float ms = msum_p[0];
+        stats[0] = s4[0] / ms;
+        stats[1] = norm;
+        stats[2] = s4[1] / ms;
+        stats[3] = s4[2] / (ms * N);
+        stats[4] = s4[3] / (ms * N);
+        stats[5] = ms;
+        stats[6] = ms;
+        stats[7] = 0.f;
+    }
+}
+
+// ================================================================================================
+// host side
+struct Plan {
+    LCfg c;
+    AgentLayout L;
+    AgentOffs ao;
+    MixOffs mo;
+    MixPack mp;
+    WsLayout w;
+    int64_t n_agent, n_mixer;
+};
+
+int check_cfg(const MlgLearnerCfg* c) {
+    MLG_REQUIRE(c != nullptr, "null learner cfg");
+    MLG_REQUIRE(c->H == 32 || c->H == 64 || c->H == 128, "rnn_hidden_dim=%d unsupported (32/64/128)", c->H);
+    MLG_REQUIRE(c->B >= 1 && c->T >= 2 && c->N >= 1 && c->N <= MAXN && c->A >= 1, "learner: bad sizes B=%d T=%d N=%d",
+                c->B, c->T, c->N);
+    MLG_REQUIRE(c->mixer == 1 || c->mixer == 2, "learner: mixer must be vdn or qmix (IQL is not built)");
+    if (c->mixer == 2) {
+        MLG_REQUIRE(c->hypernet_layers == 2, "learner: qmix hypernet_layers=%d unsupported (2)", c->hypernet_layers);
+        MLG_REQUIRE(c->E == 32 && c->HE == 64, "learner: qmix mixing_embed_dim=32, hypernet_embed=64 supported (got %d, %d)",
+                    c->E, c->HE);
+    }
+    return 0;
+}
+
+Plan make_plan(const MlgLearnerCfg* cfg, int T1) {
+    Plan p;
+    LCfg& c = p.c;
+    c.B = cfg->B;
+    c.T = cfg->T;
+    c.T1 = T1;
+    c.N = cfg->N;
+    c.A = cfg->A;
+    c.Ap = (cfg->A + 15) / 16 * 16;
+    c.d_obs = cfg->d_obs;
+    c.d_in = cfg->d_obs + (cfg->obs_last_action ? cfg->A : 0) + (cfg->obs_agent_id ? cfg->N : 0);
+    c.H = cfg->H;
+    c.S = cfg->S;
+    c.E = cfg->E;
+    c.HE = cfg->HE;
+    c.mixer = cfg->mixer;
+    c.double_q = cfg->double_q;
+    c.last_action = cfg->obs_last_action;
+    c.agent_id = cfg->obs_agent_id;
+    c.R = cfg->B * cfg->N;
+    c.RM = cfg->B * (cfg->T - 1);
+    c.gamma = cfg->gamma;
+    MlgAgentDims d{cfg->d_obs, cfg->A, cfg->N, cfg->H, c.d_in, cfg->obs_last_action, cfg->obs_agent_id};
+    p.L = make_agent_layout(d);
+    p.ao = agent_offs(c.H, c.d_in, c.A);
+    p.mo = mix_offs(c.N, c.S, c.E, c.HE);
+    p.mp = mix_pack(c.N, c.S, c.E, c.HE);
+    p.n_agent = p.ao.total;
+    p.n_mixer = c.mixer == 2 ? p.mo.total : 0;
+    WsLayout& w = p.w;
+    const int64_t T = c.T, R = c.R, H = c.H, RM = c.RM;
+    const int L1 = 2 * c.HE + 2 * c.E;
+    int64_t o = 0;
+    auto take = [&](int64_t n) { int64_t r = o; o += a4(n); return r; };
+    w.p_on = take(p.L.total);
+    w.p_tg = take(p.L.total);
+    w.wihT = take(3 * H * H);
+    w.whhT = take(3 * H * H);
+    w.mix_on = take(p.mp.total);
+    w.mix_tg = take(p.mp.total);
+    w.in = take(T * R * c.d_in);
+    w.x = take(T * R * H);
+    w.hs = take((T + 1) * R * H);
+    w.gr = take(T * R * H);
+    w.gz = take(T * R * H);
+    w.gn = take(T * R * H);
+    w.ghn = take(T * R * H);
+    w.mac = take(T * R * c.A);
+    w.tmac = take(T * R * c.A);
+    w.dq = take(T * R);
+    w.d2 = take(T * R * c.A);
+    w.dgi = take(T * R * 3 * H);
+    w.dgh = take(T * R * 3 * H);
+    w.da = take(T * R * H);
+    w.srow = take(RM * c.S);
+    w.l1act = take(RM * L1);
+    w.d1 = take(RM * L1);
+    w.da2 = take(RM * c.N * c.E);
+    w.df2 = take(RM * c.E);
+    w.dv2 = take(RM);
+    w.n_mix_tiles = (int)((RM + 15) / 16);
+    w.part = take((int64_t)w.n_mix_tiles * 4);
+    w.msum = take(4);
+    w.slab = o;
+    w.total = o;  // + slab size, filled by make_jobs
+    return p;
+}
+
+WJob job(const float* delta, int64_t ldd, const float* x, int64_t ldx, float* dw, float* db, int M, int K, int rows) {
+    WJob j;
+    j.delta = delta;
+    j.x = x;
+    j.dw = dw;
+    j.db = db;
+    j.ldd = ldd;
+    j.ldx = ldx;
+    j.M = M;
+    j.K = K;
+    j.rows = rows;
+    j.mt = (M + 15) / 16;
+    j.nt = (K + 15) / 16;
+    j.chunks = (rows + WCH - 1) / WCH;
+    return j;
+}
+
+// builds the job list; with ws == nullptr only sizes are computed (pointers are offsets from 0)
+WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_tasks) {
+    const LCfg& c = p.c;
+    float* W = ws ? ws : nullptr;
+    auto at = [&](int64_t off) { return W ? W + off : (float*)nullptr; };
+    float* G = grads;
+    auto gp = [&](int64_t off) { return G ? G + off : (float*)nullptr; };
+    const int TR = c.T * c.R, H = c.H, L1 = 2 * c.HE + 2 * c.E, RM = c.RM;
+    WJobs J;
+    J.n = 0;
+    const AgentOffs& a = p.ao;
+    J.j[J.n++] = job(at(p.w.da), H, at(p.w.in), c.d_in, gp(a.fc1w), gp(a.fc1b), H, c.d_in, TR);
+    J.j[J.n++] = job(at(p.w.dgi), 3 * H, at(p.w.x), H, gp(a.wih), gp(a.bih), 3 * H, H, TR);
+    J.j[J.n++] = job(at(p.w.dgh), 3 * H, at(p.w.hs), H, gp(a.whh), gp(a.bhh), 3 * H, H, TR);
+    J.j[J.n++] = job(at(p.w.d2), c.A, at(p.w.hs) ? at(p.w.hs) + (int64_t)c.R * H : nullptr, H, gp(a.fc2w), gp(a.fc2b),
+                     c.A, H, TR);
+    if (c.mixer == 2) {
+        const MixOffs& m = p.mo;
+        const int64_t G0 = p.n_agent;
+        auto mg = [&](int64_t off) { return G ? G + G0 + off : (float*)nullptr; };
+        const float* d1 = at(p.w.d1);
+        const float* la = at(p.w.l1act);
+        auto off = [&](const float* base, int64_t k) { return base ? base + k : (const float*)nullptr; };
+        J.j[J.n++] = job(off(d1, 0), L1, at(p.w.srow), c.S, mg(m.w1_0w), mg(m.w1_0b), c.HE, c.S, RM);
+        J.j[J.n++] = job(off(d1, c.HE), L1, at(p.w.srow), c.S, mg(m.wf_0w), mg(m.wf_0b), c.HE, c.S, RM);
+        J.j[J.n++] = job(off(d1, 2 * c.HE), L1, at(p.w.srow), c.S, mg(m.b1w), mg(m.b1b), c.E, c.S, RM);
+        J.j[J.n++] = job(off(d1, 2 * c.HE + c.E), L1, at(p.w.srow), c.S, mg(m.v0w), mg(m.v0b), c.E, c.S, RM);
+        J.j[J.n++] = job(at(p.w.da2), (int64_t)c.N * c.E, off(la, 0), L1, mg(m.w1_2w), mg(m.w1_2b), c.N * c.E, c.HE, RM);
+        J.j[J.n++] = job(at(p.w.df2), c.E, off(la, c.HE), L1, mg(m.wf_2w), mg(m.wf_2b), c.E, c.HE, RM);
+        J.j[J.n++] = job(at(p.w.dv2), 1, off(la, 2 * c.HE + c.E), L1, mg(m.v2w), mg(m.v2b), 1, c.E, RM);
+    }
+    int tasks = 0;
+    int64_t slab = 0;
+    for (int q = 0; q < J.n; ++q) {
+        J.j[q].task0 = tasks;
+        J.j[q].slab0 = slab;
+        tasks += J.j[q].mt * J.j[q].nt * J.j[q].chunks;
+        slab += (int64_t)J.j[q].mt * J.j[q].nt * J.j[q].chunks * 272;
+    }
+    *slab_floats = slab;
+    *n_tasks = tasks;
+    return J;
+}
+
+template <int H>
+int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hipStream_t s) {
+    const LCfg& c = p.c;
+    float* ws = bufs->workspace;
+    const MlgBatch& bt = bufs->batch;
+    const float* params = bufs->params;
+    const float* tparams = bufs->target_params;
+    // ---- pack ----
+    auto pack_agent = [&](const float* flat, float* out) {
+        MlgAgentDims d{c.d_obs, c.A, c.N, c.H, c.d_in, c.last_action, c.agent_id};
+        MlgAgentParams ap{flat + p.ao.fc1w, flat + p.ao.fc1b, flat + p.ao.wih, flat + p.ao.bih,
+                          flat + p.ao.whh, flat + p.ao.bhh, flat + p.ao.fc2w, flat + p.ao.fc2b};
+        return mlg_pack_agent(&d, &ap, out, s);
+    };
+    if (pack_agent(params, ws + p.w.p_on) || pack_agent(tparams, ws + p.w.p_tg)) return 1;
+    const int n3 = 3 * c.H * c.H;
+    hipLaunchKernelGGL(transpose_kernel, dim3((n3 + 255) / 256), dim3(256), 0, s, params + p.ao.wih, ws + p.w.wihT, 3 * c.H, c.H);
+    hipLaunchKernelGGL(transpose_kernel, dim3((n3 + 255) / 256), dim3(256), 0, s, params + p.ao.whh, ws + p.w.whhT, 3 * c.H, c.H);
+    MixPtrs Mon{}, Mtg{};
+    if (c.mixer == 2) {
+        const int64_t g0 = p.n_agent;
+        const int nb = (int)((p.mp.total + 255) / 256);
+        hipLaunchKernelGGL(pack_mixer_kernel, dim3(nb), dim3(256), 0, s, p.mp, p.mo, params + g0, ws + p.w.mix_on, c.N, c.S, c.E, c.HE);
+        hipLaunchKernelGGL(pack_mixer_kernel, dim3(nb), dim3(256), 0, s, p.mp, p.mo, tparams + g0, ws + p.w.mix_tg, c.N, c.S, c.E, c.HE);
+        auto ptrs = [&](const float* flat, const float* pk) {
+            MixPtrs m;
+            m.m1 = pk + p.mp.m1;
+            m.mb1 = pk + p.mp.mb1;
+            m.a2 = flat + g0 + p.mo.w1_2w;
+            m.ba2 = flat + g0 + p.mo.w1_2b;
+            m.a2T = pk + p.mp.a2T;
+            m.f2 = flat + g0 + p.mo.wf_2w;
+            m.bf2 = flat + g0 + p.mo.wf_2b;
+            m.f2T = pk + p.mp.f2T;
+            m.v2p = pk + p.mp.v2p;
+            m.bv2p = pk + p.mp.bv2p;
+            return m;
+        };
+        Mon = ptrs(params, ws + p.w.mix_on);
+        Mtg = ptrs(tparams, ws + p.w.mix_tg);
+    }
+    // d2 is sparse: zero it (and dq) every call
+    hipMemsetAsync(ws + p.w.d2, 0, sizeof(float) * (size_t)c.T * c.R * c.A, s);
+    hipMemsetAsync(ws + p.w.dq, 0, sizeof(float) * (size_t)c.T * c.R, s);
+    hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + p.w.msum);
+    const int ntiles = (c.R + 15) / 16;
+    const int threads = (c.H / 16) * 64;
+    hipLaunchKernelGGL((agent_fwd_kernel<H>), dim3(2 * ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on, ws + p.w.p_tg,
+                       ws + p.w.in, ws + p.w.x, ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn,
+                       ws + p.w.mac, ws + p.w.tmac);
+    MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
+              ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
+    hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(64), 0, s, c, bt, Mon, Mtg, p.mp,
+                       ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
+    hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on, ws + p.w.wihT,
+                       ws + p.w.whhT, ws + p.w.x, ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn,
+                       ws + p.w.dq, ws + p.w.dgi, ws + p.w.dgh, ws + p.w.da);
+    int64_t slab_floats;
+    int n_tasks;
+    WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks);
+    hipLaunchKernelGGL(wgrad_kernel, dim3((n_tasks + 3) / 4), dim3(256), 0, s, J, ws + p.w.slab);
+    int64_t n_red = 0;
+    for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n_red + 255) / 256)), dim3(256), 0, s, J, ws + p.w.slab);
+    hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(1024), 0, s, ws + p.w.part, p.w.n_mix_tiles, ws + p.w.msum,
+                       bufs->params, bufs->grads, bufs->square_avg, p.n_agent + p.n_mixer, cfg->lr, cfg->optim_alpha,
+                       cfg->optim_eps, cfg->grad_norm_clip, c.N, bufs->stats);
+    return mlg::check_launch("qlearner_train");
+}
+
+}  // namespace
+
+extern "C" int64_t mlg_qlearner_param_counts(const MlgLearnerCfg* c, int64_t* n_agent, int64_t* n_mixer) {
+    if (check_cfg(c)) return -1;
+    Plan p = make_plan(c, c->T);
+    if (n_agent) *n_agent = p.n_agent;
+    if (n_mixer) *n_mixer = p.n_mixer;
+    return p.n_agent + p.n_mixer;
+}
+
+extern "C" int64_t mlg_qlearner_workspace_floats(const MlgLearnerCfg* c) {
+    if (check_cfg(c)) return -1;
+    Plan p = make_plan(c, c->T);
+    int64_t slab;
+    int tasks;
+    make_jobs(p, nullptr, nullptr, &slab, &tasks);
+    return p.w.total + slab;
+}
+
+extern "C" int mlg_qlearner_train(const MlgLearnerCfg* c, const MlgLearnerBufs* b, void* stream) {
+    if (check_cfg(c)) return 1;
+    MLG_REQUIRE(b && b->params && b->grads && b->square_avg && b->target_params && b->workspace && b->stats,
+                "qlearner_train: null buffer");
+    const MlgBatch& bt = b->batch;
+    MLG_REQUIRE(bt.state && bt.obs && bt.actions && bt.avail && bt.reward && bt.terminated && bt.actions_onehot && bt.filled,
+                "qlearner_train: batch has null tensors");
+    MLG_REQUIRE(bt.B == c->B && bt.T1 >= c->T, "qlearner_train: batch B=%d T1=%d vs cfg B=%d T=%d", bt.B, bt.T1, c->B, c->T);
+    Plan p = make_plan(c, bt.T1);
+    hipStream_t s = (hipStream_t)stream;
+    if (c->H == 64) return run_train<64>(p, c, b, s);
+    if (c->H == 32) return run_train<32>(p, c, b, s);
+    return run_train<128>(p, c, b, s);
+}

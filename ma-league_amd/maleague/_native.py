@@ -61,6 +61,17 @@ class MlgQMixParams(ctypes.Structure):
                                               "hypernet_layers"]]
 
 
+class MlgLearnerCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ["B", "T", "N", "A", "d_obs", "H", "S", "E", "HE", "hypernet_layers",
+                                              "mixer", "double_q", "obs_last_action", "obs_agent_id"]] + \
+               [(n, ctypes.c_float) for n in ["gamma", "lr", "optim_alpha", "optim_eps", "grad_norm_clip"]]
+
+
+class MlgLearnerBufs(ctypes.Structure):
+    _fields_ = [("batch", MlgBatch)] + [(n, ctypes.c_void_p) for n in ["params", "grads", "square_avg",
+                                                                      "target_params", "workspace", "stats"]]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
 # name -> (restype, argtypes); mirrors include/maleague.h one for one.
@@ -75,6 +86,9 @@ SIGNATURES = {
     "mlg_mac_forward": (ctypes.c_int, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "mlg_select_actions": (ctypes.c_int, [_P, _P, _I, _I, _I, _P, _P, _I, ctypes.c_float, _P, _P, _P]),
     "mlg_qmix_forward": (ctypes.c_int, [_P, _P, _P, _P, _I, _P]),
+    "mlg_qlearner_param_counts": (ctypes.c_int64, [_P, _P, _P]),
+    "mlg_qlearner_workspace_floats": (ctypes.c_int64, [_P]),
+    "mlg_qlearner_train": (ctypes.c_int, [_P, _P, _P]),
     "mlg_last_error": (ctypes.c_char_p, []),
     "mlg_version": (ctypes.c_char_p, []),
 }

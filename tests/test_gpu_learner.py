@@ -1,0 +1,128 @@
+"""GPU parity of the fused QLearner.train pipeline (mlg_qlearner_train) against golden vectors of the
+reference QLearner (3 consecutive train() calls incl. a hard target update) and against the CPU oracle
+(oracle/learner_ref.py) on rollouts produced by the HIP stepper.
+
+Tolerances (fp32, different summation orders): stats rtol 1e-4; parameters after RMSprop atol 2e-5
+(RMSprop's first step moves every weight by ~lr * 10 * sign(g), so sign-level agreement of the
+gradients is what these checks exercise); north_star's 1e-4 bound on Q-values is asserted on Q.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import learner_ref as LR
+from helpers import qmix_args, scheme_for
+
+pytestmark = pytest.mark.gpu
+
+
+def _golden_batch(d, device):
+    from maleague.components.episode_batch import EpisodeBatch
+    b = LR.batch_from_npz(d)
+    B, T, N, _ = b["obs"].shape
+    A = b["avail_actions"].shape[-1]
+    info = {"state_shape": b["state"].shape[-1], "obs_shape": b["obs"].shape[-1], "n_actions": A, "n_agents": N}
+    scheme, groups, preprocess = scheme_for(info, torch)
+    eb = EpisodeBatch(scheme, groups, B, T, preprocess=preprocess, device=device)
+    for k, v in b.items():
+        eb.data.transition_data[k].copy_(v)
+    return eb
+
+
+class _Log:
+    def __init__(self):
+        self.stats = {}
+
+    def log_stat(self, k, v, t):
+        self.stats[k] = v
+
+    def info(self, *a):
+        pass
+
+
+def _learner(d, device, args, mixer_prefix="p0.mixer."):
+    from maleague.controllers import BasicMAC
+    from maleague.learners import QLearner
+    eb = _golden_batch(d, device)
+    mac = BasicMAC(eb.scheme, eb.groups, args)
+    mac.load_state_dict({k[len("p0.agent."):]: torch.from_numpy(np.array(d[k])) for k in d.files
+                         if k.startswith("p0.agent.")})
+    log = _Log()
+    learner = QLearner(mac, eb.scheme, log, args, name="home")
+    if args.mixer == "qmix":
+        msd = {k[len(mixer_prefix):]: torch.from_numpy(np.array(d[k])) for k in d.files if k.startswith(mixer_prefix)}
+        learner.mixer.load_state_dict(msd)
+        learner.target_mixer.load_state_dict(msd)
+    learner.build_optimizer()
+    return learner, eb, log
+
+
+@pytest.mark.parametrize("name,kw", [("qlearner_qmix_dq.npz", {}), ("qlearner_qmix_nodq.npz", {"double_q": False}),
+                                     ("qlearner_vdn.npz", {"mixer": "vdn"})])
+def test_qlearner_golden(device, golden, name, kw):
+    d = golden(name)
+    args = qmix_args(**kw)
+    learner, eb, log = _learner(d, device, args)
+    for i, (t_env, ep) in enumerate(d["calls"]):
+        learner.train(eb, int(t_env), int(ep))
+        for k in ["loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]:
+            np.testing.assert_allclose(learner.last_stats[k], float(d[f"stat{i}.{k}"]), rtol=1e-4, atol=1e-6,
+                                       err_msg=f"{name} call {i} {k}")
+        assert log.stats["home_qlearner_loss"] == learner.last_stats["loss"]
+    last = len(d["calls"])
+    sd = learner.mac.agent.state_dict()
+    for k, v in sd.items():
+        np.testing.assert_allclose(v.cpu().numpy(), d[f"p{last}.agent.{k}"], atol=2e-5, rtol=0, err_msg=k)
+    tsd = learner.target_mac.agent.state_dict()
+    for k, v in tsd.items():
+        np.testing.assert_allclose(v.cpu().numpy(), d[f"p{last}.target_agent.{k}"], atol=2e-5, rtol=0, err_msg=k)
+    if args.mixer == "qmix":
+        for k, v in learner.mixer.state_dict().items():
+            np.testing.assert_allclose(v.cpu().numpy(), d[f"p{last}.mixer.{k}"], atol=2e-5, rtol=0, err_msg=k)
+    assert learner.mac.agent.trained_steps == int(d["trained_steps"])
+
+
+def test_qlearner_vs_oracle_on_rollout(device):
+    """Train on a batch produced by the HIP stepper (5v5, 32 episodes) and compare one step with the oracle."""
+    from maleague.components.episode_batch import EpisodeBatch
+    from maleague.controllers import BasicMAC
+    from maleague.custom_logging import MainLogger
+    from maleague.learners import QLearner
+    from maleague.steppers import ParallelStepper
+    args = qmix_args(batch_size_run=32, seed=11, env_args={"match_build_plan": "medium_1h_2t_2a", "grid_size": 20,
+                                                           "stochastic_spawns": True, "episode_limit": 60})
+    stepper = ParallelStepper(args, MainLogger())
+    info = stepper.get_env_info()
+    args.n_agents, args.n_actions, args.state_shape = info["n_agents"], info["n_actions"], info["state_shape"]
+    scheme, groups, preprocess = scheme_for(info, torch)
+    proto = EpisodeBatch(scheme, groups, 1, 2, preprocess=preprocess, device=device)
+    torch.manual_seed(3)
+    mac = BasicMAC(proto.scheme, groups, args)
+    learner = QLearner(mac, proto.scheme, _Log(), args, name="home")
+    agent0 = {k: v.detach().cpu().clone() for k, v in mac.agent.state_dict().items()}
+    mixer0 = {k: v.detach().cpu().clone() for k, v in learner.mixer.state_dict().items()}
+    learner.build_optimizer()
+    stepper.initialize(scheme, groups, preprocess, mac)
+    stepper.t_env = 30000
+    batch, _ = stepper.run(test_mode=False)
+    T = int(batch.max_t_filled())
+    sample = batch[:, :T]
+    ref = LR.QLearnerRef(agent0, mixer0, copy.copy(args))
+    tb = {k: v.detach().cpu().clone() for k, v in sample.data.transition_data.items()}
+    exp = ref.train(tb, 30000, 0)
+    learner.train(sample, 30000, 0)
+    for k in ["loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]:
+        np.testing.assert_allclose(learner.last_stats[k], exp[k], rtol=2e-4, atol=1e-6, err_msg=k)
+    for k, v in learner.mac.agent.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), ref.agent_state()[k].numpy(), atol=5e-5, rtol=0, err_msg=k)
+    for k, v in learner.mixer.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), ref.mixer_state()[k].numpy(), atol=5e-5, rtol=0, err_msg=k)
+    # Q of the trained agent within 1e-4 of the oracle forward with the same (updated) weights
+    q_ref, _ = LR.mac_unroll({k: v.detach().cpu() for k, v in learner.mac.agent.state_dict().items()}, tb,
+                             args.n_agents, T=T)
+    learner.mac.init_hidden(sample.batch_size)
+    for t in range(T):
+        q = learner.mac.forward(sample, t)
+        np.testing.assert_allclose(q.cpu().numpy(), q_ref[:, t].numpy(), atol=1e-4, rtol=0)
