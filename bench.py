@@ -1,0 +1,151 @@
+"""bench.py -- env-steps/sec (rollout + learn), 5v5 QMIX, 4096 envs per GPU (BASELINE.json config 2).
+
+One "step" = one iteration of MultiAgentExperiment.start (src/runs/train/ma_experiment.py:173-209 via
+_train_episode :224-241): one ParallelStepper.run over all envs (one fused rollout launch) + insert into
+the HBM replay buffer + one QLearner.train on 32 sampled episodes (fused learner pipeline).
+value = env steps (t_env increments, parallel_stepper.py:178-179) of all ranks / max-over-ranks time.
+
+N > 1: one process per GPU (torch.distributed.run), each an independent league learner with its own
+4096 envs and replay buffer -- no data-path collective; barrier + max-time all_reduce only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "ma-league_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK = 157.3e12  # MI355X dense fp32 (MFMA == VALU rate), MI355X_MICROARCH.md chip table
+HBM_PEAK = 8.0e12
+
+
+def agent_flops_per_forward(N, d_in, H, A):
+    """Algorithmic FLOPs of one BasicMAC.forward per env (drqn_agent.py:29-35 for N agents)."""
+    return N * 2 * (d_in * H + 2 * H * 3 * H + H * A)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--episode-limit", type=int, default=100)
+    ap.add_argument("--plan", default="medium_1h_4t")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per rollout launch (profiles/)")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+
+    from maleague.custom_logging import MainLogger
+    from maleague.runs import MultiAgentExperiment
+    from maleague.utils.config import build_config, to_args
+
+    overrides = [f"batch_size_run={a.envs}", "runner=parallel", "buffer_cpu_only=False",
+                 f"env_args.match_build_plan={a.plan}", f"env_args.episode_limit={a.episode_limit}",
+                 f"seed={rank}", "learner_log_interval=1000000000", "log_interval=1000000000",
+                 "runner_log_interval=1000000000", "test_interval=1000000000000", "t_max=1000000000000",
+                 "show_exp_parameters=False"]
+    cfg = build_config("qmix", "ma", overrides=overrides, device_index=local_rank)
+    exp = MultiAgentExperiment(to_args(cfg), MainLogger(log_interval=10 ** 12))
+    exp._init_stepper()
+    stepper, learner = exp.stepper, exp.home_learner
+    B = stepper.batch_size
+    # steady-state exploration (epsilon floor 0.05), as SURVEY §8d prescribes for timing runs
+    stepper.t_env = 10 ** 6
+    episode = 0
+    for _ in range(a.warmup):
+        exp._train_episode(episode)
+        episode += B
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    # rollout-kernel timing with HIP events on the stream the kernel is launched on
+    stepper.timing = []
+    t0_env = stepper.t_env
+    lens = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        exp._train_episode(episode)
+        episode += B
+        lens.append(stepper.last_run["ep_len"])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    env_steps = stepper.t_env - t0_env
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        s = torch.tensor([env_steps], dtype=torch.float64, device=dev)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        env_steps = int(s.item())
+    ev_ms = [st.elapsed_time(en) for st, en in stepper.timing]
+    stepper.timing = None
+    value = env_steps / elapsed
+
+    # roofline of the dominant kernel (rollout_kernel): fp32 MFMA-bound agent cell
+    info = stepper.get_env_info()
+    N, A = info["n_agents"], info["n_actions"]
+    d_in = info["obs_shape"] + A + N
+    fl = agent_flops_per_forward(N, d_in, 64, A)
+    forwards = sum(int((l + 1).sum()) for l in lens) / len(lens)  # agent forwards per launch (env steps + final)
+    avg_kernel_s = sum(ev_ms) / len(ev_ms) / 1e3
+    achieved = fl * forwards / avg_kernel_s
+    traffic = None
+    if a.traffic_json and os.path.exists(a.traffic_json):
+        with open(a.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cpu_baseline
+        r = cpu_baseline.run(seconds=a.cpu_seconds, B=64, episode_limit=a.episode_limit,
+                             threads=min(16, os.cpu_count() or 1))
+        cpu = {"value": r["value"], "unit": "env-steps/s", "cores": r["cores"], "kind": "port",
+               "sample": f"{r['runs']} runs x 64 envs (+1 train each), {r['env_steps']} env steps in "
+                         f"{r['seconds']:.1f}s; oracle stepper + C env + PyTorch-CPU DRQN/QMIX learner"}
+    if rank == 0:
+        out = {"metric": "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X",
+               "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+               "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "f32", "data": "synthetic (spec-v1 5v5 battles, random-init QMIX)",
+               "config": {"workload": f"qmix_5v5_{a.plan}_{B}envs_ep{a.episode_limit}", "envs_per_gpu": B,
+                          "episode_limit": a.episode_limit, "learner_batch": 32, "rnn_hidden_dim": 64,
+                          "buffer_size": 5000, "parallelism": f"league{world}"},
+               "env_steps": env_steps, "mean_episode_len": env_steps / max(1, a.steps * B * world),
+               "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12,
+                            "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic,
+                            "kernel": "rollout_kernel<64,1>", "avg_kernel_ms": avg_kernel_s * 1e3,
+                            "flops_per_launch": fl * forwards},
+               "cpu_baseline": cpu}
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

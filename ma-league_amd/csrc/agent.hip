@@ -80,13 +80,14 @@ __global__ void __launch_bounds__(256) agent_forward_kernel(AgentLayout L, const
         if (valid && h_in) v = ld4(h_in + (int64_t)row * H + c * 16 + 4 * g);
         h[c] = v;
     }
-    agent_cell_hidden<H, DENSE>(P, L, in, h, lane);
+    const WView W = global_view(P, L);
+    agent_cell_hidden<H, DENSE>(W, L, in, h, lane);
     if (valid) {
 #pragma unroll
         for (int c = 0; c < HC; ++c) *reinterpret_cast<floatx4*>(h_out + (int64_t)row * H + c * 16 + 4 * g) = h[c];
     }
     for (int at = 0; at < L.Ap / 16; ++at) {
-        const floatx4 qt = agent_q_tile<H>(P, L, h, at, lane);
+        const floatx4 qt = agent_q_tile<H>(W, h, at, lane);
         if (!valid) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

@@ -77,50 +77,128 @@ __device__ __forceinline__ floatx4 load_chunk(const float* x, int k0, int n) {
     return v;
 }
 
+// Where the cell reads its weights from: the packed block in HBM/L2 (row strides = the packed widths) or a
+// padded copy in LDS (row strides + 4 floats, so the 16 rows of an A-operand read hit 16 distinct
+// 16-byte bank slots).  Offsets are in floats from p.
+struct WView {
+    const float* p;
+    int64_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2;
+    int ldd, ldo, ldh;
+};
+
+__host__ __device__ inline WView global_view(const float* P, const AgentLayout& L) {
+    WView v;
+    v.p = P;
+    v.w1d = L.w1d; v.w1o = L.w1o; v.w1a = L.w1a; v.w1n = L.w1n; v.b1 = L.b1; v.wih = L.wih; v.bih = L.bih;
+    v.whh = L.whh; v.bhh = L.bhh; v.brz = L.brz; v.w2 = L.w2; v.b2 = L.b2;
+    v.ldd = L.Dip; v.ldo = L.Dob; v.ldh = L.H;
+    return v;
+}
+
+// LDS image used by the rollout kernel (no dense w1d): offsets relative to the LDS base.
+struct LdsWeights {
+    int64_t w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;
+    int ldo, ldh;
+};
+__host__ __device__ inline LdsWeights make_lds_weights(const AgentLayout& L) {
+    LdsWeights w;
+    w.ldo = L.Dob + 4;
+    w.ldh = L.H + 4;
+    int64_t o = 0;
+    w.w1o = o; o += (int64_t)L.H * w.ldo;
+    w.w1a = o; o += L.last_action ? (int64_t)L.A * w.ldh : 0;
+    w.w1n = o; o += L.agent_id ? (int64_t)L.N * w.ldh : 0;
+    w.b1 = o; o += L.H;
+    w.wih = o; o += (int64_t)3 * L.H * w.ldh;
+    w.bih = o; o += 3 * L.H;
+    w.whh = o; o += (int64_t)3 * L.H * w.ldh;
+    w.bhh = o; o += 3 * L.H;
+    w.brz = o; o += 2 * L.H;
+    w.w2 = o; o += (int64_t)L.Ap * w.ldh;
+    w.b2 = o; o += L.Ap;
+    w.total = mlg_align4(o);
+    return w;
+}
+
+__device__ inline WView lds_view(const float* base, const LdsWeights& w, const AgentLayout& L) {
+    WView v;
+    v.p = base;
+    v.w1d = 0; v.w1o = w.w1o; v.w1a = w.w1a; v.w1n = w.w1n; v.b1 = w.b1; v.wih = w.wih; v.bih = w.bih;
+    v.whh = w.whh; v.bhh = w.bhh; v.brz = w.brz; v.w2 = w.w2; v.b2 = w.b2;
+    v.ldd = 0; v.ldo = w.ldo; v.ldh = w.ldh;
+    return v;
+}
+
+// Cooperative copy packed (global) -> padded LDS image (whole workgroup; caller syncs).
+__device__ inline void load_weights_to_lds(const float* __restrict__ P, const AgentLayout& L, const LdsWeights& w,
+                                           float* lds) {
+    const int H = L.H;
+    auto rows = [&](int64_t src, int64_t dst, int nrows, int ncols, int ld) {
+        for (int i = threadIdx.x; i < nrows * ncols; i += blockDim.x) {
+            const int r = i / ncols, c = i % ncols;
+            lds[dst + (int64_t)r * ld + c] = P[src + (int64_t)r * ncols + c];
+        }
+    };
+    rows(L.w1o, w.w1o, H, L.Dob, w.ldo);
+    if (L.last_action) rows(L.w1a, w.w1a, L.A, H, w.ldh);
+    if (L.agent_id) rows(L.w1n, w.w1n, L.N, H, w.ldh);
+    rows(L.b1, w.b1, 1, H, H);
+    rows(L.wih, w.wih, 3 * H, H, w.ldh);
+    rows(L.bih, w.bih, 1, 3 * H, 3 * H);
+    rows(L.whh, w.whh, 3 * H, H, w.ldh);
+    rows(L.bhh, w.bhh, 1, 3 * H, 3 * H);
+    rows(L.brz, w.brz, 1, 2 * H, 2 * H);
+    rows(L.w2, w.w2, L.Ap, H, w.ldh);
+    rows(L.b2, w.b2, 1, L.Ap, L.Ap);
+}
+
 // fc1 (pre-activation, bias included) for one tile -> x (HC chunks, D layout).
 template <int H, bool DENSE>
-__device__ __forceinline__ void agent_fc1(const float* __restrict__ P, const AgentLayout& L, const RowIn& in,
-                                          floatx4 (&x)[H / 16], int lane) {
+__device__ __forceinline__ void agent_fc1(const WView& W, const AgentLayout& L, const RowIn& in, floatx4 (&x)[H / 16],
+                                          int lane) {
     constexpr int HC = H / 16;
     const int col = lane & 15, g = lane >> 4;
+    const float* P = W.p;
 #pragma unroll
     for (int mt = 0; mt < HC; ++mt) {
-        floatx4 b = ld4(P + L.b1 + mt * 16 + 4 * g);
+        floatx4 b = ld4(P + W.b1 + mt * 16 + 4 * g);
         if (!DENSE) {
             if (L.last_action) {
                 if (in.onehot) {
                     for (int a = 0; a < L.A; ++a) {
                         const float v = in.onehot[a];
-                        if (v != 0.f) b += v * ld4(P + L.w1a + (int64_t)a * H + mt * 16 + 4 * g);
+                        if (v != 0.f) b += v * ld4(P + W.w1a + (int64_t)a * W.ldh + mt * 16 + 4 * g);
                     }
                 } else if (in.prev_action >= 0) {
-                    b += ld4(P + L.w1a + (int64_t)in.prev_action * H + mt * 16 + 4 * g);
+                    b += ld4(P + W.w1a + (int64_t)in.prev_action * W.ldh + mt * 16 + 4 * g);
                 }
             }
-            if (L.agent_id) b += ld4(P + L.w1n + (int64_t)in.agent * H + mt * 16 + 4 * g);
+            if (L.agent_id) b += ld4(P + W.w1n + (int64_t)in.agent * W.ldh + mt * 16 + 4 * g);
         }
         x[mt] = b;
     }
     const int K = DENSE ? L.d_in : L.d_obs;
     const int KP = DENSE ? L.Dip : L.Dob;
-    const int64_t base = DENSE ? L.w1d : L.w1o;
+    const int ld = DENSE ? W.ldd : W.ldo;
+    const float* base = P + (DENSE ? W.w1d : W.w1o) + (int64_t)col * ld + 4 * g;
     for (int kc = 0; kc < KP / 16; ++kc) {
         const int k0 = kc * 16 + 4 * g;
         const floatx4 xin = load_chunk(in.x, k0, K);
 #pragma unroll
-        for (int mt = 0; mt < HC; ++mt) x[mt] = mfma_chunk(ld4(P + base + (int64_t)(mt * 16 + col) * KP + k0), xin, x[mt]);
+        for (int mt = 0; mt < HC; ++mt) x[mt] = mfma_chunk(ld4(base + (int64_t)mt * 16 * ld + kc * 16), xin, x[mt]);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // fc1 + ReLU + GRUCell for one tile; h (HC chunks, D layout) updated in place.
 template <int H, bool DENSE = false>
-__device__ __forceinline__ void agent_cell_hidden(const float* __restrict__ P, const AgentLayout& L, const RowIn& in,
+__device__ __forceinline__ void agent_cell_hidden(const WView& W, const AgentLayout& L, const RowIn& in,
                                                   floatx4 (&h)[H / 16], int lane) {
     constexpr int HC = H / 16;
     const int col = lane & 15, g = lane >> 4;
+    const float* P = W.p;
     floatx4 x[HC];
-    agent_fc1<H, DENSE>(P, L, in, x, lane);
+    agent_fc1<H, DENSE>(W, L, in, x, lane);
 #pragma unroll
     for (int mt = 0; mt < HC; ++mt)
 #pragma unroll
@@ -129,23 +207,24 @@ __device__ __forceinline__ void agent_cell_hidden(const float* __restrict__ P, c
     //   r = sig(W_ir x + W_hr h + b_ir + b_hr), z likewise, n = tanh(W_in x + b_in + r (W_hn h + b_hn)),
     //   h' = (h - n) z + n   (PyTorch GRUCell gate order and formula)
     floatx4 hn[HC];
+    const int64_t gate = (int64_t)H * W.ldh;  // row offset between the r, z and n blocks
 #pragma unroll
     for (int mt = 0; mt < HC; ++mt) {
-        floatx4 ar = ld4(P + L.brz + mt * 16 + 4 * g);
-        floatx4 az = ld4(P + L.brz + H + mt * 16 + 4 * g);
-        floatx4 ain = ld4(P + L.bih + 2 * H + mt * 16 + 4 * g);
-        floatx4 ahn = ld4(P + L.bhh + 2 * H + mt * 16 + 4 * g);
-        const float* wr_i = P + L.wih + (int64_t)(mt * 16 + col) * H + 4 * g;
-        const float* wr_h = P + L.whh + (int64_t)(mt * 16 + col) * H + 4 * g;
+        floatx4 ar = ld4(P + W.brz + mt * 16 + 4 * g);
+        floatx4 az = ld4(P + W.brz + H + mt * 16 + 4 * g);
+        floatx4 ain = ld4(P + W.bih + 2 * H + mt * 16 + 4 * g);
+        floatx4 ahn = ld4(P + W.bhh + 2 * H + mt * 16 + 4 * g);
+        const float* wr_i = P + W.wih + (int64_t)(mt * 16 + col) * W.ldh + 4 * g;
+        const float* wr_h = P + W.whh + (int64_t)(mt * 16 + col) * W.ldh + 4 * g;
 #pragma unroll
         for (int kc = 0; kc < HC; ++kc) {
             const int k0 = kc * 16;
             ar = mfma_chunk(ld4(wr_i + k0), x[kc], ar);
-            az = mfma_chunk(ld4(wr_i + (int64_t)H * H + k0), x[kc], az);
-            ain = mfma_chunk(ld4(wr_i + (int64_t)2 * H * H + k0), x[kc], ain);
+            az = mfma_chunk(ld4(wr_i + gate + k0), x[kc], az);
+            ain = mfma_chunk(ld4(wr_i + 2 * gate + k0), x[kc], ain);
             ar = mfma_chunk(ld4(wr_h + k0), h[kc], ar);
-            az = mfma_chunk(ld4(wr_h + (int64_t)H * H + k0), h[kc], az);
-            ahn = mfma_chunk(ld4(wr_h + (int64_t)2 * H * H + k0), h[kc], ahn);
+            az = mfma_chunk(ld4(wr_h + gate + k0), h[kc], az);
+            ahn = mfma_chunk(ld4(wr_h + 2 * gate + k0), h[kc], ahn);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -162,14 +241,13 @@ __device__ __forceinline__ void agent_cell_hidden(const float* __restrict__ P, c
 
 // fc2 for action tile at (16 actions starting at 16*at): q (D layout) for this lane's row.
 template <int H>
-__device__ __forceinline__ floatx4 agent_q_tile(const float* __restrict__ P, const AgentLayout& L, const floatx4 (&h)[H / 16],
-                                                int at, int lane) {
+__device__ __forceinline__ floatx4 agent_q_tile(const WView& W, const floatx4 (&h)[H / 16], int at, int lane) {
     constexpr int HC = H / 16;
     const int col = lane & 15, g = lane >> 4;
-    floatx4 q = ld4(P + L.b2 + at * 16 + 4 * g);
+    floatx4 q = ld4(W.p + W.b2 + at * 16 + 4 * g);
 #pragma unroll
     for (int kc = 0; kc < HC; ++kc)
-        q = mfma_chunk(ld4(P + L.w2 + (int64_t)(at * 16 + col) * H + kc * 16 + 4 * g), h[kc], q);
+        q = mfma_chunk(ld4(W.p + W.w2 + (int64_t)(at * 16 + col) * W.ldh + kc * 16 + 4 * g), h[kc], q);
     return q;
 }
 

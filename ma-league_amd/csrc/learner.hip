@@ -997,8 +997,8 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
         Mtg = ptrs(tparams, ws + p.w.mix_tg);
     }
     // d2 is sparse: zero it (and dq) every call
-    hipMemsetAsync(ws + p.w.d2, 0, sizeof(float) * (size_t)c.T * c.R * c.A, s);
-    hipMemsetAsync(ws + p.w.dq, 0, sizeof(float) * (size_t)c.T * c.R, s);
+    (void)hipMemsetAsync(ws + p.w.d2, 0, sizeof(float) * (size_t)c.T * c.R * c.A, s);
+    (void)hipMemsetAsync(ws + p.w.dq, 0, sizeof(float) * (size_t)c.T * c.R, s);
     hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + p.w.msum);
     const int ntiles = (c.R + 15) / 16;
     const int threads = (c.H / 16) * 64;

@@ -75,25 +75,67 @@ __device__ __forceinline__ void write_obs_item(const EnvTables& T, const MlgEnvS
     *reinterpret_cast<floatx4*>(dst + 4) = floatx4{o[4], o[5], o[6], o[7]};
 }
 
-template <int H, int TPW>
+// Dynamic-LDS carve of the rollout workgroup (4-byte words; every region 16-byte aligned).
+struct RolloutLds {
+    int64_t wts, spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, any, total;
+    LdsWeights lw;
+    int weights_in_lds;
+};
+
+__host__ __device__ inline RolloutLds make_rollout_lds(const AgentLayout& L, int U, int n_agents, bool weights_in_lds) {
+    RolloutLds r;
+    r.lw = make_lds_weights(L);
+    r.weights_in_lds = weights_in_lds;
+    int64_t o = 0;
+    auto take = [&](int64_t n) { int64_t v = o; o += mlg_align4(n); return v; };
+    r.wts = take(weights_in_lds ? r.lw.total : 0);
+    r.spec = take((int64_t)(sizeof(SpecShared) / 4));
+    const int64_t eu = (int64_t)RE * U;
+    r.x = take(eu);
+    r.y = take(eu);
+    r.hp = take(eu);
+    r.nhp = take(eu);
+    r.act = take(eu);
+    r.pact = take((int64_t)RE * n_agents);
+    r.prev = take((int64_t)RE * n_agents);
+    r.status = take(RE);
+    r.stepped = take(RE);
+    r.len = take(RE);
+    r.episode = take(RE);
+    r.ret = take(RE);
+    r.any = take(1);
+    r.total = o;
+    return r;
+}
+
+template <int H, int TPW, bool WLDS>
 __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
                                                      const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
-                                                     float eps, int test_mode) {
+                                                     float eps, int test_mode, RolloutLds lay) {
     constexpr int HC = H / 16;
-    __shared__ SpecShared SS;
-    __shared__ int s_x[RE][MLG_MAXU], s_y[RE][MLG_MAXU], s_hp[RE][MLG_MAXU], s_nhp[RE][MLG_MAXU];
-    __shared__ int s_act[RE][MLG_MAXU], s_pact[RE][MLG_MAXU], s_prev[RE][MLG_MAXU];
-    __shared__ int s_status[RE], s_stepped[RE], s_len[RE];
-    __shared__ uint32_t s_episode[RE];
-    __shared__ float s_ret[RE];
-    __shared__ int s_any;
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    SpecShared& SS = *reinterpret_cast<SpecShared*>(smem + lay.spec);
+    const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U;
+    int* s_x = smem + lay.x;
+    int* s_y = smem + lay.y;
+    int* s_hp = smem + lay.hp;
+    int* s_nhp = smem + lay.nhp;
+    int* s_act = smem + lay.act;
+    int* s_pact = smem + lay.pact;
+    int* s_prev = smem + lay.prev;
+    int* s_status = smem + lay.status;
+    int* s_stepped = smem + lay.stepped;
+    int* s_len = smem + lay.len;
+    uint32_t* s_episode = reinterpret_cast<uint32_t*>(smem + lay.episode);
+    float* s_ret = reinterpret_cast<float*>(smem + lay.ret);
+    int& s_any = smem[lay.any];
 
     const int tid = threadIdx.x, nthr = blockDim.x;
     const int lane = tid & 63, wave = tid >> 6, W = nthr >> 6;
     const int e0 = blockIdx.x * RE;
-    const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U;
     const int B = bt.B, T1 = bt.T1;
     load_spec_tables(spec, SS);
+    if (WLDS) load_weights_to_lds(P, L, lay.lw, reinterpret_cast<float*>(smem + lay.wts));
     const EnvTables T = make_tables(spec, SS);
     const float inv_p = 1.0f / (float)pow2_at_least(spec.grid);
 
@@ -118,8 +160,8 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         const int e = i / U, u = i % U;
         if (s_status[e] == 2) continue;
         const int tm = SS.team[u];
-        env_spawn_unit(T, mlg_env_key(spec.seed, e0 + e), s_episode[e], u, SS.team_first[tm], SS.team_size[tm], s_x[e],
-                       s_y[e], s_hp[e]);
+        env_spawn_unit(T, mlg_env_key(spec.seed, e0 + e), s_episode[e], u, SS.team_first[tm], SS.team_size[tm],
+                       s_x + e * U, s_y + e * U, s_hp + e * U);
     }
     __syncthreads();
     // observation at t = 0
@@ -127,13 +169,13 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         const int e = i / (N * U), r = i % (N * U);
         if (s_status[e] == 2) continue;
         const int64_t b = e0 + e;
-        write_obs_item(T, spec, s_x[e], s_y[e], s_hp[e], bt.obs + b * T1 * N * DO, r / U, r % U, inv_p);
+        write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U, bt.obs + b * T1 * N * DO, r / U, r % U, inv_p);
     }
     for (int i = tid; i < RE * U; i += nthr) {
         const int e = i / U, j = i % U;
         if (s_status[e] == 2) continue;
         float o[6];
-        env_state_feat(T, s_x[e], s_y[e], s_hp[e], j, inv_p, o);
+        env_state_feat(T, s_x + e * U, s_y + e * U, s_hp + e * U, j, inv_p, o);
         float* dst = bt.state + (int64_t)(e0 + e) * T1 * S + j * 6;
 #pragma unroll
         for (int f = 0; f < 6; ++f) dst[f] = o[f];
@@ -142,7 +184,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         const int e = i / (N * A), r = i % (N * A);
         if (s_status[e] == 2) continue;
         bt.avail[(int64_t)(e0 + e) * T1 * N * A + r] =
-            env_avail_one(T, s_x[e], s_y[e], s_hp[e], spec.agent_unit[r / A], r % A);
+            env_avail_one(T, s_x + e * U, s_y + e * U, s_hp + e * U, spec.agent_unit[r / A], r % A);
     }
     __syncthreads();
 
@@ -166,22 +208,24 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             const int e = row / N, n = row % N;
             const bool valid = row < RE * N && s_status[e] < 2;
             if (!__any(valid)) continue;  // wave-uniform skip of finished tiles
-            // Launder the weight pointer per tile: stops LICM/CSE from keeping t- and tile-invariant
-            // weight loads live in (spilled) registers; they are L1/L2 hits every step instead.
-            const float* Pt = P;
-            asm volatile("" : "+s"(Pt));
+            // Opaque zero offset per tile: stops LICM/CSE from keeping t- and tile-invariant weight loads
+            // live across the episode loop in (spilled) registers.
+            int zero = 0;
+            asm volatile("" : "+s"(zero));
+            const WView Wv = WLDS ? lds_view(reinterpret_cast<const float*>(smem + lay.wts) + zero, lay.lw, L)
+                                  : global_view(P + zero, L);
             const int64_t b = e0 + e;
             const int64_t bt_off = valid ? (b * T1 + t) * N + n : 0;
             RowIn in;
             in.x = valid ? bt.obs + bt_off * DO : nullptr;
             in.onehot = nullptr;
-            in.prev_action = (valid && t > 0) ? s_prev[e][n] : -1;
+            in.prev_action = (valid && t > 0) ? s_prev[e * N + n] : -1;
             in.agent = valid ? n : 0;
-            agent_cell_hidden<H>(Pt, L, in, h[ti], lane);
+            agent_cell_hidden<H>(Wv, L, in, h[ti], lane);
             const int32_t* av = valid ? bt.avail + bt_off * A : nullptr;
             ArgmaxState as{-INFINITY, 1 << 30};
             for (int at = 0; at < n_at; ++at) {
-                const floatx4 q = agent_q_tile<H>(Pt, L, h[ti], at, lane);
+                const floatx4 q = agent_q_tile<H>(Wv, h[ti], at, lane);
                 argmax_accumulate(as, q, av, at, A, lane);
             }
             int act = argmax_reduce(as);
@@ -194,7 +238,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                         act = random_available(av, A, r2);
                     }
                 }
-                s_pact[e][n] = act;
+                s_pact[e * N + n] = act;
                 bt.actions[bt_off] = act;
                 bt.actions_onehot[bt_off * A + act] = 1.0f;
             }
@@ -205,14 +249,15 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             const int e = i / U, u = i % U;
             if (s_status[e] != 0) continue;
             const int ag = SS.agent[u];
-            s_act[e][u] = env_exec_action(T, s_x[e], s_y[e], s_hp[e], u, ag ? (int64_t)s_pact[e][ag - 1] : 0);
+            s_act[e * U + u] = env_exec_action(T, s_x + e * U, s_y + e * U, s_hp + e * U, u,
+                                               ag ? (int64_t)s_pact[e * N + ag - 1] : 0);
         }
         __syncthreads();
         for (int i = tid; i < RE * U; i += nthr) {
             const int e = i / U, j = i % U;
             if (s_status[e] != 0) continue;
-            s_nhp[e][j] = env_resolve_hp(T, s_act[e], s_hp[e], j);
-            if (s_hp[e][j] > 0) env_apply_move(s_act[e][j], &s_x[e][j], &s_y[e][j]);
+            s_nhp[e * U + j] = env_resolve_hp(T, s_act + e * U, s_hp + e * U, j);
+            if (s_hp[e * U + j] > 0) env_apply_move(s_act[e * U + j], &s_x[e * U + j], &s_y[e * U + j]);
         }
         __syncthreads();
         for (int e = tid; e < RE; e += nthr) {
@@ -220,7 +265,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             const int status = s_status[e];
             s_stepped[e] = 0;
             if (status == 2) continue;
-            for (int n = 0; n < N; ++n) s_prev[e][n] = s_pact[e][n];
+            for (int n = 0; n < N; ++n) s_prev[e * N + n] = s_pact[e * N + n];
             if (status == 1) {  // final action recorded; env done (parallel_stepper.py:153)
                 s_status[e] = 2;
                 continue;
@@ -228,13 +273,13 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             int alive[2] = {0, 0}, lost[2] = {0, 0}, kills[2] = {0, 0};
             for (int j = 0; j < U; ++j) {
                 const int tm = SS.team[j];
-                const int h0 = s_hp[e][j], h1 = s_nhp[e][j];
+                const int h0 = s_hp[e * U + j], h1 = s_nhp[e * U + j];
                 if (h0 > 0) {
                     lost[tm] += h0 - h1 > 0 ? h0 - h1 : 0;
                     if (h1 == 0) kills[1 - tm] += 1;
                 }
                 if (h1 > 0) alive[tm] += 1;
-                s_hp[e][j] = h1;
+                s_hp[e * U + j] = h1;
             }
             const int done = alive[0] == 0 || alive[1] == 0 || t + 1 >= spec.episode_limit;
             int won[2];
@@ -262,13 +307,14 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             const int e = i / (N * U), r = i % (N * U);
             if (!s_stepped[e]) continue;
             const int64_t b = e0 + e;
-            write_obs_item(T, spec, s_x[e], s_y[e], s_hp[e], bt.obs + (b * T1 + t + 1) * N * DO, r / U, r % U, inv_p);
+            write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U, bt.obs + (b * T1 + t + 1) * N * DO, r / U,
+                           r % U, inv_p);
         }
         for (int i = tid; i < RE * U; i += nthr) {
             const int e = i / U, j = i % U;
             if (!s_stepped[e]) continue;
             float o[6];
-            env_state_feat(T, s_x[e], s_y[e], s_hp[e], j, inv_p, o);
+            env_state_feat(T, s_x + e * U, s_y + e * U, s_hp + e * U, j, inv_p, o);
             float* dst = bt.state + ((int64_t)(e0 + e) * T1 + t + 1) * S + j * 6;
 #pragma unroll
             for (int f = 0; f < 6; ++f) dst[f] = o[f];
@@ -277,7 +323,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             const int e = i / (N * A), r = i % (N * A);
             if (!s_stepped[e]) continue;
             bt.avail[((int64_t)(e0 + e) * T1 + t + 1) * N * A + r] =
-                env_avail_one(T, s_x[e], s_y[e], s_hp[e], spec.agent_unit[r / A], r % A);
+                env_avail_one(T, s_x + e * U, s_y + e * U, s_hp + e * U, spec.agent_unit[r / A], r % A);
         }
         if (tid == 0) {
             int any = 0;
@@ -299,9 +345,9 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         const int e = i / U, u = i % U;
         const int64_t b = e0 + e;
         if (b >= B) continue;
-        st.x[b * U + u] = s_x[e][u];
-        st.y[b * U + u] = s_y[e][u];
-        st.hp[b * U + u] = s_hp[e][u];
+        st.x[b * U + u] = s_x[e * U + u];
+        st.y[b * U + u] = s_y[e * U + u];
+        st.hp[b * U + u] = s_hp[e * U + u];
     }
 }
 
@@ -418,10 +464,31 @@ int check_state(const MlgEnvState* st) {
     return 0;
 }
 
+constexpr int LDS_LIMIT_BYTES = 160 * 1024;
+
+template <int H, int TPW, bool WLDS>
+int launch_rollout_t(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st,
+                     const AgentLayout& L, const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
+                     const RolloutLds& lay) {
+    const size_t bytes = (size_t)lay.total * 4;
+    auto kern = rollout_kernel<H, TPW, WLDS>;
+    if (bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)bytes);
+        if (e != hipSuccess) return mlg::fail("rollout: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
+    return 0;
+}
+
 template <int H, int TPW>
-void launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st,
-                    const AgentLayout& L, const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm) {
-    hipLaunchKernelGGL((rollout_kernel<H, TPW>), dim3(grid), dim3(threads), 0, s, spec, st, L, P, bt, info, eps, tm);
+int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st,
+                   const AgentLayout& L, const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm) {
+    RolloutLds lay = make_rollout_lds(L, spec.U, spec.n_agents, true);
+    if (lay.total * 4 <= LDS_LIMIT_BYTES && !getenv("MLG_ROLLOUT_GLOBAL_WEIGHTS"))
+        return launch_rollout_t<H, TPW, true>(grid, threads, s, spec, st, L, P, bt, info, eps, tm, lay);
+    lay = make_rollout_lds(L, spec.U, spec.n_agents, false);
+    return launch_rollout_t<H, TPW, false>(grid, threads, s, spec, st, L, P, bt, info, eps, tm, lay);
 }
 
 }  // namespace
@@ -474,7 +541,8 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
     const int threads = W * 64;
     hipStream_t s = (hipStream_t)stream;
     const float eps = test_mode ? 0.f : epsilon;
-#define MLG_RO(HH, TT) launch_rollout<HH, TT>(grid, threads, s, *spec, *st, L, packed, *batch, *info, eps, test_mode)
+    int rc = 0;
+#define MLG_RO(HH, TT) rc = launch_rollout<HH, TT>(grid, threads, s, *spec, *st, L, packed, *batch, *info, eps, test_mode)
     if (dims->hidden == 64) {
         if (tpw == 1) MLG_RO(64, 1);
         else if (tpw == 2) MLG_RO(64, 2);
@@ -494,5 +562,6 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
         return mlg::fail("rollout: rnn_hidden_dim=%d unsupported (32, 64, 128)", dims->hidden);
     }
 #undef MLG_RO
+    if (rc) return rc;
     return mlg::check_launch("rollout_kernel");
 }

@@ -47,14 +47,15 @@ class MainLogger:
     def collect(self, key: Collectibles, data, origin: Originator = None, parallel=False):
         name = (("test_" if self.test_mode else "") + (f"{origin.value}_" if origin is not None else "") + key.value)
         if parallel and isinstance(data, (list, tuple, np.ndarray)):
-            self._buf[(key, name)].extend(list(data))
+            self._buf[(key, name)].append(np.asarray(data))
         else:
-            self._buf[(key, name)].append(data)
+            self._buf[(key, name)].append(np.asarray([data]))
 
     def log(self, t_env):
         if t_env - self._last_log_t < self.log_interval:
             return
-        for (key, name), values in self._buf.items():
+        for (key, name), chunks in self._buf.items():
+            values = np.concatenate(chunks) if chunks else np.zeros(0)
             for suffix, fn in _AGG.get(key, []):
                 if len(values):
                     self.log_stat(f"{name}_{suffix}", float(fn(values)), t_env)

@@ -8,8 +8,10 @@ summary (episode length, return, won/draw) for t_env and the logger.
 """
 from __future__ import annotations
 
+from collections.abc import Sequence
 from functools import partial
 
+import numpy as np
 import torch
 
 from .. import _native
@@ -18,6 +20,22 @@ from ..components.episode_batch import EpisodeBatch
 from ..custom_logging import Collectibles, Originator
 from ..envs.teams_env import TeamsEnvSpec, VecEnvState
 from ..exceptions import MultiAgentControllerNotInitialized
+
+
+class EnvInfos(Sequence):
+    """The per-run list of env_info dicts (``{"battle_won": [home, away], "draw": bool}``) in order of
+    termination, materialised on access (a plain list of 4096 dicts per run costs milliseconds of host time)."""
+
+    def __init__(self, won, draw):
+        self.won, self.draw = won, draw
+
+    def __len__(self):
+        return len(self.draw)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        return {"battle_won": [bool(self.won[i, 0]), bool(self.won[i, 1])], "draw": bool(self.draw[i])}
 
 
 class EnvStepper:
@@ -56,6 +74,7 @@ class ParallelStepper(EnvStepper):
         self.home_mac = None
         self.home_batch = None
         self.last_run = None
+        self.timing = None  # list -> (start, end) HIP events around every rollout launch (bench.py)
 
     def initialize(self, scheme, groups, preprocess, home_mac, away_mac=None):
         if away_mac is not None:
@@ -88,9 +107,17 @@ class ParallelStepper(EnvStepper):
         agent = self.home_mac.agent
         d = agent.dims()
         st = self.envs.to_c()
+        packed = agent.packed()
+        ev = None
+        if self.timing is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         _native.call("mlg_rollout", _native.byref(self._cspec), _native.byref(st), _native.byref(d),
-                     _native.ptr(agent.packed()), _native.byref(mb), _native.byref(run_info), float(epsilon),
+                     _native.ptr(packed), _native.byref(mb), _native.byref(run_info), float(epsilon),
                      int(bool(test_mode)), _native.stream_ptr(self.device))
+        if ev is not None:
+            ev[1].record()
+            self.timing.append(ev)
         del keep
 
     def run(self, test_mode=False):
@@ -106,26 +133,24 @@ class ParallelStepper(EnvStepper):
             sel.epsilon = 0.0
         self._launch(self.home_batch, eps, test_mode)
         B = self.batch_size
-        host = self._info.cpu()
+        host = self._info.cpu().numpy()
         ep_len = host[0:B]
-        won = host[B:3 * B].view(B, 2)
-        draw = host[3 * B:4 * B]
-        ret = host[4 * B:5 * B].view(torch.float32)
+        won = host[B:3 * B].reshape(B, 2).astype(bool)
+        draw = host[3 * B:4 * B].astype(bool)
+        ret = host[4 * B:5 * B].view(np.float32)
         self.t = int(ep_len.max())
         if not test_mode:
             self.env_steps_this_run = int(ep_len.sum())
             self.t_env += self.env_steps_this_run
         # env_infos in order of termination (parallel_stepper.py:124,183-184): by episode length, then env index
-        order = sorted(range(B), key=lambda i: (int(ep_len[i]), i))
-        won_l, draw_l = won.tolist(), draw.tolist()
-        env_infos = [{"battle_won": [bool(won_l[i][0]), bool(won_l[i][1])], "draw": bool(draw_l[i])} for i in order]
-        self.last_run = {"ep_len": ep_len, "returns": ret}
-        self.logger.collect(Collectibles.RETURN, ret.tolist(), origin=Originator.HOME, parallel=True)
-        self.logger.collect(Collectibles.WON, [e["battle_won"][0] for e in env_infos], origin=Originator.HOME,
-                            parallel=True)
-        self.logger.collect(Collectibles.WON, [e["battle_won"][1] for e in env_infos], origin=Originator.AWAY,
-                            parallel=True)
-        self.logger.collect(Collectibles.DRAW, [e["draw"] for e in env_infos], parallel=True)
+        order = np.lexsort((np.arange(B), ep_len))
+        env_infos = EnvInfos(won[order], draw[order])
+        self.last_run = {"ep_len": torch.from_numpy(ep_len.copy()), "returns": torch.from_numpy(ret.copy()),
+                         "order": order}
+        self.logger.collect(Collectibles.RETURN, ret.astype(np.float64), origin=Originator.HOME, parallel=True)
+        self.logger.collect(Collectibles.WON, won[order, 0], origin=Originator.HOME, parallel=True)
+        self.logger.collect(Collectibles.WON, won[order, 1], origin=Originator.AWAY, parallel=True)
+        self.logger.collect(Collectibles.DRAW, draw[order], parallel=True)
         self.logger.collect(Collectibles.STEPS, self.t, parallel=True)
         self.logger.log(self.t_env)
         return self.home_batch, env_infos

@@ -1,0 +1,99 @@
+"""CPU baseline for bench.py (TEST INFRASTRUCTURE / BASELINE ONLY -- never the measured product).
+
+The reference's hot path restated on the host: the ParallelStepper bookkeeping (stepper_ref.run), the
+synthetic env in C (env_ref.c via ctypes, one call per env per step like EnvWorker), the DRQN agent
+forward batched over all B*N rows per step in PyTorch-CPU (basic_controller.py:38-50), epsilon-greedy,
+and one QLearner.train (learner_ref.QLearnerRef, PyTorch-CPU autograd + RMSprop) on 32 sampled episodes
+per run -- the loop shape of ma_experiment.py:224-241. Runs for a bounded wall-clock sample.
+"""
+from __future__ import annotations
+
+import os
+import time
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+import envref
+import learner_ref as LR
+import stepper_ref as SR
+
+PLAN_MEDIUM_1H_4T = {"team": [0] * 5 + [1] * 5, "role": [0, 0, 1, 0, 0] * 2, "melee": [0] * 10,
+                     "scripted": [True, False]}
+
+
+def _init_params(d_in, H, A, N, S, E=32, HE=64, seed=0):
+    torch.manual_seed(seed)
+    fc1, gru, fc2 = torch.nn.Linear(d_in, H), torch.nn.GRUCell(H, H), torch.nn.Linear(H, A)
+    agent = {"fc1.weight": fc1.weight, "fc1.bias": fc1.bias, "gru.weight_ih": gru.weight_ih,
+             "gru.weight_hh": gru.weight_hh, "gru.bias_ih": gru.bias_ih, "gru.bias_hh": gru.bias_hh,
+             "fc2.weight": fc2.weight, "fc2.bias": fc2.bias}
+    mix = {}
+    for name, shapes in [("hyper_w_1", [(HE, S), (N * E, HE)]), ("hyper_w_final", [(HE, S), (E, HE)])]:
+        l0, l2 = torch.nn.Linear(shapes[0][1], shapes[0][0]), torch.nn.Linear(shapes[1][1], shapes[1][0])
+        mix.update({f"{name}.0.weight": l0.weight, f"{name}.0.bias": l0.bias, f"{name}.2.weight": l2.weight,
+                    f"{name}.2.bias": l2.bias})
+    hb, v0, v2 = torch.nn.Linear(S, E), torch.nn.Linear(S, E), torch.nn.Linear(E, 1)
+    mix.update({"hyper_b_1.weight": hb.weight, "hyper_b_1.bias": hb.bias, "V.0.weight": v0.weight,
+                "V.0.bias": v0.bias, "V.2.weight": v2.weight, "V.2.bias": v2.bias})
+    det = lambda d: {k: v.detach().numpy().copy() for k, v in d.items()}  # noqa: E731
+    return det(agent), det(mix)
+
+
+def run(seconds=15.0, B=64, episode_limit=100, eps=0.05, threads=None, seed=0, batch_size=32, capacity=512):
+    threads = threads or os.cpu_count()
+    torch.set_num_threads(threads)
+    p = PLAN_MEDIUM_1H_4T
+    U, N = 10, 5
+    A, d_obs, S = 5 + U, 8 * U, 6 * U
+    d_in = d_obs + A + N
+    agent, mix = _init_params(d_in, 64, A, N, S, seed=seed)
+    args = SimpleNamespace(n_agents=N, n_actions=A, mixer="qmix", mixing_embed_dim=32, hypernet_layers=2,
+                           double_q=True, gamma=0.99, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10,
+                           target_update_interval=200, obs_last_action=True, obs_agent_id=True)
+    learner = LR.QLearnerRef(agent, mix, args)
+    envs = SR.RefVecEnv([envref.RefEnv(p["team"], p["role"], p["melee"], p["scripted"], episode_limit=episode_limit,
+                                       seed=seed, env_index=b) for b in range(B)])
+    T1 = episode_limit + 1
+    eye = torch.eye(N).unsqueeze(0).expand(B, -1, -1).reshape(B * N, N)
+    buffer, rng = [], np.random.RandomState(seed)
+    env_steps, runs, trains = 0, 0, 0
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < seconds:
+        h = [torch.zeros(B * N, 64)]
+
+        def policy(t, ids, batch):
+            obs = torch.from_numpy(batch["obs"][:, t].reshape(B * N, d_obs))
+            last = torch.from_numpy(batch["actions_onehot"][:, t - 1].reshape(B * N, A)) if t > 0 \
+                else torch.zeros(B * N, A)
+            with torch.no_grad():
+                q, h[0] = LR.drqn_forward(learner.p, torch.cat([obs, last, eye], 1), h[0])
+            q = q.view(B, N, A)[ids]
+            av = torch.from_numpy(batch["avail_actions"][ids, t])
+            a = LR.greedy_select(q, av).numpy()
+            coin = rng.rand(*a.shape) < eps
+            for (k, n) in zip(*np.nonzero(coin)):
+                a[k, n] = rng.choice(np.nonzero(av[k, n].numpy())[0])
+            return a
+
+        res = SR.run(envs, policy, B, T1, N, A, d_obs, S)
+        env_steps += res["env_steps"]
+        runs += 1
+        for b in range(B):
+            buffer.append({k: v[b] for k, v in res["batch"].items()})
+        del buffer[:-capacity]
+        if len(buffer) >= batch_size:
+            idx = rng.choice(len(buffer), batch_size, replace=False)
+            smp = {k: torch.from_numpy(np.stack([buffer[i][k] for i in idx])) for k in buffer[0]}
+            T = int(smp["filled"].sum(1).max())
+            smp = {k: v[:, :T].clone() for k, v in smp.items()}
+            learner.train(smp, env_steps, runs * B)
+            trains += 1
+    elapsed = time.perf_counter() - t_start
+    return {"value": env_steps / elapsed, "env_steps": env_steps, "seconds": elapsed, "runs": runs, "trains": trains,
+            "cores": threads, "B": B}
+
+
+if __name__ == "__main__":
+    print(run(seconds=10))
