@@ -17,6 +17,21 @@
 #include "agent_device.h"
 #include "mlg_host.h"
 
+#ifdef MLG_STAMPS
+// Diagnostic build only (-DMLG_STAMPS, libmaleague_stamps.so): per-wave cycle shares of the rollout phases.
+__device__ unsigned long long* g_mlg_stamps = nullptr;
+#define MLG_STAMP(k)                                             \
+    do {                                                         \
+        const unsigned long long _now = __builtin_amdgcn_s_memtime(); \
+        st_acc[k] += _now - st_last;                             \
+        st_last = _now;                                          \
+    } while (0)
+#else
+#define MLG_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 namespace {
 
 constexpr int RE = 16;  // envs per workgroup
@@ -193,6 +208,11 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     for (int ti = 0; ti < TPW; ++ti)
 #pragma unroll
         for (int c = 0; c < HC; ++c) h[ti][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+#ifdef MLG_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+    const unsigned long long st_begin = st_last;
+#endif
 
     const int n_tiles = (RE * N + 15) / 16;
     const int col = lane & 15, g = lane >> 4;
@@ -243,7 +263,9 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                 bt.actions_onehot[bt_off * A + act] = 1.0f;
             }
         }
+        MLG_STAMP(0);
         __syncthreads();
+        MLG_STAMP(1);
         // ================= env phase (status 0 envs) ===========================================
         for (int i = tid; i < RE * U; i += nthr) {
             const int e = i / U, u = i % U;
@@ -253,6 +275,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                                                ag ? (int64_t)s_pact[e * N + ag - 1] : 0);
         }
         __syncthreads();
+        MLG_STAMP(2);
         for (int i = tid; i < RE * U; i += nthr) {
             const int e = i / U, j = i % U;
             if (s_status[e] != 0) continue;
@@ -260,6 +283,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             if (s_hp[e * U + j] > 0) env_apply_move(s_act[e * U + j], &s_x[e * U + j], &s_y[e * U + j]);
         }
         __syncthreads();
+        MLG_STAMP(3);
         for (int e = tid; e < RE; e += nthr) {
             const int b = e0 + e;
             const int status = s_status[e];
@@ -302,6 +326,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             }
         }
         __syncthreads();
+        MLG_STAMP(4);
         // observation at t + 1 for envs that stepped (incl. those that just terminated)
         for (int i = tid; i < RE * N * U; i += nthr) {
             const int e = i / (N * U), r = i % (N * U);
@@ -331,8 +356,17 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             s_any = any;
         }
         __syncthreads();
+        MLG_STAMP(5);
         if (!s_any) break;
     }
+#ifdef MLG_STAMPS
+    if (lane == 0 && g_mlg_stamps) {
+        unsigned long long* o = g_mlg_stamps + ((int64_t)blockIdx.x * 8 + wave) * 8;
+        for (int k = 0; k < 6; ++k) o[k] = st_acc[k];
+        o[6] = __builtin_amdgcn_s_memtime() - st_begin;
+        o[7] = 1;
+    }
+#endif
     // ---- per-env summary + env state write-back ----
     for (int e = tid; e < RE; e += nthr) {
         const int b = e0 + e;
@@ -494,6 +528,17 @@ int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec,
 }  // namespace
 
 int check_agent_dims(const MlgAgentDims* d);  // agent.hip
+
+extern "C" int mlg_debug_set_stamps(void* ptr) {
+#ifdef MLG_STAMPS
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_mlg_stamps), &ptr, sizeof(ptr));
+    if (e != hipSuccess) return mlg::fail("set stamps: %s", hipGetErrorString(e));
+    return 0;
+#else
+    (void)ptr;
+    return mlg::fail("not a stamps build (-DMLG_STAMPS)");
+#endif
+}
 
 extern "C" int mlg_env_reset(const MlgEnvSpec* spec, MlgEnvState* st, void* stream) {
     if (check_spec(spec) || check_state(st)) return 1;

@@ -13,7 +13,8 @@ import os
 import torch
 
 MAXU = 64
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmaleague.so")
+_LIB_PATH = os.environ.get("MLG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                      "libmaleague.so")
 
 
 class NativeError(RuntimeError):
@@ -89,6 +90,7 @@ SIGNATURES = {
     "mlg_qlearner_param_counts": (ctypes.c_int64, [_P, _P, _P]),
     "mlg_qlearner_workspace_floats": (ctypes.c_int64, [_P]),
     "mlg_qlearner_train": (ctypes.c_int, [_P, _P, _P]),
+    "mlg_debug_set_stamps": (ctypes.c_int, [_P]),
     "mlg_last_error": (ctypes.c_char_p, []),
     "mlg_version": (ctypes.c_char_p, []),
 }
