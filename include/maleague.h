@@ -71,6 +71,10 @@ typedef struct {
     float *actions_onehot; /* [B][T1][N][A] */
     int64_t *filled;       /* [B][T1][1] */
     int32_t B, T1;
+    /* Ring mode (mlg_rollout only): env b writes slot (ring_slot0 + b) % ring_size of tensors that hold
+     * ring_size slots (the replay buffer itself -- zero-copy insert); full_write = 1 makes the kernel write
+     * every byte of the slots it owns (zeros included), so the caller need not zero-initialise them. */
+    int32_t ring_slot0, ring_size, full_write;
 } MlgBatch;
 
 /* Per-run episode summary written by mlg_rollout. */
@@ -110,6 +114,12 @@ int mlg_env_observe(const MlgEnvSpec *spec, const MlgEnvState *st, float *obs /*
  * (DecayThenFlatSchedule.eval(t_env)); test_mode forces epsilon 0. */
 int mlg_rollout(const MlgEnvSpec *spec, MlgEnvState *st, const MlgAgentDims *dims, const float *packed,
                 MlgBatch *batch, MlgRunInfo *info, float epsilon, int32_t test_mode, void *stream);
+
+/* Zero `count` EpisodeBatch slots starting at slot0 (mod ring_size) in every key -- one launch; the
+ * ring-mode pre-fill that replaces constructing a zero EpisodeBatch. slot_bytes[8] = bytes per slot of
+ * state, obs, actions, avail, reward, terminated, actions_onehot, filled. */
+int mlg_zero_slots_bytes(const MlgBatch *batch, const int64_t *slot_bytes, int32_t slot0, int32_t count,
+                         int32_t ring_size, void *stream);
 
 /* DRQN forward over R rows: q[R][A], h_out[R][H] from inputs[R][d_in], h_in[R][H]. */
 int mlg_agent_forward(const MlgAgentDims *d, const float *packed, const float *inputs, const float *h_in,

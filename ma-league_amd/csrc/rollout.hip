@@ -90,9 +90,41 @@ __device__ __forceinline__ void write_obs_item(const EnvTables& T, const MlgEnvS
     *reinterpret_cast<floatx4*>(dst + 4) = floatx4{o[4], o[5], o[6], o[7]};
 }
 
+// Zero every key of slots [t0, t1) of the envs of this workgroup that are done and did not step
+// (status 2, or stepped == 0 with status 2 after the final action): the full-write (ring) mode's
+// replacement for zero-initialising the EpisodeBatch.
+__device__ void zero_slots(const MlgBatch& bt, const int* s_slot, const int* s_status, const int* s_stepped, int e0,
+                           int B, int t0, int t1, int N, int A, int S, int DO) {
+    const int T1 = bt.T1;
+    const int per = S + N * DO + 2 * N * A + 2 * N + 3;  // words per slot (actions/filled are 2 words)
+    const int total = RE * (t1 - t0) * per;
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+        const int e = i / ((t1 - t0) * per), rem = i % ((t1 - t0) * per);
+        const int t = t0 + rem / per;
+        int k = rem % per;
+        if (e0 + e >= B || s_status[e] != 2 || s_stepped[e]) continue;
+        const int64_t sl = (int64_t)s_slot[e] * T1 + t;
+        if (k < S) { bt.state[sl * S + k] = 0.f; continue; }
+        k -= S;
+        if (k < N * DO) { bt.obs[sl * N * DO + k] = 0.f; continue; }
+        k -= N * DO;
+        if (k < N * A) { bt.avail[sl * N * A + k] = 0; continue; }
+        k -= N * A;
+        if (k < N * A) { bt.actions_onehot[sl * N * A + k] = 0.f; continue; }
+        k -= N * A;
+        if (k < N) { bt.actions[sl * N + k] = 0; continue; }
+        k -= N;
+        if (k < N) continue;  // (second word of the int64 actions, covered above)
+        k -= N;
+        if (k == 0) bt.reward[sl] = 0.f;
+        else if (k == 1) bt.terminated[sl] = 0;
+        else bt.filled[sl] = 0;
+    }
+}
+
 // Dynamic-LDS carve of the rollout workgroup (4-byte words; every region 16-byte aligned).
 struct RolloutLds {
-    int64_t wts, spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, any, total;
+    int64_t wts, spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, any, total;
     LdsWeights lw;
     int weights_in_lds;
 };
@@ -118,6 +150,7 @@ __host__ __device__ inline RolloutLds make_rollout_lds(const AgentLayout& L, int
     r.len = take(RE);
     r.episode = take(RE);
     r.ret = take(RE);
+    r.slot = take(RE);
     r.any = take(1);
     r.total = o;
     return r;
@@ -143,6 +176,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     int* s_len = smem + lay.len;
     uint32_t* s_episode = reinterpret_cast<uint32_t*>(smem + lay.episode);
     float* s_ret = reinterpret_cast<float*>(smem + lay.ret);
+    int* s_slot = smem + lay.slot;  // batch slot of env e (ring mode: the replay-buffer slot)
     int& s_any = smem[lay.any];
 
     const int tid = threadIdx.x, nthr = blockDim.x;
@@ -165,7 +199,9 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             st.episode[b] = ep + 1;
             s_episode[e] = ep;
             s_status[e] = 0;
-            bt.filled[(int64_t)b * T1] = 1;
+            const int sl = bt.ring_size > 0 ? (bt.ring_slot0 + b) % bt.ring_size : b;
+            s_slot[e] = sl;
+            bt.filled[(int64_t)sl * T1] = 1;
         } else {
             s_status[e] = 2;
         }
@@ -183,22 +219,22 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     for (int i = tid; i < RE * N * U; i += nthr) {
         const int e = i / (N * U), r = i % (N * U);
         if (s_status[e] == 2) continue;
-        const int64_t b = e0 + e;
-        write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U, bt.obs + b * T1 * N * DO, r / U, r % U, inv_p);
+        write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U, bt.obs + (int64_t)s_slot[e] * T1 * N * DO, r / U,
+                       r % U, inv_p);
     }
     for (int i = tid; i < RE * U; i += nthr) {
         const int e = i / U, j = i % U;
         if (s_status[e] == 2) continue;
         float o[6];
         env_state_feat(T, s_x + e * U, s_y + e * U, s_hp + e * U, j, inv_p, o);
-        float* dst = bt.state + (int64_t)(e0 + e) * T1 * S + j * 6;
+        float* dst = bt.state + (int64_t)s_slot[e] * T1 * S + j * 6;
 #pragma unroll
         for (int f = 0; f < 6; ++f) dst[f] = o[f];
     }
     for (int i = tid; i < RE * N * A; i += nthr) {
         const int e = i / (N * A), r = i % (N * A);
         if (s_status[e] == 2) continue;
-        bt.avail[(int64_t)(e0 + e) * T1 * N * A + r] =
+        bt.avail[(int64_t)s_slot[e] * T1 * N * A + r] =
             env_avail_one(T, s_x + e * U, s_y + e * U, s_hp + e * U, spec.agent_unit[r / A], r % A);
     }
     __syncthreads();
@@ -217,6 +253,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     const int n_tiles = (RE * N + 15) / 16;
     const int col = lane & 15, g = lane >> 4;
     const int n_at = L.Ap / 16;
+    int last_t = 0;
 
     for (int t = 0; t < T1; ++t) {
         // ================= agent phase: rows of envs with status 0 (running) or 1 (final action) ======
@@ -235,7 +272,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             const WView Wv = WLDS ? lds_view(reinterpret_cast<const float*>(smem + lay.wts) + zero, lay.lw, L)
                                   : global_view(P + zero, L);
             const int64_t b = e0 + e;
-            const int64_t bt_off = valid ? (b * T1 + t) * N + n : 0;
+            const int64_t bt_off = valid ? ((int64_t)s_slot[e] * T1 + t) * N + n : 0;
             RowIn in;
             in.x = valid ? bt.obs + bt_off * DO : nullptr;
             in.onehot = nullptr;
@@ -260,7 +297,10 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                 }
                 s_pact[e * N + n] = act;
                 bt.actions[bt_off] = act;
-                bt.actions_onehot[bt_off * A + act] = 1.0f;
+                if (bt.full_write)
+                    for (int k = 0; k < A; ++k) bt.actions_onehot[bt_off * A + k] = k == act ? 1.0f : 0.0f;
+                else
+                    bt.actions_onehot[bt_off * A + act] = 1.0f;
             }
         }
         MLG_STAMP(0);
@@ -292,6 +332,10 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             for (int n = 0; n < N; ++n) s_prev[e * N + n] = s_pact[e * N + n];
             if (status == 1) {  // final action recorded; env done (parallel_stepper.py:153)
                 s_status[e] = 2;
+                if (bt.full_write) {
+                    bt.reward[(int64_t)s_slot[e] * T1 + t] = 0.f;
+                    bt.terminated[(int64_t)s_slot[e] * T1 + t] = 0;
+                }
                 continue;
             }
             int alive[2] = {0, 0}, lost[2] = {0, 0}, kills[2] = {0, 0};
@@ -312,9 +356,9 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             const int pt = spec.policy_team;
             const int r_int = lost[1 - pt] + 10 * kills[pt] + 200 * won[pt];
             const float r = (float)r_int * 0.0625f;
-            bt.reward[(int64_t)b * T1 + t] = r;
-            bt.terminated[(int64_t)b * T1 + t] = (uint8_t)done;
-            bt.filled[(int64_t)b * T1 + t + 1] = 1;
+            bt.reward[(int64_t)s_slot[e] * T1 + t] = r;
+            bt.terminated[(int64_t)s_slot[e] * T1 + t] = (uint8_t)done;
+            bt.filled[(int64_t)s_slot[e] * T1 + t + 1] = 1;
             s_ret[e] += r;
             s_stepped[e] = 1;
             if (done) {
@@ -331,25 +375,26 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         for (int i = tid; i < RE * N * U; i += nthr) {
             const int e = i / (N * U), r = i % (N * U);
             if (!s_stepped[e]) continue;
-            const int64_t b = e0 + e;
-            write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U, bt.obs + (b * T1 + t + 1) * N * DO, r / U,
-                           r % U, inv_p);
+            write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U,
+                           bt.obs + ((int64_t)s_slot[e] * T1 + t + 1) * N * DO, r / U, r % U, inv_p);
         }
         for (int i = tid; i < RE * U; i += nthr) {
             const int e = i / U, j = i % U;
             if (!s_stepped[e]) continue;
             float o[6];
             env_state_feat(T, s_x + e * U, s_y + e * U, s_hp + e * U, j, inv_p, o);
-            float* dst = bt.state + ((int64_t)(e0 + e) * T1 + t + 1) * S + j * 6;
+            float* dst = bt.state + ((int64_t)s_slot[e] * T1 + t + 1) * S + j * 6;
 #pragma unroll
             for (int f = 0; f < 6; ++f) dst[f] = o[f];
         }
         for (int i = tid; i < RE * N * A; i += nthr) {
             const int e = i / (N * A), r = i % (N * A);
             if (!s_stepped[e]) continue;
-            bt.avail[((int64_t)(e0 + e) * T1 + t + 1) * N * A + r] =
+            bt.avail[((int64_t)s_slot[e] * T1 + t + 1) * N * A + r] =
                 env_avail_one(T, s_x + e * U, s_y + e * U, s_hp + e * U, spec.agent_unit[r / A], r % A);
         }
+        // full-write mode: slot t+1 of envs that are done (t+1 > episode length) gets zeros
+        if (bt.full_write && t + 1 < T1) zero_slots(bt, s_slot, s_status, s_stepped, e0, B, t + 1, t + 2, N, A, S, DO);
         if (tid == 0) {
             int any = 0;
             for (int e = 0; e < RE; ++e) any |= s_status[e] < 2;
@@ -357,6 +402,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         }
         __syncthreads();
         MLG_STAMP(5);
+        last_t = t;
         if (!s_any) break;
     }
 #ifdef MLG_STAMPS
@@ -367,6 +413,10 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         o[7] = 1;
     }
 #endif
+    // full-write mode: the remaining slots of every env (all of them are done here)
+    for (int e = tid; e < RE; e += nthr) s_stepped[e] = 0;
+    __syncthreads();
+    if (bt.full_write && last_t + 2 < T1) zero_slots(bt, s_slot, s_status, s_stepped, e0, B, last_t + 2, T1, N, A, S, DO);
     // ---- per-env summary + env state write-back ----
     for (int e = tid; e < RE; e += nthr) {
         const int b = e0 + e;
@@ -528,6 +578,65 @@ int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec,
 }  // namespace
 
 int check_agent_dims(const MlgAgentDims* d);  // agent.hip
+
+// ---- zero a range of EpisodeBatch slots (ring mode pre-fill): one launch over every key ----------------
+struct ZeroJobs {
+    unsigned char* base[16];
+    int64_t begin[16], end[16];  // byte ranges
+    int64_t words0[17];          // prefix sums of 16-byte words of each job's aligned interior
+    int n;
+};
+
+__global__ void zero_ranges_kernel(ZeroJobs J) {
+    const int64_t total = J.words0[J.n];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int j = 0;
+        while (j + 1 < J.n && J.words0[j + 1] <= i) ++j;
+        const int64_t a0 = (J.begin[j] + 15) & ~int64_t(15);
+        *reinterpret_cast<uint4*>(J.base[j] + a0 + (i - J.words0[j]) * 16) = make_uint4(0, 0, 0, 0);
+    }
+    // unaligned heads / tails (< 16 bytes each): one thread per job
+    if (blockIdx.x == 0 && threadIdx.x < J.n) {
+        const int j = threadIdx.x;
+        const int64_t a0 = (J.begin[j] + 15) & ~int64_t(15), a1 = J.end[j] & ~int64_t(15);
+        if (a0 >= a1) {
+            for (int64_t b = J.begin[j]; b < J.end[j]; ++b) J.base[j][b] = 0;
+        } else {
+            for (int64_t b = J.begin[j]; b < a0; ++b) J.base[j][b] = 0;
+            for (int64_t b = a1; b < J.end[j]; ++b) J.base[j][b] = 0;
+        }
+    }
+}
+
+extern "C" int mlg_zero_slots_bytes(const MlgBatch* bt, const int64_t* slot_bytes /*[8]*/, int32_t slot0, int32_t count,
+                                    int32_t ring_size, void* stream) {
+    MLG_REQUIRE(bt && slot_bytes, "zero_slots: null argument");
+    MLG_REQUIRE(ring_size >= 1 && count >= 0 && count <= ring_size && slot0 >= 0 && slot0 < ring_size,
+                "zero_slots: bad range (slot0=%d count=%d ring=%d)", slot0, count, ring_size);
+    void* ptrs[8] = {bt->state, bt->obs, bt->actions, bt->avail, bt->reward, bt->terminated, bt->actions_onehot,
+                     bt->filled};
+    ZeroJobs J;
+    J.n = 0;
+    J.words0[0] = 0;
+    const int first = (slot0 + count <= ring_size) ? count : ring_size - slot0;
+    const int second = count - first;
+    for (int k = 0; k < 8; ++k) {
+        MLG_REQUIRE(ptrs[k] != nullptr && slot_bytes[k] > 0, "zero_slots: key %d missing", k);
+        for (int part = 0; part < 2; ++part) {
+            const int s0 = part == 0 ? slot0 : 0, n = part == 0 ? first : second;
+            if (n <= 0) continue;
+            J.base[J.n] = reinterpret_cast<unsigned char*>(ptrs[k]);
+            J.begin[J.n] = (int64_t)s0 * slot_bytes[k];
+            J.end[J.n] = (int64_t)(s0 + n) * slot_bytes[k];
+            const int64_t a0 = (J.begin[J.n] + 15) & ~int64_t(15), a1 = J.end[J.n] & ~int64_t(15);
+            J.words0[J.n + 1] = J.words0[J.n] + (a1 > a0 ? (a1 - a0) / 16 : 0);
+            ++J.n;
+        }
+    }
+    if (J.n == 0) return 0;
+    hipLaunchKernelGGL(zero_ranges_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, J);
+    return mlg::check_launch("zero_ranges_kernel");
+}
 
 extern "C" int mlg_debug_set_stamps(void* ptr) {
 #ifdef MLG_STAMPS

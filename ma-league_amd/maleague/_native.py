@@ -38,7 +38,8 @@ class MlgBatch(ctypes.Structure):
     _fields_ = [("state", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("actions", ctypes.c_void_p),
                 ("avail", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
                 ("actions_onehot", ctypes.c_void_p), ("filled", ctypes.c_void_p), ("B", ctypes.c_int32),
-                ("T1", ctypes.c_int32)]
+                ("T1", ctypes.c_int32), ("ring_slot0", ctypes.c_int32), ("ring_size", ctypes.c_int32),
+                ("full_write", ctypes.c_int32)]
 
 
 class MlgRunInfo(ctypes.Structure):
@@ -90,6 +91,7 @@ SIGNATURES = {
     "mlg_qlearner_param_counts": (ctypes.c_int64, [_P, _P, _P]),
     "mlg_qlearner_workspace_floats": (ctypes.c_int64, [_P]),
     "mlg_qlearner_train": (ctypes.c_int, [_P, _P, _P]),
+    "mlg_zero_slots_bytes": (ctypes.c_int, [_P, _P, _I, _I, _I, _P]),
     "mlg_debug_set_stamps": (ctypes.c_int, [_P]),
     "mlg_last_error": (ctypes.c_char_p, []),
     "mlg_version": (ctypes.c_char_p, []),

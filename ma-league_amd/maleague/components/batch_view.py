@@ -50,5 +50,5 @@ def mlg_batch(batch, required=KEYS):
         T1 = batch.max_seq_length
     p = lambda k: None if tensors[k] is None else tensors[k].data_ptr()  # noqa: E731
     mb = _native.MlgBatch(p("state"), p("obs"), p("actions"), p("avail_actions"), p("reward"), p("terminated"),
-                          p("actions_onehot"), p("filled"), B, T1)
+                          p("actions_onehot"), p("filled"), B, T1, 0, 0, 0)
     return mb, list(tensors.values())

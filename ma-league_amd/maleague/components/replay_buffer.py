@@ -17,6 +17,12 @@ class ReplayBuffer(EpisodeBatch):
         self.episodes_in_buffer = 0
 
     def insert_episode_batch(self, ep_batch: EpisodeBatch):
+        if isinstance(ep_batch, RingEpisodeBatch) and ep_batch.ring is self and not ep_batch.committed:
+            if ep_batch.slot0 != self.buffer_index:
+                raise RuntimeError("ring episodes must be inserted in the order they were written")
+            self._advance(ep_batch.batch_size)
+            ep_batch.committed = True
+            return
         room = self.buffer_size - self.buffer_index
         if ep_batch.batch_size > room:
             # split at the wrap point and insert both halves (replay_buffer.py:37-41)
@@ -29,6 +35,17 @@ class ReplayBuffer(EpisodeBatch):
         self.episodes_in_buffer = max(self.episodes_in_buffer, self.buffer_index)
         self.buffer_index %= self.buffer_size
         assert self.buffer_index < self.buffer_size
+
+    def _advance(self, n: int):
+        """Index bookkeeping of inserting n episodes at buffer_index (same as the split insert)."""
+        room = self.buffer_size - self.buffer_index
+        if n > room:
+            self._advance(room)
+            self._advance(n - room)
+            return
+        self.buffer_index += n
+        self.episodes_in_buffer = max(self.episodes_in_buffer, self.buffer_index)
+        self.buffer_index %= self.buffer_size
 
     def _copy_in(self, ep_batch: EpisodeBatch, dst: slice):
         """Same result as update(..., mark_filled=False) of every key: the preprocessed keys that the
@@ -63,3 +80,35 @@ class ReplayBuffer(EpisodeBatch):
     def __repr__(self):
         return (f"ReplayBuffer. {self.episodes_in_buffer}/{self.buffer_size} episodes. "
                 f"Keys:{self.scheme.keys()} Groups:{self.groups.keys()}")
+
+
+class RingEpisodeBatch(EpisodeBatch):
+    """The B episodes one rollout wrote straight into replay-buffer slots [slot0, slot0 + B) mod size
+    (zero-copy insert). Reads materialise views (or a gathered copy when the range wraps); the content
+    is valid until the ring slots are written again."""
+
+    def __init__(self, ring: ReplayBuffer, slot0: int, batch_size: int):
+        self.ring, self.slot0, self.committed = ring, slot0, False
+        self.scheme, self.groups, self.preprocess = ring.scheme, ring.groups, ring.preprocess
+        self.batch_size, self.max_seq_length, self.device = batch_size, ring.max_seq_length, ring.device
+        self._data = None
+
+    @property
+    def data(self):
+        if self._data is None:
+            from types import SimpleNamespace
+            import torch
+            size, B = self.ring.buffer_size, self.batch_size
+            if self.slot0 + B <= size:
+                sel = lambda v: v[self.slot0:self.slot0 + B]  # noqa: E731
+            else:
+                idx = (torch.arange(B, device=self.device) + self.slot0) % size
+                sel = lambda v: v.index_select(0, idx)  # noqa: E731
+            self._data = SimpleNamespace(
+                transition_data={k: sel(v) for k, v in self.ring.data.transition_data.items()},
+                episode_data={k: sel(v) for k, v in self.ring.data.episode_data.items()})
+        return self._data
+
+    @data.setter
+    def data(self, value):
+        self._data = value

@@ -84,6 +84,9 @@ class MultiAgentExperiment:
         if not self.stepper.is_initalized:
             self.stepper.initialize(scheme=self.scheme, groups=self.groups, preprocess=self.preprocess,
                                     home_mac=self.home_mac)
+            # zero-copy insert: train-mode rollouts write straight into the HBM replay ring
+            if getattr(self.args, "zero_copy_insert", True) and hasattr(self.stepper, "attach_replay"):
+                self.stepper.attach_replay(self.home_buffer)
 
     @property
     def _has_not_reached_t_max(self):

@@ -8,6 +8,7 @@ summary (episode length, return, won/draw) for t_env and the logger.
 """
 from __future__ import annotations
 
+import ctypes
 from collections.abc import Sequence
 from functools import partial
 
@@ -17,9 +18,20 @@ import torch
 from .. import _native
 from ..components.batch_view import mlg_batch
 from ..components.episode_batch import EpisodeBatch
+from ..components.replay_buffer import RingEpisodeBatch
 from ..custom_logging import Collectibles, Originator
 from ..envs.teams_env import TeamsEnvSpec, VecEnvState
 from ..exceptions import MultiAgentControllerNotInitialized
+
+
+def _same_device(a, b) -> bool:
+    a, b = torch.device(a), torch.device(b)
+    if a.type != b.type:
+        return False
+    if a.type == "cuda":
+        cur = torch.cuda.current_device()
+        return (cur if a.index is None else a.index) == (cur if b.index is None else b.index)
+    return True
 
 
 class EnvInfos(Sequence):
@@ -75,6 +87,7 @@ class ParallelStepper(EnvStepper):
         self.home_batch = None
         self.last_run = None
         self.timing = None  # list -> (start, end) HIP events around every rollout launch (bench.py)
+        self._ring = None   # ReplayBuffer written in place (zero-copy insert), see attach_replay()
 
     def initialize(self, scheme, groups, preprocess, home_mac, away_mac=None):
         if away_mac is not None:
@@ -87,6 +100,17 @@ class ParallelStepper(EnvStepper):
     def get_env_info(self):
         return self.env_info
 
+    def attach_replay(self, buffer) -> bool:
+        """Let train-mode runs write their episodes straight into `buffer`'s next slots (the buffer's
+        insert_episode_batch then only advances its indices). Returns False when the layouts differ."""
+        ok = (_same_device(buffer.device, self.device) and buffer.max_seq_length == self.episode_limit + 1
+              and buffer.buffer_size >= self.batch_size
+              and all(k in buffer.data.transition_data for k in ("state", "obs", "actions", "avail_actions",
+                                                                  "reward", "terminated", "actions_onehot",
+                                                                  "filled")))
+        self._ring = buffer if ok else None
+        return ok
+
     def save_replay(self):
         pass
 
@@ -94,16 +118,19 @@ class ParallelStepper(EnvStepper):
         pass
 
     def reset(self):
-        self.home_batch = self.new_batch_fn()
         self.t = 0
         self.env_steps_this_run = 0
 
     def _launch(self, batch: EpisodeBatch, epsilon: float, test_mode: bool):
+        mb, keep = mlg_batch(batch)
+        self._launch_mb(mb, epsilon, test_mode)
+        del keep
+
+    def _launch_mb(self, mb, epsilon: float, test_mode: bool):
         B = self.batch_size
         info = self._info
         run_info = _native.MlgRunInfo(info[0:B].data_ptr(), info[4 * B:5 * B].data_ptr(),
                                       info[B:3 * B].data_ptr(), info[3 * B:4 * B].data_ptr())
-        mb, keep = mlg_batch(batch)
         agent = self.home_mac.agent
         d = agent.dims()
         st = self.envs.to_c()
@@ -118,7 +145,6 @@ class ParallelStepper(EnvStepper):
         if ev is not None:
             ev[1].record()
             self.timing.append(ev)
-        del keep
 
     def run(self, test_mode=False):
         if self.home_mac is None:
@@ -131,7 +157,21 @@ class ParallelStepper(EnvStepper):
         eps = 0.0 if test_mode else float(sel.epsilon)
         if test_mode:
             sel.epsilon = 0.0
-        self._launch(self.home_batch, eps, test_mode)
+        ring = self._ring if not test_mode else None
+        if ring is not None:
+            slot0 = ring.buffer_index
+            mb, keep = mlg_batch(ring)
+            # pre-zero the B ring slots in one launch (replaces the zero EpisodeBatch), then sparse writes
+            sb = (ctypes.c_int64 * 8)(*[t[0].numel() * t.element_size() for t in keep])
+            _native.call("mlg_zero_slots_bytes", _native.byref(mb), sb, slot0, self.batch_size, ring.buffer_size,
+                         _native.stream_ptr(self.device))
+            mb.B, mb.ring_slot0, mb.ring_size, mb.full_write = self.batch_size, slot0, ring.buffer_size, 0
+            self._launch_mb(mb, eps, test_mode)
+            del keep
+            self.home_batch = RingEpisodeBatch(ring, slot0, self.batch_size)
+        else:
+            self.home_batch = self.new_batch_fn()
+            self._launch(self.home_batch, eps, test_mode)
         B = self.batch_size
         host = self._info.cpu().numpy()
         ep_len = host[0:B]

@@ -280,3 +280,39 @@ def test_rollout_headline_config_properties(device):
             rew, done, _ = r.step(nb["actions"][b, t, :, 0])
             assert nb["reward"][b, t, 0] == np.float32(rew[0])
             np.testing.assert_array_equal(nb["obs"][b, t + 1], r.obs())
+
+
+def test_rollout_ring_mode_zero_copy_insert(device):
+    """Train-mode rollouts written straight into the replay ring (full-write mode, wrap-around, garbage in the
+    slots beforehand) equal the ordinary zero-initialised EpisodeBatch bit for bit, and the buffer indices
+    advance exactly like ReplayBuffer.insert_episode_batch."""
+    from maleague.components.replay_buffer import ReplayBuffer
+    from maleague.envs.teams_env import VecEnvState
+    stepper, mac, args = _build_stepper(device, plan="medium_1h_4t", B=48, episode_limit=30, seed=2)
+    info = stepper.get_env_info()
+    scheme, groups, preprocess = scheme_for(info, torch)
+    ring = ReplayBuffer(scheme, groups, 100, 31, preprocess=preprocess, device=device)
+    ref = ReplayBuffer(scheme, groups, 100, 31, preprocess=preprocess, device=device)
+    for v in ring.data.transition_data.values():
+        v.fill_(7)
+    stepper.t_env = 20000
+    for it in range(4):  # slots 0-47, 48-95, 96-43 (wraps), 44-91
+        st0 = VecEnvState(stepper.spec, 48, device)
+        st0.episode.fill_(it)
+        stepper.envs = st0
+        stepper._ring = None
+        b_plain, _ = stepper.run(test_mode=False)
+        stepper.t_env -= int(stepper.last_run["ep_len"].sum())
+        st1 = VecEnvState(stepper.spec, 48, device)
+        st1.episode.fill_(it)
+        stepper.envs = st1
+        assert stepper.attach_replay(ring)
+        b_ring, _ = stepper.run(test_mode=False)
+        for k in b_plain.data.transition_data:
+            assert torch.equal(b_plain[k], b_ring[k]), (it, k)
+        ring.insert_episode_batch(b_ring)
+        ref.insert_episode_batch(b_plain)
+        assert (ring.buffer_index, ring.episodes_in_buffer) == (ref.buffer_index, ref.episodes_in_buffer)
+    for k in ref.data.transition_data:
+        n = ref.episodes_in_buffer
+        assert torch.equal(ring[k][:n], ref[k][:n]), k
