@@ -176,7 +176,7 @@ int64_t mlg_qlearner_param_counts(const MlgLearnerCfg *c, int64_t *n_agent, int6
 int64_t mlg_qlearner_workspace_floats(const MlgLearnerCfg *c);
 int mlg_qlearner_train(const MlgLearnerCfg *c, const MlgLearnerBufs *b, void *stream);
 
-/* Diagnostic builds only (-DMLG_STAMPS): device buffer [grid][8 waves][8] u64 of per-phase cycle counts
+/* Diagnostic builds only (-DMLG_STAMPS): device buffer [grid][8 waves][16] u64 of per-phase cycle counts
  * of mlg_rollout. Returns nonzero in normal builds. */
 int mlg_debug_set_stamps(void *ptr);
 

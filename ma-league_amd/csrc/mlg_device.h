@@ -129,20 +129,25 @@ __device__ int env_ai_action(const EnvTables& T, const int* x, const int* y, con
     return near >= 0 ? env_move_toward(x, y, i, near) : 0;
 }
 
-__device__ __forceinline__ void env_spawn_unit(const EnvTables& T, uint64_t key, uint32_t episode, int u, int team_first,
-                                               int team_size, int* x, int* y, int* hp) {
+__device__ __forceinline__ void env_spawn_xyh(const EnvTables& T, uint64_t key, uint32_t episode, int u, int team_first,
+                                              int team_size, int& x, int& y, int& hp) {
     const int G = T.grid, tm = T.team[u];
-    hp[u] = role_maxhp(T.role[u]);
+    hp = role_maxhp(T.role[u]);
     if (T.stochastic) {
         const uint64_t r = mlg_rng(key, mlg_ctr(episode, 0, MLG_PURPOSE_SPAWN, (uint32_t)u));
         const int col = (int)(r % 4u);
-        x[u] = tm == 0 ? col : G - 1 - col;
-        y[u] = (int)((r >> 8) % (uint64_t)G);
+        x = tm == 0 ? col : G - 1 - col;
+        y = (int)((r >> 8) % (uint64_t)G);
     } else {
         const int k = u - team_first;
-        x[u] = tm == 0 ? 1 : G - 2;
-        y[u] = (k * G) / team_size + (G / team_size) / 2;
+        x = tm == 0 ? 1 : G - 2;
+        y = (k * G) / team_size + (G / team_size) / 2;
     }
+}
+
+__device__ __forceinline__ void env_spawn_unit(const EnvTables& T, uint64_t key, uint32_t episode, int u, int team_first,
+                                               int team_size, int* x, int* y, int* hp) {
+    env_spawn_xyh(T, key, episode, u, team_first, team_size, x[u], y[u], hp[u]);
 }
 
 // Obs features of unit j seen by unit i (spec §3.5): writes 8 floats.

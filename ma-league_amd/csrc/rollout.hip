@@ -18,18 +18,34 @@
 #include "mlg_host.h"
 
 #ifdef MLG_STAMPS
-// Diagnostic build only (-DMLG_STAMPS, libmaleague_stamps.so): per-wave cycle shares of the rollout phases.
+// Diagnostic build only (-DMLG_STAMPS, libmaleague_stamps.so): per-wave cycle counts of the rollout phases,
+// written to g_mlg_stamps[block][wave][16] (slots 0..13 phases, 14 total, 15 = 1).
 __device__ unsigned long long* g_mlg_stamps = nullptr;
-#define MLG_STAMP(k)                                             \
-    do {                                                         \
-        const unsigned long long _now = __builtin_amdgcn_s_memtime(); \
-        st_acc[k] += _now - st_last;                             \
-        st_last = _now;                                          \
-    } while (0)
+struct Stamps {
+    unsigned long long acc[14], last, begin;
+    __device__ void init() {
+        for (int k = 0; k < 14; ++k) acc[k] = 0;
+        last = begin = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void mark(int k) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - last;
+        last = now;
+    }
+    __device__ void flush() {
+        if ((threadIdx.x & 63) || !g_mlg_stamps) return;
+        unsigned long long* o = g_mlg_stamps + ((int64_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 16;
+        for (int k = 0; k < 14; ++k) o[k] = acc[k];
+        o[14] = __builtin_amdgcn_s_memtime() - begin;
+        o[15] = 1;
+    }
+};
 #else
-#define MLG_STAMP(k) \
-    do {             \
-    } while (0)
+struct Stamps {
+    __device__ void init() {}
+    __device__ void mark(int) {}
+    __device__ void flush() {}
+};
 #endif
 
 namespace {
@@ -38,6 +54,7 @@ constexpr int RE = 16;  // envs per workgroup
 
 struct SpecShared {
     int team[MLG_MAXU], role[MLG_MAXU], melee[MLG_MAXU], agent[MLG_MAXU];
+    int aunit[MLG_MAXU];  // unit of agent a
     int team_first[2], team_size[2];
 };
 
@@ -51,7 +68,10 @@ __device__ void load_spec_tables(const MlgEnvSpec& spec, SpecShared& s) {
         s.agent[u] = 0;
     }
     __syncthreads();
-    for (int a = tid; a < spec.n_agents; a += blockDim.x) s.agent[spec.agent_unit[a]] = a + 1;
+    for (int a = tid; a < spec.n_agents; a += blockDim.x) {
+        s.agent[spec.agent_unit[a]] = a + 1;
+        s.aunit[a] = spec.agent_unit[a];
+    }
     if (tid == 0) {
         for (int tm = 0; tm < 2; ++tm) {
             s.team_first[tm] = -1;
@@ -79,31 +99,246 @@ __device__ __forceinline__ EnvTables make_tables(const MlgEnvSpec& spec, const S
     return T;
 }
 
-// Writes obs/state/avail of env (x,y,hp) for batch slot (b, t); called cooperatively:
-// item index i in [0, items) distributed over the threads of the block by the caller.
-__device__ __forceinline__ void write_obs_item(const EnvTables& T, const MlgEnvSpec& spec, const int* x, const int* y,
-                                               const int* hp, float* obs_bt, int a, int j, float inv_p) {
-    float o[8];
-    env_obs_feat(T, x, y, hp, spec.agent_unit[a], j, inv_p, o);
-    float* dst = obs_bt + ((int64_t)a * T.U + j) * 8;
-    *reinterpret_cast<floatx4*>(dst) = floatx4{o[0], o[1], o[2], o[3]};
-    *reinterpret_cast<floatx4*>(dst + 4) = floatx4{o[4], o[5], o[6], o[7]};
+// ---- per-workgroup env bookkeeping shared by both rollout kernels --------------------------------
+// LDS pointers of the RE envs a workgroup owns. lobs/lavail (v2 only, else nullptr) mirror the obs and
+// avail rows the agent phase reads, so the cell never reads back what the env phase wrote to HBM.
+struct RoEnv {
+    int *x, *y, *hp, *nhp, *act, *pact, *prev, *status, *stepped, *len, *slot, *list, *misc;
+    uint32_t* episode;
+    float* ret;
+    float* lobs;
+    int32_t* lavail;
+    int ldo;
+};
+
+// Dynamic-LDS carve of the env part (4-byte words).
+struct RoEnvLds {
+    int64_t spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, list, misc;
+};
+
+__host__ __device__ inline int64_t ro_take(int64_t& o, int64_t n) {
+    const int64_t v = o;
+    o += mlg_align4(n);
+    return v;
+}
+
+__host__ __device__ inline RoEnvLds make_env_lds(int64_t& o, int U, int n_agents) {
+    RoEnvLds r;
+    r.spec = ro_take(o, (int64_t)(sizeof(SpecShared) / 4));
+    const int64_t eu = (int64_t)RE * U;
+    r.x = ro_take(o, eu);
+    r.y = ro_take(o, eu);
+    r.hp = ro_take(o, eu);
+    r.nhp = ro_take(o, eu);
+    r.act = ro_take(o, eu);
+    r.pact = ro_take(o, (int64_t)RE * n_agents);
+    r.prev = ro_take(o, (int64_t)RE * n_agents);
+    r.status = ro_take(o, RE);
+    r.stepped = ro_take(o, RE);
+    r.len = ro_take(o, RE);
+    r.episode = ro_take(o, RE);
+    r.ret = ro_take(o, RE);
+    r.slot = ro_take(o, RE);
+    r.list = ro_take(o, RE);
+    r.misc = ro_take(o, 4);  // [0] any env running, [1] number of running envs
+    return r;
+}
+
+__device__ inline RoEnv env_view(int* smem, const RoEnvLds& l) {
+    RoEnv R;
+    R.x = smem + l.x;
+    R.y = smem + l.y;
+    R.hp = smem + l.hp;
+    R.nhp = smem + l.nhp;
+    R.act = smem + l.act;
+    R.pact = smem + l.pact;
+    R.prev = smem + l.prev;
+    R.status = smem + l.status;
+    R.stepped = smem + l.stepped;
+    R.len = smem + l.len;
+    R.slot = smem + l.slot;
+    R.list = smem + l.list;
+    R.misc = smem + l.misc;
+    R.episode = reinterpret_cast<uint32_t*>(smem + l.episode);
+    R.ret = reinterpret_cast<float*>(smem + l.ret);
+    R.lobs = nullptr;
+    R.lavail = nullptr;
+    R.ldo = 0;
+    return R;
+}
+
+// obs/state/avail of batch time index t for the envs selected by `sel` (0: not done at reset, 1: stepped).
+__device__ void ro_observe(const EnvTables& T, const MlgEnvSpec& spec, const RoEnv& R, const MlgBatch& bt, int t,
+                           bool stepped_only, float inv_p, Stamps& sp) {
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int U = T.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, T1 = bt.T1;
+    auto on = [&](int e) { return stepped_only ? R.stepped[e] != 0 : R.status[e] != 2; };
+    for (int i = tid; i < RE * N * U; i += nthr) {
+        const int e = i / (N * U), r = i % (N * U);
+        if (!on(e)) continue;
+        const int a = r / U, j = r % U;
+        float o[8];
+        env_obs_feat(T, R.x + e * U, R.y + e * U, R.hp + e * U, spec.agent_unit[a], j, inv_p, o);
+        const floatx4 lo{o[0], o[1], o[2], o[3]}, hi{o[4], o[5], o[6], o[7]};
+        float* dst = bt.obs + (((int64_t)R.slot[e] * T1 + t) * N + a) * DO + j * 8;
+        *reinterpret_cast<floatx4*>(dst) = lo;
+        *reinterpret_cast<floatx4*>(dst + 4) = hi;
+        if (R.lobs) {
+            float* l = R.lobs + (e * N + a) * R.ldo + j * 8;
+            *reinterpret_cast<floatx4*>(l) = lo;
+            *reinterpret_cast<floatx4*>(l + 4) = hi;
+        }
+    }
+    sp.mark(7);
+    for (int i = tid; i < RE * U; i += nthr) {
+        const int e = i / U, j = i % U;
+        if (!on(e)) continue;
+        float o[6];
+        env_state_feat(T, R.x + e * U, R.y + e * U, R.hp + e * U, j, inv_p, o);
+        float* dst = bt.state + ((int64_t)R.slot[e] * T1 + t) * S + j * 6;
+#pragma unroll
+        for (int f = 0; f < 6; ++f) dst[f] = o[f];
+    }
+    sp.mark(8);
+    for (int i = tid; i < RE * N * A; i += nthr) {
+        const int e = i / (N * A), r = i % (N * A);
+        if (!on(e)) continue;
+        const int v = env_avail_one(T, R.x + e * U, R.y + e * U, R.hp + e * U, spec.agent_unit[r / A], r % A);
+        bt.avail[((int64_t)R.slot[e] * T1 + t) * N * A + r] = v;
+        if (R.lavail) R.lavail[e * N * A + r] = v;
+    }
+    sp.mark(9);
+}
+
+// Reset of the RE envs (parallel_stepper.py:82-104; env_worker_process.py:54-60) + observation at t = 0.
+__device__ void ro_reset(const EnvTables& T, const SpecShared& SS, const MlgEnvSpec& spec, const MlgEnvState& st,
+                         const RoEnv& R, const MlgBatch& bt, int e0, float inv_p) {
+    const int tid = threadIdx.x, nthr = blockDim.x, U = T.U, B = bt.B;
+    for (int e = tid; e < RE; e += nthr) {
+        const int b = e0 + e;
+        R.len[e] = 0;
+        R.ret[e] = 0.f;
+        R.stepped[e] = 0;
+        if (b < B) {
+            const uint32_t ep = st.episode[b];
+            st.episode[b] = ep + 1;
+            R.episode[e] = ep;
+            R.status[e] = 0;
+            const int sl = bt.ring_size > 0 ? (bt.ring_slot0 + b) % bt.ring_size : b;
+            R.slot[e] = sl;
+            bt.filled[(int64_t)sl * bt.T1] = 1;
+        } else {
+            R.status[e] = 2;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < RE * U; i += nthr) {
+        const int e = i / U, u = i % U;
+        if (R.status[e] == 2) continue;
+        const int tm = SS.team[u];
+        env_spawn_unit(T, mlg_env_key(spec.seed, e0 + e), R.episode[e], u, SS.team_first[tm], SS.team_size[tm],
+                       R.x + e * U, R.y + e * U, R.hp + e * U);
+    }
+    __syncthreads();
+    Stamps none;
+    ro_observe(T, spec, R, bt, 0, false, inv_p, none);
+}
+
+// Running-env list (status < 2, ascending) and count; single thread, caller syncs.
+__device__ inline void ro_list_running(const RoEnv& R) {
+    int n = 0;
+    for (int e = 0; e < RE; ++e)
+        if (R.status[e] < 2) R.list[n++] = e;
+    R.misc[0] = n > 0;
+    R.misc[1] = n;
+}
+
+// Env phase of step t for the running envs (env_worker_process.py:32-53 batched): executed actions
+// (policy or scripted AI), simultaneous resolution, per-env reward / termination, then obs of t + 1.
+__device__ void ro_env_step(const EnvTables& T, const SpecShared& SS, const MlgEnvSpec& spec, const RoEnv& R,
+                            const MlgBatch& bt, const MlgRunInfo& info, int e0, int t, float inv_p, Stamps& sp) {
+    const int tid = threadIdx.x, nthr = blockDim.x, U = T.U, N = spec.n_agents, T1 = bt.T1;
+    for (int i = tid; i < RE * U; i += nthr) {
+        const int e = i / U, u = i % U;
+        if (R.status[e] != 0) continue;
+        const int ag = SS.agent[u];
+        R.act[e * U + u] = env_exec_action(T, R.x + e * U, R.y + e * U, R.hp + e * U, u,
+                                           ag ? (int64_t)R.pact[e * N + ag - 1] : 0);
+    }
+    sp.mark(4);
+    __syncthreads();
+    for (int i = tid; i < RE * U; i += nthr) {
+        const int e = i / U, j = i % U;
+        if (R.status[e] != 0) continue;
+        R.nhp[e * U + j] = env_resolve_hp(T, R.act + e * U, R.hp + e * U, j);
+        if (R.hp[e * U + j] > 0) env_apply_move(R.act[e * U + j], &R.x[e * U + j], &R.y[e * U + j]);
+    }
+    sp.mark(5);
+    __syncthreads();
+    for (int e = tid; e < RE; e += nthr) {
+        const int b = e0 + e;
+        const int status = R.status[e];
+        R.stepped[e] = 0;
+        if (status == 2) continue;
+        for (int n = 0; n < N; ++n) R.prev[e * N + n] = R.pact[e * N + n];
+        if (status == 1) {  // final action recorded; env done (parallel_stepper.py:153)
+            R.status[e] = 2;
+            if (bt.full_write) {
+                bt.reward[(int64_t)R.slot[e] * T1 + t] = 0.f;
+                bt.terminated[(int64_t)R.slot[e] * T1 + t] = 0;
+            }
+            continue;
+        }
+        int alive[2] = {0, 0}, lost[2] = {0, 0}, kills[2] = {0, 0};
+        for (int j = 0; j < U; ++j) {
+            const int tm = SS.team[j];
+            const int h0 = R.hp[e * U + j], h1 = R.nhp[e * U + j];
+            if (h0 > 0) {
+                lost[tm] += h0 - h1 > 0 ? h0 - h1 : 0;
+                if (h1 == 0) kills[1 - tm] += 1;
+            }
+            if (h1 > 0) alive[tm] += 1;
+            R.hp[e * U + j] = h1;
+        }
+        const int done = alive[0] == 0 || alive[1] == 0 || t + 1 >= spec.episode_limit;
+        int won[2];
+        won[0] = alive[1] == 0 && alive[0] > 0;
+        won[1] = alive[0] == 0 && alive[1] > 0;
+        const int pt = spec.policy_team;
+        const int r_int = lost[1 - pt] + 10 * kills[pt] + 200 * won[pt];
+        const float r = (float)r_int * 0.0625f;
+        bt.reward[(int64_t)R.slot[e] * T1 + t] = r;
+        bt.terminated[(int64_t)R.slot[e] * T1 + t] = (uint8_t)done;
+        bt.filled[(int64_t)R.slot[e] * T1 + t + 1] = 1;
+        R.ret[e] += r;
+        R.stepped[e] = 1;
+        if (done) {
+            R.status[e] = 1;
+            R.len[e] = t + 1;
+            info.won[2 * b] = won[pt];
+            info.won[2 * b + 1] = won[1 - pt];
+            info.draw[b] = !won[0] && !won[1];
+        }
+    }
+    sp.mark(6);
+    __syncthreads();
+    // observation at t + 1 for envs that stepped (incl. those that just terminated)
+    ro_observe(T, spec, R, bt, t + 1, true, inv_p, sp);
 }
 
 // Zero every key of slots [t0, t1) of the envs of this workgroup that are done and did not step
 // (status 2, or stepped == 0 with status 2 after the final action): the full-write (ring) mode's
 // replacement for zero-initialising the EpisodeBatch.
-__device__ void zero_slots(const MlgBatch& bt, const int* s_slot, const int* s_status, const int* s_stepped, int e0,
-                           int B, int t0, int t1, int N, int A, int S, int DO) {
-    const int T1 = bt.T1;
+__device__ void zero_slots(const MlgBatch& bt, const RoEnv& R, int e0, int t0, int t1, int N, int A, int S, int DO) {
+    const int T1 = bt.T1, B = bt.B;
     const int per = S + N * DO + 2 * N * A + 2 * N + 3;  // words per slot (actions/filled are 2 words)
     const int total = RE * (t1 - t0) * per;
     for (int i = threadIdx.x; i < total; i += blockDim.x) {
         const int e = i / ((t1 - t0) * per), rem = i % ((t1 - t0) * per);
         const int t = t0 + rem / per;
         int k = rem % per;
-        if (e0 + e >= B || s_status[e] != 2 || s_stepped[e]) continue;
-        const int64_t sl = (int64_t)s_slot[e] * T1 + t;
+        if (e0 + e >= B || R.status[e] != 2 || R.stepped[e]) continue;
+        const int64_t sl = (int64_t)R.slot[e] * T1 + t;
         if (k < S) { bt.state[sl * S + k] = 0.f; continue; }
         k -= S;
         if (k < N * DO) { bt.obs[sl * N * DO + k] = 0.f; continue; }
@@ -122,9 +357,56 @@ __device__ void zero_slots(const MlgBatch& bt, const int* s_slot, const int* s_s
     }
 }
 
-// Dynamic-LDS carve of the rollout workgroup (4-byte words; every region 16-byte aligned).
+// Per-env summary + env state write-back.
+__device__ void ro_finish(const MlgEnvState& st, const RoEnv& R, const MlgRunInfo& info, int e0, int B, int U) {
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    for (int e = tid; e < RE; e += nthr) {
+        const int b = e0 + e;
+        if (b >= B) continue;
+        info.ep_len[b] = R.len[e];
+        info.ret[b] = R.ret[e];
+        st.t[b] = R.len[e];
+    }
+    for (int i = tid; i < RE * U; i += nthr) {
+        const int e = i / U, u = i % U;
+        const int64_t b = e0 + e;
+        if (b >= B) continue;
+        st.x[b * U + u] = R.x[e * U + u];
+        st.y[b * U + u] = R.y[e * U + u];
+        st.hp[b * U + u] = R.hp[e * U + u];
+    }
+}
+
+// Picks the action of this lane's row from the masked argmax (EpsilonGreedyActionSelector.select,
+// action_selectors.py:44-62) and records it: LDS pending action, batch actions / actions_onehot.
+__device__ __forceinline__ void ro_record_action(const MlgEnvSpec& spec, const RoEnv& R, const MlgBatch& bt, int act,
+                                                 const int32_t* av, int e, int n, int b, int t, float eps,
+                                                 int test_mode) {
+    const int N = spec.n_agents, A = spec.n_actions;
+    if (!test_mode && eps > 0.f) {
+        const uint64_t key = mlg_env_key(spec.seed, b);
+        const uint64_t r1 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n));
+        if (mlg_u01(r1) < eps) {
+            const uint64_t r2 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)n));
+            act = random_available(av, A, r2);
+        }
+    }
+    R.pact[e * N + n] = act;
+    const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
+    bt.actions[bt_off] = act;
+    if (bt.full_write)
+        for (int k = 0; k < A; ++k) bt.actions_onehot[bt_off * A + k] = k == act ? 1.0f : 0.0f;
+    else
+        bt.actions_onehot[bt_off * A + act] = 1.0f;
+}
+
+// ================================================================================================
+// v1: generic kernel (any H in {32, 64, 128}, weights in LDS or HBM). Workgroup = W waves
+// (W = min(tiles, 8)); wave w owns the 16-row agent tiles w, w + W, ... (row = env * N + agent) for the
+// whole episode with the GRU hidden state in VGPRs.
 struct RolloutLds {
-    int64_t wts, spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, any, total;
+    int64_t wts, total;
+    RoEnvLds env;
     LdsWeights lw;
     int weights_in_lds;
 };
@@ -134,24 +416,8 @@ __host__ __device__ inline RolloutLds make_rollout_lds(const AgentLayout& L, int
     r.lw = make_lds_weights(L);
     r.weights_in_lds = weights_in_lds;
     int64_t o = 0;
-    auto take = [&](int64_t n) { int64_t v = o; o += mlg_align4(n); return v; };
-    r.wts = take(weights_in_lds ? r.lw.total : 0);
-    r.spec = take((int64_t)(sizeof(SpecShared) / 4));
-    const int64_t eu = (int64_t)RE * U;
-    r.x = take(eu);
-    r.y = take(eu);
-    r.hp = take(eu);
-    r.nhp = take(eu);
-    r.act = take(eu);
-    r.pact = take((int64_t)RE * n_agents);
-    r.prev = take((int64_t)RE * n_agents);
-    r.status = take(RE);
-    r.stepped = take(RE);
-    r.len = take(RE);
-    r.episode = take(RE);
-    r.ret = take(RE);
-    r.slot = take(RE);
-    r.any = take(1);
+    r.wts = ro_take(o, weights_in_lds ? r.lw.total : 0);
+    r.env = make_env_lds(o, U, n_agents);
     r.total = o;
     return r;
 }
@@ -162,81 +428,18 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                                                      float eps, int test_mode, RolloutLds lay) {
     constexpr int HC = H / 16;
     extern __shared__ __attribute__((aligned(16))) int smem[];
-    SpecShared& SS = *reinterpret_cast<SpecShared*>(smem + lay.spec);
+    SpecShared& SS = *reinterpret_cast<SpecShared*>(smem + lay.env.spec);
+    const RoEnv R = env_view(smem, lay.env);
     const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U;
-    int* s_x = smem + lay.x;
-    int* s_y = smem + lay.y;
-    int* s_hp = smem + lay.hp;
-    int* s_nhp = smem + lay.nhp;
-    int* s_act = smem + lay.act;
-    int* s_pact = smem + lay.pact;
-    int* s_prev = smem + lay.prev;
-    int* s_status = smem + lay.status;
-    int* s_stepped = smem + lay.stepped;
-    int* s_len = smem + lay.len;
-    uint32_t* s_episode = reinterpret_cast<uint32_t*>(smem + lay.episode);
-    float* s_ret = reinterpret_cast<float*>(smem + lay.ret);
-    int* s_slot = smem + lay.slot;  // batch slot of env e (ring mode: the replay-buffer slot)
-    int& s_any = smem[lay.any];
-
     const int tid = threadIdx.x, nthr = blockDim.x;
     const int lane = tid & 63, wave = tid >> 6, W = nthr >> 6;
     const int e0 = blockIdx.x * RE;
-    const int B = bt.B, T1 = bt.T1;
+    const int T1 = bt.T1;
     load_spec_tables(spec, SS);
     if (WLDS) load_weights_to_lds(P, L, lay.lw, reinterpret_cast<float*>(smem + lay.wts));
     const EnvTables T = make_tables(spec, SS);
     const float inv_p = 1.0f / (float)pow2_at_least(spec.grid);
-
-    // ---- reset (parallel_stepper.py:82-104; env_worker_process.py:54-60) ----
-    for (int e = tid; e < RE; e += nthr) {
-        const int b = e0 + e;
-        s_len[e] = 0;
-        s_ret[e] = 0.f;
-        s_stepped[e] = 0;
-        if (b < B) {
-            const uint32_t ep = st.episode[b];
-            st.episode[b] = ep + 1;
-            s_episode[e] = ep;
-            s_status[e] = 0;
-            const int sl = bt.ring_size > 0 ? (bt.ring_slot0 + b) % bt.ring_size : b;
-            s_slot[e] = sl;
-            bt.filled[(int64_t)sl * T1] = 1;
-        } else {
-            s_status[e] = 2;
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < RE * U; i += nthr) {
-        const int e = i / U, u = i % U;
-        if (s_status[e] == 2) continue;
-        const int tm = SS.team[u];
-        env_spawn_unit(T, mlg_env_key(spec.seed, e0 + e), s_episode[e], u, SS.team_first[tm], SS.team_size[tm],
-                       s_x + e * U, s_y + e * U, s_hp + e * U);
-    }
-    __syncthreads();
-    // observation at t = 0
-    for (int i = tid; i < RE * N * U; i += nthr) {
-        const int e = i / (N * U), r = i % (N * U);
-        if (s_status[e] == 2) continue;
-        write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U, bt.obs + (int64_t)s_slot[e] * T1 * N * DO, r / U,
-                       r % U, inv_p);
-    }
-    for (int i = tid; i < RE * U; i += nthr) {
-        const int e = i / U, j = i % U;
-        if (s_status[e] == 2) continue;
-        float o[6];
-        env_state_feat(T, s_x + e * U, s_y + e * U, s_hp + e * U, j, inv_p, o);
-        float* dst = bt.state + (int64_t)s_slot[e] * T1 * S + j * 6;
-#pragma unroll
-        for (int f = 0; f < 6; ++f) dst[f] = o[f];
-    }
-    for (int i = tid; i < RE * N * A; i += nthr) {
-        const int e = i / (N * A), r = i % (N * A);
-        if (s_status[e] == 2) continue;
-        bt.avail[(int64_t)s_slot[e] * T1 * N * A + r] =
-            env_avail_one(T, s_x + e * U, s_y + e * U, s_hp + e * U, spec.agent_unit[r / A], r % A);
-    }
+    ro_reset(T, SS, spec, st, R, bt, e0, inv_p);
     __syncthreads();
 
     floatx4 h[TPW][HC];
@@ -244,17 +447,12 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     for (int ti = 0; ti < TPW; ++ti)
 #pragma unroll
         for (int c = 0; c < HC; ++c) h[ti][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-#ifdef MLG_STAMPS
-    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long st_last = __builtin_amdgcn_s_memtime();
-    const unsigned long long st_begin = st_last;
-#endif
-
+    Stamps sp;
+    sp.init();
     const int n_tiles = (RE * N + 15) / 16;
     const int col = lane & 15, g = lane >> 4;
     const int n_at = L.Ap / 16;
     int last_t = 0;
-
     for (int t = 0; t < T1; ++t) {
         // ================= agent phase: rows of envs with status 0 (running) or 1 (final action) ======
 #pragma unroll
@@ -263,7 +461,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             if (tile >= n_tiles) continue;
             const int row = tile * 16 + col;
             const int e = row / N, n = row % N;
-            const bool valid = row < RE * N && s_status[e] < 2;
+            const bool valid = row < RE * N && R.status[e] < 2;
             if (!__any(valid)) continue;  // wave-uniform skip of finished tiles
             // Opaque zero offset per tile: stops LICM/CSE from keeping t- and tile-invariant weight loads
             // live across the episode loop in (spilled) registers.
@@ -271,12 +469,11 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
             asm volatile("" : "+s"(zero));
             const WView Wv = WLDS ? lds_view(reinterpret_cast<const float*>(smem + lay.wts) + zero, lay.lw, L)
                                   : global_view(P + zero, L);
-            const int64_t b = e0 + e;
-            const int64_t bt_off = valid ? ((int64_t)s_slot[e] * T1 + t) * N + n : 0;
+            const int64_t bt_off = valid ? ((int64_t)R.slot[e] * T1 + t) * N + n : 0;
             RowIn in;
             in.x = valid ? bt.obs + bt_off * DO : nullptr;
             in.onehot = nullptr;
-            in.prev_action = (valid && t > 0) ? s_prev[e * N + n] : -1;
+            in.prev_action = (valid && t > 0) ? R.prev[e * N + n] : -1;
             in.agent = valid ? n : 0;
             agent_cell_hidden<H>(Wv, L, in, h[ti], lane);
             const int32_t* av = valid ? bt.avail + bt_off * A : nullptr;
@@ -285,153 +482,507 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                 const floatx4 q = agent_q_tile<H>(Wv, h[ti], at, lane);
                 argmax_accumulate(as, q, av, at, A, lane);
             }
-            int act = argmax_reduce(as);
-            if (valid && g == 0) {
-                if (!test_mode && eps > 0.f) {
-                    const uint64_t key = mlg_env_key(spec.seed, (int)b);
-                    const uint64_t r1 = mlg_rng(key, mlg_ctr(s_episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n));
-                    if (mlg_u01(r1) < eps) {
-                        const uint64_t r2 = mlg_rng(key, mlg_ctr(s_episode[e], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)n));
-                        act = random_available(av, A, r2);
+            const int act = argmax_reduce(as);
+            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, e, n, e0 + e, t, eps, test_mode);
+        }
+        sp.mark(0);
+        __syncthreads();
+        sp.mark(1);
+        ro_env_step(T, SS, spec, R, bt, info, e0, t, inv_p, sp);
+        // full-write mode: slot t+1 of envs that are done (t+1 > episode length) gets zeros
+        if (bt.full_write && t + 1 < T1) zero_slots(bt, R, e0, t + 1, t + 2, N, A, S, DO);
+        if (tid == 0) ro_list_running(R);
+        __syncthreads();
+        sp.mark(10);
+        last_t = t;
+        if (!R.misc[0]) break;
+    }
+    sp.flush();
+    // full-write mode: the remaining slots of every env (all of them are done here)
+    for (int e = tid; e < RE; e += nthr) R.stepped[e] = 0;
+    __syncthreads();
+    if (bt.full_write && last_t + 2 < T1) zero_slots(bt, R, e0, last_t + 2, T1, N, A, S, DO);
+    ro_finish(st, R, info, e0, bt.B, U);
+}
+
+// ================================================================================================
+// v2 env: one half-wave (32 lanes) per env, lane u = unit u (U <= 32). Unit state lives in VGPRs for the
+// whole episode; everything an env step needs from other units travels by cross-lane permutes, so the
+// env phase has no workgroup barrier and no LDS round trips (same spec-v1 arithmetic as mlg_device.h,
+// bit-exact; checked against v1 and the C oracle).
+struct UnitMasks {
+    uint32_t team1, healer, tank, melee;  // bit u set iff unit u is on plan team 1 / HEALER / TANK / MELEE
+};
+
+__device__ inline UnitMasks make_unit_masks(const SpecShared& SS, int U) {
+    UnitMasks m{0u, 0u, 0u, 0u};
+    for (int u = 0; u < U; ++u) {
+        m.team1 |= (uint32_t)(SS.team[u] == 1) << u;
+        m.healer |= (uint32_t)(SS.role[u] == 1) << u;
+        m.tank |= (uint32_t)(SS.role[u] == 0) << u;
+        m.melee |= (uint32_t)(SS.melee[u] == 1) << u;
+    }
+    return m;
+}
+
+__device__ __forceinline__ int pk_unit(int x, int y, int hp) { return x | (y << 12) | (hp << 24); }
+__device__ __forceinline__ int pk_x(int q) { return q & 0xFFF; }
+__device__ __forceinline__ int pk_y(int q) { return (q >> 12) & 0xFFF; }
+__device__ __forceinline__ int pk_hp(int q) { return q >> 24; }
+__device__ __forceinline__ int mask_role(const UnitMasks& M, int j) {
+    return ((M.tank >> j) & 1) ? 0 : (((M.healer >> j) & 1) ? 1 : 2);
+}
+__device__ __forceinline__ int move_toward_d(int dx, int dy) {
+    const int adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+    if (adx >= ady && dx != 0) return dx > 0 ? 3 : 4;
+    if (dy != 0) return dy > 0 ? 1 : 2;
+    return 0;
+}
+
+// Lane-resident unit of the half-wave's env.
+struct UnitLane {
+    int x, y, hp;        // state
+    uint32_t tgt, sight; // bit j: action 5+j available / unit j visible (current state)
+    int ai;              // scripted action decided on the current state (spec §3.3)
+};
+
+// One pass over all units j of the env for unit u (every lane of the half-wave runs all U iterations):
+// attack/heal availability, sight, and the scripted AI choice (lowest-hp target in range, else nearest
+// ally for a healer when one is alive, else nearest enemy) -- spec §3.2-3.3 in mask form.
+__device__ __forceinline__ void v2_pair_pass(const UnitMasks& M, int U, int hbase, int u, UnitLane& L) {
+    const int my_team = (M.team1 >> u) & 1;
+    const bool healer = (M.healer >> u) & 1;
+    const int r2 = ((M.melee >> u) & 1) ? 2 : 9;
+    const bool alive = L.hp > 0;
+    const int pk = pk_unit(L.x, L.y, L.hp);
+    int best = -1, besthp = 0, na = -1, nda = 0, ne = -1, nde = 0, adx = 0, ady = 0, edx = 0, edy = 0;
+    uint32_t tgt = 0, sight = 0;
+    for (int j = 0; j < U; ++j) {
+        const int q = __shfl(pk, hbase + j, 64);
+        const int hj = pk_hp(q);
+        const int dx = pk_x(q) - L.x, dy = pk_y(q) - L.y, d2 = dx * dx + dy * dy;
+        const int tj = (M.team1 >> j) & 1;
+        const int mxj = ((M.tank >> j) & 1) ? 64 : 32;
+        if (alive && hj > 0) {
+            if (d2 <= MLG_SIGHT2) sight |= 1u << j;
+            const bool cond = healer ? (j != u && tj == my_team && hj < mxj) : (tj != my_team);
+            if (d2 <= r2 && cond) {
+                tgt |= 1u << j;
+                if (best < 0 || hj < besthp) { best = j; besthp = hj; }
+            }
+            if (j != u && tj == my_team && (na < 0 || d2 < nda)) { na = j; nda = d2; adx = dx; ady = dy; }
+            if (tj != my_team && (ne < 0 || d2 < nde)) { ne = j; nde = d2; edx = dx; edy = dy; }
+        }
+    }
+    int ai = 0;
+    if (alive) {
+        if (best >= 0) ai = MLG_ACT_BASE + best;
+        else if (healer && na >= 0) ai = nda > 2 ? move_toward_d(adx, ady) : 0;
+        else if (ne >= 0) ai = move_toward_d(edx, edy);
+    }
+    L.tgt = tgt;
+    L.sight = sight;
+    L.ai = ai;
+}
+
+__device__ __forceinline__ int v2_avail(const UnitMasks& M, int G, int x, int y, int hp, uint32_t tgt, int k) {
+    const bool alive = hp > 0;
+    if (k == 0) return !alive;
+    if (!alive) return 0;
+    if (k == 1) return y + 1 < G;
+    if (k == 2) return y - 1 >= 0;
+    if (k == 3) return x + 1 < G;
+    if (k == 4) return x - 1 >= 0;
+    return (int)((tgt >> (k - MLG_ACT_BASE)) & 1u);
+}
+
+// obs / state / avail of batch index t for the half-wave's env (all 32 lanes call; `on` uniform per half).
+__device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec& spec, const SpecShared& SS,
+                                           const int* pairtab, const int* avtab, const MlgBatch& bt, int slot, int t,
+                                           int e, int hbase, int hl, const UnitLane& L, float* lobs, int ldo,
+                                           int32_t* lavail, float inv_p) {
+    const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, G = spec.grid;
+    const int64_t st_row = (int64_t)slot * bt.T1 + t;
+    const int pk = pk_unit(L.x, L.y, L.hp);
+    for (int k0 = 0; k0 < N * U; k0 += 32) {
+        const int k = k0 + hl;
+        const bool valid = k < N * U;
+        const int pt = pairtab[valid ? k : 0];
+        const int a = pt >> 8, j = pt & 255, i = SS.aunit[a];
+        const int qi = __shfl(pk, hbase + i, 64), qj = __shfl(pk, hbase + j, 64);
+        const uint32_t ti = __shfl((int)L.tgt, hbase + i, 64), si = __shfl((int)L.sight, hbase + i, 64);
+        floatx4 lo{0.f, 0.f, 0.f, 0.f}, hi{0.f, 0.f, 0.f, 0.f};
+        if ((si >> j) & 1u) {
+            const int rj = mask_role(M, j);
+            lo = floatx4{1.0f, (float)(pk_x(qj) - pk_x(qi)) * inv_p, (float)(pk_y(qj) - pk_y(qi)) * inv_p,
+                         (float)pk_hp(qj) * inv_maxhp(rj)};
+            hi = floatx4{(float)((ti >> j) & 1u), (float)(((M.team1 >> j) & 1) == ((M.team1 >> i) & 1)),
+                         (float)rj * 0.5f, (float)((M.melee >> j) & 1)};
+        }
+        if (valid) {
+            float* dst = bt.obs + (st_row * N + a) * DO + j * 8;
+            *reinterpret_cast<floatx4*>(dst) = lo;
+            *reinterpret_cast<floatx4*>(dst + 4) = hi;
+            float* l = lobs + (e * N + a) * ldo + j * 8;
+            *reinterpret_cast<floatx4*>(l) = lo;
+            *reinterpret_cast<floatx4*>(l + 4) = hi;
+        }
+    }
+    for (int k0 = 0; k0 < N * A; k0 += 32) {
+        const int k = k0 + hl;
+        const bool valid = k < N * A;
+        const int pt = avtab[valid ? k : 0];
+        const int a = pt >> 8, kk = pt & 255, i = SS.aunit[a];
+        const int qi = __shfl(pk, hbase + i, 64);
+        const uint32_t ti = __shfl((int)L.tgt, hbase + i, 64);
+        const int v = v2_avail(M, G, pk_x(qi), pk_y(qi), pk_hp(qi), ti, kk);
+        if (valid) {
+            bt.avail[st_row * N * A + k] = v;
+            lavail[e * N * A + k] = v;
+        }
+    }
+    if (hl < U) {
+        const int r = mask_role(M, hl);
+        float* dst = bt.state + st_row * S + hl * 6;
+        *reinterpret_cast<float2*>(dst) = make_float2((float)(L.hp > 0), (float)L.x * inv_p);
+        *reinterpret_cast<float2*>(dst + 2) = make_float2((float)L.y * inv_p, (float)L.hp * inv_maxhp(r));
+        *reinterpret_cast<float2*>(dst + 4) = make_float2((float)((M.team1 >> hl) & 1), (float)r * 0.5f);
+    }
+}
+
+// ================================================================================================
+// v2: the headline kernel (H in {32, 64}, U <= 32; everything the step reads resident on chip).
+//
+// Agent phase. Work per timestep is split into (tile, 16-feature chunk) units so that all four SIMDs carry
+// the same MFMA load whatever the tile count (5 tiles of 16 rows for 16 envs x 5 agents), and only rows
+// of envs still running are processed: running envs are compacted into tiles every step.
+//   wave w owns feature chunk j = w % HC of the GRU for tiles w / HC, w / HC + 8 / HC, ...; its
+//   W_ih / W_hh rows for that chunk (3 gates x 16 features x H) live in VGPRs for the whole episode.
+//   fc1 weights, fc2 weights, biases, the obs and avail rows of the current step, fc1 output x and the
+//   hidden state h (double buffered, indexed by env row) live in LDS.
+//   A: fc1 + ReLU per (tile, chunk) -> x        B: GRU per (tile, chunk) -> h'      C: fc2 + select per tile
+// Arithmetic order is identical to v1 (same chunked K order, same bias folding).
+// Env phase: half-wave per env, lane per unit (v2 env above); wave w steps envs 2w and 2w + 1.
+// Barriers per step: A|B, B|C, C|env, env|A.
+struct RolloutLds2 {
+    int64_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, total;
+    int ldo, ldh;
+    RoEnvLds env;
+};
+
+__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N) {
+    RolloutLds2 r;
+    r.ldo = L.Dob + 4;
+    r.ldh = L.H + 4;
+    int64_t o = 0;
+    r.w1o = ro_take(o, (int64_t)L.H * r.ldo);
+    r.w1a = ro_take(o, L.last_action ? (int64_t)L.A * r.ldh : 0);
+    r.w1n = ro_take(o, L.agent_id ? (int64_t)N * r.ldh : 0);
+    r.b1 = ro_take(o, L.H);
+    r.w2 = ro_take(o, (int64_t)L.Ap * r.ldh);
+    r.b2 = ro_take(o, L.Ap);
+    r.gb = ro_take(o, 4 * L.H);
+    const int rows = RE * N, rows16 = (rows + 15) / 16 * 16;
+    r.obs = ro_take(o, (int64_t)rows * r.ldo);
+    r.avail = ro_take(o, (int64_t)rows * L.A);
+    r.xb = ro_take(o, (int64_t)rows16 * r.ldh);
+    r.hsz = mlg_align4((int64_t)rows * r.ldh);
+    r.hb = ro_take(o, 2 * r.hsz);
+    r.pairtab = ro_take(o, (int64_t)N * U);
+    r.avtab = ro_take(o, (int64_t)N * L.A);
+    r.env = make_env_lds(o, U, N);
+    r.total = o;
+    return r;
+}
+
+__device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
+    for (int i = 0; i < k; ++i) m &= m - 1;
+    return __builtin_ctz(m);
+}
+
+template <int H>
+__global__ void __launch_bounds__(512) rollout_v2_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
+                                                        const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
+                                                        float eps, int test_mode, RolloutLds2 lay) {
+    constexpr int HC = H / 16;
+    constexpr int NW = 8;        // waves per workgroup
+    constexpr int G = NW / HC;   // waves sharing one feature chunk
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    float* fm = reinterpret_cast<float*>(smem);
+    SpecShared& SS = *reinterpret_cast<SpecShared*>(smem + lay.env.spec);
+    RoEnv R = env_view(smem, lay.env);
+    float* lobs = fm + lay.obs;
+    int32_t* lavail = smem + lay.avail;
+    int* pairtab = smem + lay.pairtab;
+    int* avtab = smem + lay.avtab;
+    const int U = spec.U, N = spec.n_agents, A = spec.n_actions;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int e0 = blockIdx.x * RE;
+    const int B = bt.B, T1 = bt.T1, ldo = lay.ldo, ldh = lay.ldh;
+    const int rows = RE * N;
+
+    load_spec_tables(spec, SS);
+    // small weights -> LDS (padded rows), activation buffers zeroed (obs pad columns stay zero), index tables
+    {
+        auto rows_cp = [&](int64_t src, int64_t dst, int nr, int nc, int ld) {
+            for (int i = tid; i < nr * nc; i += nthr) fm[dst + (int64_t)(i / nc) * ld + i % nc] = P[src + i];
+        };
+        for (int64_t i = tid; i < (int64_t)rows * ldo; i += nthr) fm[lay.obs + i] = 0.f;
+        for (int64_t i = tid; i < 2 * lay.hsz; i += nthr) fm[lay.hb + i] = 0.f;
+        rows_cp(L.w1o, lay.w1o, H, L.Dob, ldo);
+        if (L.last_action) rows_cp(L.w1a, lay.w1a, L.A, H, ldh);
+        if (L.agent_id) rows_cp(L.w1n, lay.w1n, N, H, ldh);
+        rows_cp(L.b1, lay.b1, 1, H, H);
+        rows_cp(L.w2, lay.w2, L.Ap, H, ldh);
+        rows_cp(L.b2, lay.b2, 1, L.Ap, L.Ap);
+        rows_cp(L.brz, lay.gb, 1, 2 * H, 2 * H);
+        rows_cp(L.bih + 2 * H, lay.gb + 2 * H, 1, H, H);
+        rows_cp(L.bhh + 2 * H, lay.gb + 3 * H, 1, H, H);
+        for (int k = tid; k < N * U; k += nthr) pairtab[k] = ((k / U) << 8) | (k % U);
+        for (int k = tid; k < N * A; k += nthr) avtab[k] = ((k / A) << 8) | (k % A);
+    }
+    __syncthreads();
+    const UnitMasks M = make_unit_masks(SS, U);
+    const float inv_p = 1.0f / (float)pow2_at_least(spec.grid);
+
+    // ---- env lanes: half-wave h of wave w owns env e = 2w + h, lane hl = unit ----
+    const int half = lane >> 5, hl = lane & 31, hbase = half * 32;
+    const int e = wave * 2 + half, b = e0 + e;
+    const bool uvalid = hl < U;
+    UnitLane UL{0, 0, 0, 0u, 0u, 0};
+    int ust = 2, uslot = 0, ulen = 0;
+    uint32_t uep = 0;
+    float uret = 0.f;
+    if (b < B) {  // reset (parallel_stepper.py:82-104; env_worker_process.py:54-60)
+        uep = st.episode[b];
+        ust = 0;
+        uslot = bt.ring_size > 0 ? (bt.ring_slot0 + b) % bt.ring_size : b;
+        if (uvalid) {
+            const int tm = SS.team[hl];
+            env_spawn_xyh(make_tables(spec, SS), mlg_env_key(spec.seed, b), uep, hl, SS.team_first[tm],
+                          SS.team_size[tm], UL.x, UL.y, UL.hp);
+        }
+        if (hl == 0) {
+            st.episode[b] = uep + 1;
+            bt.filled[(int64_t)uslot * T1] = 1;
+        }
+    }
+    if (hl == 0) {
+        R.status[e] = ust;
+        R.slot[e] = uslot;
+        R.episode[e] = uep;
+    }
+    if (b < B) {
+        v2_pair_pass(M, U, hbase, hl, UL);
+        v2_observe(M, spec, SS, pairtab, avtab, bt, uslot, 0, e, hbase, hl, UL, lobs, ldo, lavail, inv_p);
+    }
+
+    // this wave's GRU weight rows (chunk j, all three gates), A-operand layout, for the whole episode
+    const int j = wave % HC, gi = wave / HC;
+    floatx4 wi[3][HC], wh[3][HC];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int kc = 0; kc < HC; ++kc) {
+            const int64_t r = (int64_t)(q * H + j * 16 + col) * H + kc * 16 + 4 * g;
+            wi[q][kc] = ld4(P + L.wih + r);
+            wh[q][kc] = ld4(P + L.whh + r);
+        }
+    const floatx4 br = ld4(fm + lay.gb + j * 16 + 4 * g), bz = ld4(fm + lay.gb + H + j * 16 + 4 * g);
+    const floatx4 bin = ld4(fm + lay.gb + 2 * H + j * 16 + 4 * g), bhn = ld4(fm + lay.gb + 3 * H + j * 16 + 4 * g);
+    __syncthreads();
+    Stamps sp;
+    sp.init();
+    const int n_at = L.Ap / 16, KO = L.Dob / 16;
+    for (int t = 0; t < T1; ++t) {
+        // running envs (status < 2), uniform over the workgroup
+        const uint32_t run = (uint32_t)__ballot(lane < RE && R.status[lane & (RE - 1)] < 2);
+        if (run == 0) break;
+        const int rows_run = __builtin_popcount(run) * N;
+        const int tiles = (rows_run + 15) / 16;
+        const float* hc = fm + lay.hb + (t & 1) * lay.hsz;
+        float* hn = fm + lay.hb + ((t & 1) ^ 1) * lay.hsz;
+        auto row_of = [&](int cr, int& ee, int& nn) {
+            const bool v = cr < rows_run;
+            const int k = v ? cr / N : 0;
+            nn = v ? cr - k * N : 0;
+            ee = nth_set_bit(run, k);
+            return v;
+        };
+        // ---- A: fc1 + ReLU for (tile, chunk j) ----
+        for (int ti = gi; ti < tiles; ti += G) {
+            int zero = 0;
+            asm volatile("" : "+s"(zero));
+            const int cr = ti * 16 + col;
+            int ee, n;
+            const bool valid = row_of(cr, ee, n);
+            const int er = ee * N + n;
+            floatx4 acc = ld4(fm + lay.b1 + zero + j * 16 + 4 * g);
+            const int pa = (valid && t > 0) ? R.prev[er] : -1;
+            if (L.last_action && pa >= 0) acc += ld4(fm + lay.w1a + (int64_t)pa * ldh + j * 16 + 4 * g);
+            if (L.agent_id) acc += ld4(fm + lay.w1n + (int64_t)n * ldh + j * 16 + 4 * g);
+            const float* wrow = fm + lay.w1o + zero + (int64_t)(j * 16 + col) * ldo + 4 * g;
+            const float* orow = lobs + (int64_t)er * ldo + 4 * g;
+            for (int kc = 0; kc < KO; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), ld4(orow + kc * 16), acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.f);
+            *reinterpret_cast<floatx4*>(fm + lay.xb + (int64_t)cr * ldh + j * 16 + 4 * g) = acc;
+        }
+        sp.mark(0);
+        __syncthreads();
+        // ---- B: GRU cell for (tile, chunk j) -> h' rows of running envs ----
+        for (int ti = gi; ti < tiles; ti += G) {
+            const int cr = ti * 16 + col;
+            int ee, n;
+            const bool valid = row_of(cr, ee, n);
+            const int er = ee * N + n;
+            const float* xr = fm + lay.xb + (int64_t)cr * ldh + 4 * g;
+            const float* hr = hc + (int64_t)er * ldh + 4 * g;
+            floatx4 ar = br, az = bz, ain = bin, ahn = bhn;
+#pragma unroll
+            for (int kc = 0; kc < HC; ++kc) {
+                const floatx4 xin = ld4(xr + kc * 16), hin = ld4(hr + kc * 16);
+                ar = mfma_chunk(wi[0][kc], xin, ar);
+                az = mfma_chunk(wi[1][kc], xin, az);
+                ain = mfma_chunk(wi[2][kc], xin, ain);
+                ar = mfma_chunk(wh[0][kc], hin, ar);
+                az = mfma_chunk(wh[1][kc], hin, az);
+                ahn = mfma_chunk(wh[2][kc], hin, ahn);
+            }
+            const floatx4 ho = ld4(hr + j * 16);
+            floatx4 hv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float rg = 1.f / (1.f + expf(-ar[r]));
+                const float zg = 1.f / (1.f + expf(-az[r]));
+                const float ng = tanhf(ain[r] + rg * ahn[r]);
+                hv[r] = ng + zg * (ho[r] - ng);
+            }
+            if (valid) *reinterpret_cast<floatx4*>(hn + (int64_t)er * ldh + j * 16 + 4 * g) = hv;
+        }
+        sp.mark(1);
+        __syncthreads();
+        // ---- C: fc2 + masked argmax + epsilon-greedy per tile ----
+        for (int ti = wave; ti < tiles; ti += NW) {
+            int zero = 0;
+            asm volatile("" : "+s"(zero));
+            const int cr = ti * 16 + col;
+            int ee, n;
+            const bool valid = row_of(cr, ee, n);
+            const int er = ee * N + n;
+            const float* hr = hn + (int64_t)er * ldh + 4 * g;
+            const int32_t* av = lavail + er * A;
+            ArgmaxState as{-INFINITY, 1 << 30};
+            for (int at = 0; at < n_at; ++at) {
+                floatx4 q = ld4(fm + lay.b2 + zero + at * 16 + 4 * g);
+                const float* w2r = fm + lay.w2 + zero + (int64_t)(at * 16 + col) * ldh + 4 * g;
+#pragma unroll
+                for (int kc = 0; kc < HC; ++kc) q = mfma_chunk(ld4(w2r + kc * 16), ld4(hr + kc * 16), q);
+                argmax_accumulate(as, q, av, at, A, lane);
+            }
+            const int act = argmax_reduce(as);
+            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, ee, n, e0 + ee, t, eps, test_mode);
+        }
+        sp.mark(2);
+        __syncthreads();
+        sp.mark(3);
+        // ---- env phase: half-wave per env (env_worker_process.py:32-53 batched) ----
+        if (ust != 2) {
+            if (hl < N) R.prev[e * N + hl] = R.pact[e * N + hl];
+            if (ust == 1) {  // final action recorded; env done (parallel_stepper.py:153)
+                ust = 2;
+            } else {
+                // E1: executed action -- validated policy action or the scripted AI choice (spec §3.4)
+                int act = 0;
+                if (uvalid) {
+                    const int ag = SS.agent[hl];
+                    if (ag) {
+                        const int a = R.pact[e * N + ag - 1];
+                        act = (a >= 0 && a < MLG_ACT_BASE + U && v2_avail(M, spec.grid, UL.x, UL.y, UL.hp, UL.tgt, a)) ? a : 0;
+                    } else {
+                        act = UL.ai;
                     }
                 }
-                s_pact[e * N + n] = act;
-                bt.actions[bt_off] = act;
-                if (bt.full_write)
-                    for (int k = 0; k < A; ++k) bt.actions_onehot[bt_off * A + k] = k == act ? 1.0f : 0.0f;
-                else
-                    bt.actions_onehot[bt_off * A + act] = 1.0f;
-            }
-        }
-        MLG_STAMP(0);
-        __syncthreads();
-        MLG_STAMP(1);
-        // ================= env phase (status 0 envs) ===========================================
-        for (int i = tid; i < RE * U; i += nthr) {
-            const int e = i / U, u = i % U;
-            if (s_status[e] != 0) continue;
-            const int ag = SS.agent[u];
-            s_act[e * U + u] = env_exec_action(T, s_x + e * U, s_y + e * U, s_hp + e * U, u,
-                                               ag ? (int64_t)s_pact[e * N + ag - 1] : 0);
-        }
-        __syncthreads();
-        MLG_STAMP(2);
-        for (int i = tid; i < RE * U; i += nthr) {
-            const int e = i / U, j = i % U;
-            if (s_status[e] != 0) continue;
-            s_nhp[e * U + j] = env_resolve_hp(T, s_act + e * U, s_hp + e * U, j);
-            if (s_hp[e * U + j] > 0) env_apply_move(s_act[e * U + j], &s_x[e * U + j], &s_y[e * U + j]);
-        }
-        __syncthreads();
-        MLG_STAMP(3);
-        for (int e = tid; e < RE; e += nthr) {
-            const int b = e0 + e;
-            const int status = s_status[e];
-            s_stepped[e] = 0;
-            if (status == 2) continue;
-            for (int n = 0; n < N; ++n) s_prev[e * N + n] = s_pact[e * N + n];
-            if (status == 1) {  // final action recorded; env done (parallel_stepper.py:153)
-                s_status[e] = 2;
-                if (bt.full_write) {
-                    bt.reward[(int64_t)s_slot[e] * T1 + t] = 0.f;
-                    bt.terminated[(int64_t)s_slot[e] * T1 + t] = 0;
+                sp.mark(4);
+                // E2: simultaneous resolution on the pre-step state, then moves (spec §3.4)
+                const int pk = pk_unit(UL.x, UL.y, UL.hp);
+                int dmg = 0, heal = 0;
+                for (int i = 0; i < U; ++i) {
+                    const int qi = __shfl(pk, hbase + i, 64), ai = __shfl(act, hbase + i, 64);
+                    const bool hit = pk_hp(qi) > 0 && ai == MLG_ACT_BASE + hl;
+                    const int ri = mask_role(M, i);
+                    heal += (hit && ri == 1) ? role_power(1) : 0;
+                    dmg += (hit && ri != 1) ? role_power(ri) : 0;
                 }
-                continue;
-            }
-            int alive[2] = {0, 0}, lost[2] = {0, 0}, kills[2] = {0, 0};
-            for (int j = 0; j < U; ++j) {
-                const int tm = SS.team[j];
-                const int h0 = s_hp[e * U + j], h1 = s_nhp[e * U + j];
-                if (h0 > 0) {
-                    lost[tm] += h0 - h1 > 0 ? h0 - h1 : 0;
-                    if (h1 == 0) kills[1 - tm] += 1;
+                const int h0 = UL.hp;
+                int h1 = h0;
+                if (uvalid && h0 > 0) {
+                    const int v = h0 - dmg + heal, mx = role_maxhp(mask_role(M, hl));
+                    h1 = v < 0 ? 0 : (v > mx ? mx : v);
+                    UL.x += (act == 3) - (act == 4);  // env_apply_move on registers
+                    UL.y += (act == 1) - (act == 2);
                 }
-                if (h1 > 0) alive[tm] += 1;
-                s_hp[e * U + j] = h1;
-            }
-            const int done = alive[0] == 0 || alive[1] == 0 || t + 1 >= spec.episode_limit;
-            int won[2];
-            won[0] = alive[1] == 0 && alive[0] > 0;
-            won[1] = alive[0] == 0 && alive[1] > 0;
-            const int pt = spec.policy_team;
-            const int r_int = lost[1 - pt] + 10 * kills[pt] + 200 * won[pt];
-            const float r = (float)r_int * 0.0625f;
-            bt.reward[(int64_t)s_slot[e] * T1 + t] = r;
-            bt.terminated[(int64_t)s_slot[e] * T1 + t] = (uint8_t)done;
-            bt.filled[(int64_t)s_slot[e] * T1 + t + 1] = 1;
-            s_ret[e] += r;
-            s_stepped[e] = 1;
-            if (done) {
-                s_status[e] = 1;
-                s_len[e] = t + 1;
-                info.won[2 * b] = won[pt];
-                info.won[2 * b + 1] = won[1 - pt];
-                info.draw[b] = !won[0] && !won[1];
-            }
-        }
-        __syncthreads();
-        MLG_STAMP(4);
-        // observation at t + 1 for envs that stepped (incl. those that just terminated)
-        for (int i = tid; i < RE * N * U; i += nthr) {
-            const int e = i / (N * U), r = i % (N * U);
-            if (!s_stepped[e]) continue;
-            write_obs_item(T, spec, s_x + e * U, s_y + e * U, s_hp + e * U,
-                           bt.obs + ((int64_t)s_slot[e] * T1 + t + 1) * N * DO, r / U, r % U, inv_p);
-        }
-        for (int i = tid; i < RE * U; i += nthr) {
-            const int e = i / U, j = i % U;
-            if (!s_stepped[e]) continue;
-            float o[6];
-            env_state_feat(T, s_x + e * U, s_y + e * U, s_hp + e * U, j, inv_p, o);
-            float* dst = bt.state + ((int64_t)s_slot[e] * T1 + t + 1) * S + j * 6;
+                UL.hp = h1;
+                sp.mark(5);
+                // E3: per-env reduction over the half-wave (ballots + one packed shuffle sum)
+                const int my_team = (M.team1 >> hl) & 1;
+                const uint32_t alive_m = (uint32_t)(__ballot(uvalid && h1 > 0) >> hbase);
+                const uint32_t kill_m = (uint32_t)(__ballot(uvalid && h0 > 0 && h1 == 0) >> hbase);
+                int lostv = (uvalid && h0 > 0 && h0 > h1) ? (h0 - h1) << (16 * my_team) : 0;
 #pragma unroll
-            for (int f = 0; f < 6; ++f) dst[f] = o[f];
+                for (int m = 16; m >= 1; m >>= 1) lostv += __shfl_xor(lostv, m, 64);
+                const int alive0 = __builtin_popcount(alive_m & ~M.team1), alive1 = __builtin_popcount(alive_m & M.team1);
+                const int kills0 = __builtin_popcount(kill_m & M.team1), kills1 = __builtin_popcount(kill_m & ~M.team1);
+                const int lost0 = lostv & 0xFFFF, lost1 = lostv >> 16;
+                const int done = alive0 == 0 || alive1 == 0 || t + 1 >= spec.episode_limit;
+                const int won0 = alive1 == 0 && alive0 > 0, won1 = alive0 == 0 && alive1 > 0;
+                const int pt = spec.policy_team;
+                const int wpt = pt ? won1 : won0, wop = pt ? won0 : won1;
+                const int r_int = (pt ? lost0 : lost1) + 10 * (pt ? kills1 : kills0) + 200 * wpt;
+                const float r = (float)r_int * 0.0625f;
+                uret += r;
+                if (hl == 0) {
+                    const int64_t sl = (int64_t)uslot * T1 + t;
+                    bt.reward[sl] = r;
+                    bt.terminated[sl] = (uint8_t)done;
+                    bt.filled[sl + 1] = 1;
+                    if (done) {
+                        info.won[2 * b] = wpt;
+                        info.won[2 * b + 1] = wop;
+                        info.draw[b] = !won0 && !won1;
+                    }
+                }
+                if (done) {
+                    ust = 1;
+                    ulen = t + 1;
+                }
+                sp.mark(6);
+                // observation at t + 1 (incl. envs that just terminated)
+                v2_pair_pass(M, U, hbase, hl, UL);
+                v2_observe(M, spec, SS, pairtab, avtab, bt, uslot, t + 1, e, hbase, hl, UL, lobs, ldo, lavail, inv_p);
+                sp.mark(7);
+            }
+            if (hl == 0) R.status[e] = ust;
         }
-        for (int i = tid; i < RE * N * A; i += nthr) {
-            const int e = i / (N * A), r = i % (N * A);
-            if (!s_stepped[e]) continue;
-            bt.avail[((int64_t)s_slot[e] * T1 + t + 1) * N * A + r] =
-                env_avail_one(T, s_x + e * U, s_y + e * U, s_hp + e * U, spec.agent_unit[r / A], r % A);
-        }
-        // full-write mode: slot t+1 of envs that are done (t+1 > episode length) gets zeros
-        if (bt.full_write && t + 1 < T1) zero_slots(bt, s_slot, s_status, s_stepped, e0, B, t + 1, t + 2, N, A, S, DO);
-        if (tid == 0) {
-            int any = 0;
-            for (int e = 0; e < RE; ++e) any |= s_status[e] < 2;
-            s_any = any;
-        }
+        sp.mark(8);
         __syncthreads();
-        MLG_STAMP(5);
-        last_t = t;
-        if (!s_any) break;
+        sp.mark(10);
     }
-#ifdef MLG_STAMPS
-    if (lane == 0 && g_mlg_stamps) {
-        unsigned long long* o = g_mlg_stamps + ((int64_t)blockIdx.x * 8 + wave) * 8;
-        for (int k = 0; k < 6; ++k) o[k] = st_acc[k];
-        o[6] = __builtin_amdgcn_s_memtime() - st_begin;
-        o[7] = 1;
-    }
-#endif
-    // full-write mode: the remaining slots of every env (all of them are done here)
-    for (int e = tid; e < RE; e += nthr) s_stepped[e] = 0;
-    __syncthreads();
-    if (bt.full_write && last_t + 2 < T1) zero_slots(bt, s_slot, s_status, s_stepped, e0, B, last_t + 2, T1, N, A, S, DO);
+    sp.flush();
     // ---- per-env summary + env state write-back ----
-    for (int e = tid; e < RE; e += nthr) {
-        const int b = e0 + e;
-        if (b >= B) continue;
-        info.ep_len[b] = s_len[e];
-        info.ret[b] = s_ret[e];
-        st.t[b] = s_len[e];
-    }
-    for (int i = tid; i < RE * U; i += nthr) {
-        const int e = i / U, u = i % U;
-        const int64_t b = e0 + e;
-        if (b >= B) continue;
-        st.x[b * U + u] = s_x[e * U + u];
-        st.y[b * U + u] = s_y[e * U + u];
-        st.hp[b * U + u] = s_hp[e * U + u];
+    if (b < B) {
+        if (hl == 0) {
+            info.ep_len[b] = ulen;
+            info.ret[b] = uret;
+            st.t[b] = ulen;
+        }
+        if (uvalid) {
+            st.x[(int64_t)b * U + hl] = UL.x;
+            st.y[(int64_t)b * U + hl] = UL.y;
+            st.hp[(int64_t)b * U + hl] = UL.hp;
+        }
     }
 }
 
@@ -575,6 +1126,31 @@ int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec,
     return launch_rollout_t<H, TPW, false>(grid, threads, s, spec, st, L, P, bt, info, eps, tm, lay);
 }
 
+template <int H>
+int launch_rollout_v2(int grid, hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
+                      const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
+                      const RolloutLds2& lay) {
+    const size_t bytes = (size_t)lay.total * 4;
+    auto kern = rollout_v2_kernel<H>;
+    if (bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)bytes);
+        if (e != hipSuccess) return mlg::fail("rollout v2: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
+    return 0;
+}
+
+// v2 when the shape allows it (H 32/64, LDS fits) unless MLG_ROLLOUT_KERNEL=v1.
+bool use_rollout_v2(const AgentLayout& L, const MlgEnvSpec& spec, const MlgBatch& bt, RolloutLds2* lay) {
+    const char* k = getenv("MLG_ROLLOUT_KERNEL");
+    if (k && k[0] == 'v' && k[1] == '1') return false;
+    if (L.H != 64 && L.H != 32) return false;
+    if (spec.U > 32 || bt.full_write) return false;
+    *lay = make_rollout_lds2(L, spec.U, spec.n_agents);
+    return lay->total * 4 <= LDS_LIMIT_BYTES;
+}
+
 }  // namespace
 
 int check_agent_dims(const MlgAgentDims* d);  // agent.hip
@@ -696,6 +1272,13 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
     hipStream_t s = (hipStream_t)stream;
     const float eps = test_mode ? 0.f : epsilon;
     int rc = 0;
+    RolloutLds2 lay2;
+    if (use_rollout_v2(L, *spec, *batch, &lay2)) {
+        rc = dims->hidden == 64 ? launch_rollout_v2<64>(grid, s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
+                                : launch_rollout_v2<32>(grid, s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
+        if (rc) return rc;
+        return mlg::check_launch("rollout_v2_kernel");
+    }
 #define MLG_RO(HH, TT) rc = launch_rollout<HH, TT>(grid, threads, s, *spec, *st, L, packed, *batch, *info, eps, test_mode)
     if (dims->hidden == 64) {
         if (tpw == 1) MLG_RO(64, 1);

@@ -20,16 +20,22 @@ exp._init_stepper()
 st = exp.stepper
 st.t_env = 10 ** 6
 grid = (B + 15) // 16
-buf = torch.zeros(grid * 8 * 8, dtype=torch.int64, device="cuda")
+buf = torch.zeros(grid * 8 * 16, dtype=torch.int64, device="cuda")
 _native.call("mlg_debug_set_stamps", _native.ptr(buf))
 for it in range(3):
     buf.zero_()
     exp._train_episode(it * B)
 torch.cuda.synchronize()
-a = buf.view(grid, 8, 8).cpu().numpy().astype(np.float64)
-valid = a[:, :, 7] == 1
-names = ["agent", "barrier_after_agent", "E1_actions", "E2_resolve", "E3_reduce", "obs_write+final"]
-tot = a[:, :, 6][valid].mean()
+a = buf.view(grid, 8, 16).cpu().numpy().astype(np.float64)
+valid = a[:, :, 15] == 1
+if os.environ.get("MLG_ROLLOUT_KERNEL", "v2") == "v1":
+    names = ["agent", "barrier_after_agent", "-", "-"]
+    names += ["E1_exec_actions", "E2_resolve(+bar)", "E3_reduce(+bar)", "obs(+bar)", "state", "avail",
+              "zero+list+barrier"]
+else:
+    names = ["A_fc1", "B_gru(+barrier A)", "C_fc2_select(+barrier B)", "barrier_after_C", "E1_exec", "E2_resolve",
+             "E3_reduce", "pairs+obs/state/avail", "status", "-", "barrier_end"]
+tot = a[:, :, 14][valid].mean()
 print(f"rollout waves={valid.sum()} mean total cycles/wave={tot:.0f} (~{tot / 2.1e3:.1f} us at 2.1GHz)")
 for k, n in enumerate(names):
     v = a[:, :, k][valid]

@@ -316,3 +316,23 @@ def test_rollout_ring_mode_zero_copy_insert(device):
     for k in ref.data.transition_data:
         n = ref.episodes_in_buffer
         assert torch.equal(ring[k][:n], ref[k][:n]), k
+
+
+@pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium_1h_2t_2a", "medium"])
+def test_rollout_v2_equals_v1(device, plan, monkeypatch):
+    """The chunk-split, compacted headline kernel (v2) and the generic per-tile kernel (v1) compute in the same
+    arithmetic order: the whole batch and the run summary must be bit-identical."""
+    from maleague.envs.teams_env import VecEnvState
+    stepper, mac, args = _build_stepper(device, plan=plan, B=100, episode_limit=60, seed=3)
+    out = {}
+    for k in ("v1", "v2"):
+        monkeypatch.setenv("MLG_ROLLOUT_KERNEL", k)
+        stepper.envs = VecEnvState(stepper.spec, 100, device)
+        stepper.t_env = 30000
+        b, _ = stepper.run(test_mode=False)
+        out[k] = ({kk: b[kk].clone() for kk in b.data.transition_data},
+                  {kk: v.clone() for kk, v in stepper.last_run.items() if torch.is_tensor(v)})
+    for kk, v in out["v1"][0].items():
+        assert torch.equal(v, out["v2"][0][kk]), kk
+    for kk, v in out["v1"][1].items():
+        assert torch.equal(v, out["v2"][1][kk]), kk
