@@ -1,12 +1,15 @@
 // learner.hip -- QLearner.train (src/marl/learners/q_learner.py:34-131) as one device pipeline on gfx950.
 //
-//   pack        online/target agent + mixer weights -> kernel layouts (+ transposes for backward)
+//   pack        online/target agent + mixer weights -> kernel layouts (+ W_ih^T for backward)
 //   mask_sum    mask = filled[:, :-1] * (1 - terminated shifted) and its sum                (:36-42, :89-98)
-//   agent_fwd   online + target BPTT unroll, one workgroup per 16 sequence rows, wave w owns
-//               hidden chunk w; saves inputs/activations/gates for backward                  (:44-65)
+//   agent_in    fc1 + W_ih x for every (t, row), online + target, fully parallel               (:44-65)
+//   agent_rec   the recurrence only (W_hh h + gates), one workgroup per 16 sequence rows,
+//               wave w owns hidden chunk w with its W_hh rows in VGPRs; saves gates
+//   agent_q     fc2 for every (t, row), fully parallel
 //   mix_td      per (b, t) row: gather chosen Q, double-Q target, QMixer fwd (online+target),
 //               TD error, masked MSE partials, QMixer backward -> dQ and mixer deltas         (:55-98)
 //   agent_bwd   reverse-time GRU backward (dh carried in registers, dGH exchanged in LDS)    (:103)
+//   agent_dx    dX = W_ih^T dGI * relu' for every (t, row), fully parallel
 //   wgrad       every weight/bias gradient as sum_rows delta^T x, split over row chunks
 //               (deterministic slab reduction; MFMA with the row index as K)
 //   finish      loss/stat reduction, clip_grad_norm_(10), RMSprop step                       (:104-105, learner.py:25-31)
@@ -96,10 +99,10 @@ struct LCfg {
 
 // ---- workspace layout --------------------------------------------------------------------------------
 struct WsLayout {
-    int64_t p_on, p_tg, wihT, whhT, mix_on, mix_tg;
-    int64_t in, x, hs, gr, gz, gn, ghn, mac, tmac, dq, d2, dgi, dgh, da;
+    int64_t p_on, p_tg, wihT, mix_on, mix_tg;
+    int64_t in, x, hs, hs_tg, gi_on, gi_tg, gr, gz, gn, ghn, mac, tmac, dq, d2, dgi, dgh, da;
     int64_t srow, l1act, d1, da2, df2, dv2;
-    int64_t part, msum, slab, total;
+    int64_t part, msum, nrm, slab, total;
     int n_mix_tiles, n_tasks;
 };
 
@@ -188,120 +191,180 @@ __device__ __forceinline__ floatx4 tile_mm_lds(const float* __restrict__ W, int6
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 // ================================================================================================
-// forward unroll: blockIdx.x < ntiles -> online (saves), else target (q only)
+// forward, split into the parallel (non-recurrent) and the recurrent part:
+//   agent_in_kernel  (t, tile, net): dense input row (online), x = relu(fc1(inputs)), and
+//                    GI = [b_ir + b_hr + W_ir x | b_iz + b_hz + W_iz x | b_in + W_in x]  for every timestep
+//   agent_rec_kernel (tile, net):    h_t = GRU(GI_t, h_{t-1}) with W_hh in VGPRs, GI prefetched a step ahead
+//   agent_q_kernel   (t, tile, net): q = fc2(h_t)
+// The accumulation order per output is the one of the fused unroll (bias, W_ih x chunks, W_hh h chunks).
+// grid (ntiles, T, 2), HC waves: wave w computes x chunk w, then GI chunks w, w + HC, w + 2 HC.
 template <int H>
-__global__ void __launch_bounds__(512) agent_fwd_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ Pon,
-                                                        const float* __restrict__ Ptg, float* __restrict__ ws_in,
-                                                        float* __restrict__ ws_x, float* __restrict__ ws_hs,
-                                                        float* __restrict__ ws_gr, float* __restrict__ ws_gz,
-                                                        float* __restrict__ ws_gn, float* __restrict__ ws_ghn,
-                                                        float* __restrict__ mac, float* __restrict__ tmac) {
+__global__ void __launch_bounds__(512) agent_in_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ Pon,
+                                                       const float* __restrict__ Ptg, float* __restrict__ ws_in,
+                                                       float* __restrict__ ws_x, float* __restrict__ gi_on,
+                                                       float* __restrict__ gi_tg) {
     constexpr int HC = H / 16;
     constexpr int LDA = H + 4;
     __shared__ __attribute__((aligned(16))) float xs[16 * LDA];
+    const int tile = blockIdx.x, t = blockIdx.y;
+    const bool online = blockIdx.z == 0;
+    const float* P = online ? Pon : Ptg;
+    float* gi = online ? gi_on : gi_tg;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int N = c.N, A = c.A, R = c.R;
+    const int r = tile * 16 + col;
+    const bool valid = r < R;
+    const int b = valid ? r / N : 0, n = valid ? r % N : 0;
+    const int64_t boff = ((int64_t)b * bt.T1 + t) * N + n;
+    {
+        floatx4 acc = ld4(P + L.b1 + w * 16 + 4 * g);
+        if (valid) {
+            if (L.last_action && t > 0) {
+                const float* oh = bt.actions_onehot + (boff - N) * A;
+                for (int a = 0; a < A; ++a) {
+                    const float v = oh[a];
+                    if (v != 0.f) acc += v * ld4(P + L.w1a + (int64_t)a * H + w * 16 + 4 * g);
+                }
+            }
+            if (L.agent_id) acc += ld4(P + L.w1n + (int64_t)n * H + w * 16 + 4 * g);
+        }
+        const float* orow = valid ? bt.obs + boff * c.d_obs : nullptr;
+        const float* wrow = P + L.w1o + (int64_t)(w * 16 + col) * L.Dob + 4 * g;
+        for (int kc = 0; kc < L.Dob / 16; ++kc)
+            acc = mfma_chunk(ld4(wrow + kc * 16), load_chunk(orow, kc * 16 + 4 * g, c.d_obs), acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = fmaxf(acc[q], 0.f);
+        *reinterpret_cast<floatx4*>(xs + col * LDA + w * 16 + 4 * g) = acc;
+        if (online && valid) *reinterpret_cast<floatx4*>(ws_x + ((int64_t)t * R + r) * H + w * 16 + 4 * g) = acc;
+    }
+    if (online) {  // dense input row for dW1 (basic_controller.py:80-92 layout)
+        for (int i = tid; i < 16 * c.d_in; i += blockDim.x) {
+            const int rr = tile * 16 + i / c.d_in, k = i % c.d_in;
+            if (rr >= R) continue;
+            const int bb = rr / N, nn = rr % N;
+            const int64_t bo = ((int64_t)bb * bt.T1 + t) * N + nn;
+            float v;
+            if (k < c.d_obs) v = bt.obs[bo * c.d_obs + k];
+            else if (L.last_action && k < c.d_obs + A) v = t > 0 ? bt.actions_onehot[(bo - N) * A + (k - c.d_obs)] : 0.f;
+            else v = (k - c.d_obs - (L.last_action ? A : 0)) == nn ? 1.f : 0.f;
+            ws_in[((int64_t)t * R + rr) * c.d_in + k] = v;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {  // gate q, feature chunk w
+        floatx4 acc = q < 2 ? ld4(P + L.brz + q * H + w * 16 + 4 * g) : ld4(P + L.bih + 2 * H + w * 16 + 4 * g);
+        acc = tile_mm_lds(P + L.wih, H, q * H + w * 16, xs, LDA, HC, acc, lane);
+        if (valid) *reinterpret_cast<floatx4*>(gi + ((int64_t)t * R + r) * 3 * H + q * H + w * 16 + 4 * g) = acc;
+    }
+}
+
+// grid (2 * ntiles): blockIdx < ntiles online (saves gates), else target. HC waves, wave w owns chunk w.
+template <int H>
+__global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
+                                                        const float* __restrict__ Ptg, const float* __restrict__ gi_on,
+                                                        const float* __restrict__ gi_tg, float* __restrict__ hs_on,
+                                                        float* __restrict__ hs_tg, float* __restrict__ ws_gr,
+                                                        float* __restrict__ ws_gz, float* __restrict__ ws_gn,
+                                                        float* __restrict__ ws_ghn) {
+    constexpr int HC = H / 16;
+    constexpr int LDA = H + 4;
     __shared__ __attribute__((aligned(16))) float hs[2][16 * LDA];
     const int ntiles = (c.R + 15) / 16;
     const bool online = blockIdx.x < ntiles;
     const int tile = online ? blockIdx.x : blockIdx.x - ntiles;
     const float* P = online ? Pon : Ptg;
-    float* qout = online ? mac : tmac;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;  // wave w owns hidden chunk w
+    const float* gi = online ? gi_on : gi_tg;
+    float* hsg = online ? hs_on : hs_tg;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int col = lane & 15, g = lane >> 4;
+    const int R = c.R;
     const int r = tile * 16 + col;
-    const bool valid = r < c.R;
-    const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
-    const int N = c.N, A = c.A, R = c.R;
+    const bool valid = r < R;
+    const int f0 = w * 16 + 4 * g;  // this lane's 4 hidden features
+    floatx4 wr[3][HC];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int kc = 0; kc < HC; ++kc) wr[q][kc] = ld4(P + L.whh + (int64_t)(q * H + w * 16 + col) * H + kc * 16 + 4 * g);
+    const floatx4 bhn = ld4(P + L.bhh + 2 * H + f0);
     for (int i = tid; i < 16 * LDA; i += blockDim.x) hs[0][i] = 0.f;
-    if (online && w == 0 && valid)
-        for (int k = 0; k < H; k += 4) *reinterpret_cast<floatx4*>(ws_hs + (int64_t)r * H + k) = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (valid) *reinterpret_cast<floatx4*>(hsg + (int64_t)r * H + f0) = floatx4{0.f, 0.f, 0.f, 0.f};  // HS[0]
+    const int rr = valid ? r : 0;
+    auto gi_at = [&](int t, int q) { return ld4(gi + ((int64_t)t * R + rr) * 3 * H + q * H + f0); };
+    floatx4 nr = gi_at(0, 0), nz = gi_at(0, 1), nn = gi_at(0, 2);
     __syncthreads();
     int cur = 0;
     for (int t = 0; t < c.T; ++t) {
-        const float* Pt = P;
-        asm volatile("" : "+s"(Pt));
-        const int64_t boff = ((int64_t)b * bt.T1 + t) * N + n;
-        // ---- fc1 chunk w ----
-        {
-            floatx4 acc = ld4(Pt + L.b1 + w * 16 + 4 * g);
-            if (valid) {
-                if (L.last_action && t > 0) {
-                    const float* oh = bt.actions_onehot + (boff - N) * A;
-                    for (int a = 0; a < A; ++a) {
-                        const float v = oh[a];
-                        if (v != 0.f) acc += v * ld4(Pt + L.w1a + (int64_t)a * H + w * 16 + 4 * g);
-                    }
-                }
-                if (L.agent_id) acc += ld4(Pt + L.w1n + (int64_t)n * H + w * 16 + 4 * g);
-            }
-            const float* orow = valid ? bt.obs + boff * c.d_obs : nullptr;
-            const float* wrow = Pt + L.w1o + (int64_t)(w * 16 + col) * L.Dob + 4 * g;
-            for (int kc = 0; kc < L.Dob / 16; ++kc)
-                acc = mfma_chunk(ld4(wrow + kc * 16), load_chunk(orow, kc * 16 + 4 * g, c.d_obs), acc);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = fmaxf(acc[q], 0.f);
-            *reinterpret_cast<floatx4*>(xs + col * LDA + w * 16 + 4 * g) = acc;
-            if (online && valid) *reinterpret_cast<floatx4*>(ws_x + ((int64_t)t * R + r) * H + w * 16 + 4 * g) = acc;
+        floatx4 ar = nr, az = nz;
+        const floatx4 gin = nn;
+        if (t + 1 < c.T) {  // prefetch the next step's input gates
+            nr = gi_at(t + 1, 0);
+            nz = gi_at(t + 1, 1);
+            nn = gi_at(t + 1, 2);
         }
-        if (online) {  // dense input row for dW1 (basic_controller.py:80-92 layout)
-            for (int i = tid; i < 16 * c.d_in; i += blockDim.x) {
-                const int rr = tile * 16 + i / c.d_in, k = i % c.d_in;
-                if (rr >= R) continue;
-                const int bb = rr / N, nn = rr % N;
-                const int64_t bo = ((int64_t)bb * bt.T1 + t) * N + nn;
-                float v;
-                if (k < c.d_obs) v = bt.obs[bo * c.d_obs + k];
-                else if (L.last_action && k < c.d_obs + A) v = t > 0 ? bt.actions_onehot[(bo - N) * A + (k - c.d_obs)] : 0.f;
-                else v = (k - c.d_obs - (L.last_action ? A : 0)) == nn ? 1.f : 0.f;
-                ws_in[((int64_t)t * R + rr) * c.d_in + k] = v;
-            }
-        }
-        __syncthreads();
-        // ---- GRU chunk w ----
-        {
-            const float* hcur = hs[cur];
-            floatx4 ar = ld4(Pt + L.brz + w * 16 + 4 * g);
-            floatx4 az = ld4(Pt + L.brz + H + w * 16 + 4 * g);
-            floatx4 ain = ld4(Pt + L.bih + 2 * H + w * 16 + 4 * g);
-            floatx4 ahn = ld4(Pt + L.bhh + 2 * H + w * 16 + 4 * g);
-            ar = tile_mm_lds(Pt + L.wih, H, w * 16, xs, LDA, HC, ar, lane);
-            ar = tile_mm_lds(Pt + L.whh, H, w * 16, hcur, LDA, HC, ar, lane);
-            az = tile_mm_lds(Pt + L.wih, H, H + w * 16, xs, LDA, HC, az, lane);
-            az = tile_mm_lds(Pt + L.whh, H, H + w * 16, hcur, LDA, HC, az, lane);
-            ain = tile_mm_lds(Pt + L.wih, H, 2 * H + w * 16, xs, LDA, HC, ain, lane);
-            ahn = tile_mm_lds(Pt + L.whh, H, 2 * H + w * 16, hcur, LDA, HC, ahn, lane);
-            const floatx4 hp = ld4(hcur + col * LDA + w * 16 + 4 * g);
-            floatx4 rg, zg, ng, hn;
+        floatx4 ahn = bhn;
+        const float* hrow = hs[cur] + col * LDA + 4 * g;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                rg[q] = sigm(ar[q]);
-                zg[q] = sigm(az[q]);
-                ng[q] = tanhf(ain[q] + rg[q] * ahn[q]);
-                hn[q] = ng[q] + zg[q] * (hp[q] - ng[q]);
-            }
-            *reinterpret_cast<floatx4*>(hs[cur ^ 1] + col * LDA + w * 16 + 4 * g) = hn;
-            if (online && valid) {
-                const int64_t o = ((int64_t)t * R + r) * H + w * 16 + 4 * g;
+        for (int kc = 0; kc < HC; ++kc) {
+            const floatx4 hin = ld4(hrow + kc * 16);
+            ar = mfma_chunk(wr[0][kc], hin, ar);
+            az = mfma_chunk(wr[1][kc], hin, az);
+            ahn = mfma_chunk(wr[2][kc], hin, ahn);
+        }
+        const floatx4 hp = ld4(hs[cur] + col * LDA + f0);
+        floatx4 rg, zg, ng, hn;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            rg[q] = sigm(ar[q]);
+            zg[q] = sigm(az[q]);
+            ng[q] = tanhf(gin[q] + rg[q] * ahn[q]);
+            hn[q] = ng[q] + zg[q] * (hp[q] - ng[q]);
+        }
+        *reinterpret_cast<floatx4*>(hs[cur ^ 1] + col * LDA + f0) = hn;
+        if (valid) {
+            const int64_t o = ((int64_t)t * R + r) * H + f0;
+            *reinterpret_cast<floatx4*>(hsg + o + (int64_t)R * H) = hn;  // HS[t + 1]
+            if (online) {
                 *reinterpret_cast<floatx4*>(ws_gr + o) = rg;
                 *reinterpret_cast<floatx4*>(ws_gz + o) = zg;
                 *reinterpret_cast<floatx4*>(ws_gn + o) = ng;
                 *reinterpret_cast<floatx4*>(ws_ghn + o) = ahn;
-                *reinterpret_cast<floatx4*>(ws_hs + o + (int64_t)R * H) = hn;  // HS[t + 1]
             }
         }
         __syncthreads();
-        // ---- fc2: action tiles w, w + HC, ... ----
-        for (int at = w; at < L.Ap / 16; at += HC) {
-            floatx4 q = ld4(Pt + L.b2 + at * 16 + 4 * g);
-            q = tile_mm_lds(Pt + L.w2, H, at * 16, hs[cur ^ 1], LDA, HC, q, lane);
-            if (valid) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int a = at * 16 + 4 * g + k;
-                    if (a < A) qout[((int64_t)t * R + r) * A + a] = q[k];
-                }
-            }
-        }
         cur ^= 1;
+    }
+}
+
+// grid (ntiles, T, 2), Ap/16 waves: wave = action tile. q = b2 + W2 . h_t (h_t = HS[t + 1]).
+template <int H>
+__global__ void __launch_bounds__(512) agent_q_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
+                                                      const float* __restrict__ Ptg, const float* __restrict__ hs_on,
+                                                      const float* __restrict__ hs_tg, float* __restrict__ mac,
+                                                      float* __restrict__ tmac) {
+    constexpr int HC = H / 16;
+    const int tile = blockIdx.x, t = blockIdx.y;
+    const bool online = blockIdx.z == 0;
+    const float* P = online ? Pon : Ptg;
+    const float* hsg = (online ? hs_on : hs_tg) + (int64_t)(t + 1) * c.R * H;
+    float* qout = online ? mac : tmac;
+    const int lane = threadIdx.x & 63, at = threadIdx.x >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int r = tile * 16 + col;
+    const bool valid = r < c.R;
+    const float* hrow = hsg + (int64_t)(valid ? r : 0) * H + 4 * g;
+    const float* wrow = P + L.w2 + (int64_t)(at * 16 + col) * H + 4 * g;
+    floatx4 q = ld4(P + L.b2 + at * 16 + 4 * g);
+#pragma unroll
+    for (int kc = 0; kc < HC; ++kc) q = mfma_chunk(ld4(wrow + kc * 16), ld4(hrow + kc * 16), q);
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int a = at * 16 + 4 * g + k;
+            if (a < c.A) qout[((int64_t)t * c.R + r) * c.A + a] = q[k];
+        }
     }
 }
 
@@ -587,58 +650,73 @@ __global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs
 }
 
 // ================================================================================================
-// reverse-time GRU backward; wave w owns hidden chunk w (same ownership as agent_fwd_kernel)
+// reverse-time GRU backward; wave w owns hidden chunk w. W_hh^T rows of the chunk live in VGPRs, the
+// step's gate values are prefetched one step ahead, dGH is exchanged through LDS (double buffered).
+// dh_{t-1} = dh * z + W_hh^T dGH.  dX = W_ih^T dGI does not feed the recurrence: agent_dx_kernel.
 template <int H>
 __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ P,
-                                                        const float* __restrict__ wihT, const float* __restrict__ whhT,
-                                                        const float* __restrict__ ws_x, const float* __restrict__ ws_hs,
-                                                        const float* __restrict__ ws_gr, const float* __restrict__ ws_gz,
-                                                        const float* __restrict__ ws_gn, const float* __restrict__ ws_ghn,
-                                                        const float* __restrict__ dqv, float* __restrict__ dgi,
-                                                        float* __restrict__ dgh, float* __restrict__ da) {
+                                                        const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
+                                                        const float* __restrict__ ws_gz, const float* __restrict__ ws_gn,
+                                                        const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
+                                                        float* __restrict__ dgi, float* __restrict__ dgh) {
     constexpr int LDG = 3 * H + 4;
-    __shared__ __attribute__((aligned(16))) float sgi[16 * LDG];
-    __shared__ __attribute__((aligned(16))) float sgh[16 * LDG];
+    constexpr int KC = 3 * H / 16;
+    __shared__ __attribute__((aligned(16))) float sgh[2][16 * LDG];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int col = lane & 15, g = lane >> 4;
     const int r = blockIdx.x * 16 + col;
     const bool valid = r < c.R;
     const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
     const int R = c.R, N = c.N;
-    floatx4 dh = {0.f, 0.f, 0.f, 0.f};
-    const int f0 = w * 16 + 4 * g;  // this lane's 4 hidden features
-    for (int t = c.T - 1; t >= 0; --t) {
-        const int64_t o = ((int64_t)t * R + (valid ? r : 0)) * H + f0;
-        if (valid && t < c.T - 1) {
-            const float dq = dqv[(int64_t)t * R + r];
+    const int f0 = w * 16 + 4 * g;
+    // A operand of W_hh^T: row = feature w*16 + col, K = gate-row k: W_hh[k][feature]
+    floatx4 wt[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wt[kc][q] = P[L.whh + (int64_t)(kc * 16 + 4 * g + q) * H + w * 16 + col];
+    const int rr = valid ? r : 0;
+    struct Step {
+        floatx4 rg, zg, ng, ghn, hp, w2;
+        float dq;
+    };
+    auto load_step = [&](int t) {
+        Step s;
+        const int64_t o = ((int64_t)t * R + rr) * H + f0;
+        s.rg = ld4(ws_gr + o);
+        s.zg = ld4(ws_gz + o);
+        s.ng = ld4(ws_gn + o);
+        s.ghn = ld4(ws_ghn + o);
+        s.hp = ld4(ws_hs + o);  // HS[t] = h_{t-1}
+        s.dq = 0.f;
+        s.w2 = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (t < c.T - 1) {
+            s.dq = dqv[(int64_t)t * R + rr];
             const int a = (int)bt.actions[((int64_t)b * bt.T1 + t) * N + n];
-            dh += dq * ld4(P + L.w2 + (int64_t)a * H + f0);
+            s.w2 = ld4(P + L.w2 + (int64_t)a * H + f0);
         }
-        floatx4 rg = {0.f, 0.f, 0.f, 0.f}, zg = rg, ng = rg, ghn = rg, hp = rg;
-        if (valid) {
-            rg = ld4(ws_gr + o);
-            zg = ld4(ws_gz + o);
-            ng = ld4(ws_gn + o);
-            ghn = ld4(ws_ghn + o);
-            hp = ld4(ws_hs + o);  // HS[t] = h_{t-1}
-        }
+        return s;
+    };
+    floatx4 dh = {0.f, 0.f, 0.f, 0.f};
+    Step nx = load_step(c.T - 1);
+    int cur = 0;
+    for (int t = c.T - 1; t >= 0; --t) {
+        const Step s = nx;
+        if (t > 0) nx = load_step(t - 1);
+        if (valid && t < c.T - 1) dh += s.dq * s.w2;
         floatx4 drp, dzp, dnp, dghn, dhd;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float dn = dh[q] * (1.f - zg[q]);
-            const float dz = dh[q] * (hp[q] - ng[q]);
-            dhd[q] = dh[q] * zg[q];
-            dnp[q] = dn * (1.f - ng[q] * ng[q]);
-            const float dr = dnp[q] * ghn[q];
-            drp[q] = dr * rg[q] * (1.f - rg[q]);
-            dzp[q] = dz * zg[q] * (1.f - zg[q]);
-            dghn[q] = dnp[q] * rg[q];
+            const float dn = dh[q] * (1.f - s.zg[q]);
+            const float dz = dh[q] * (s.hp[q] - s.ng[q]);
+            dhd[q] = dh[q] * s.zg[q];
+            dnp[q] = dn * (1.f - s.ng[q] * s.ng[q]);
+            const float dr = dnp[q] * s.ghn[q];
+            drp[q] = dr * s.rg[q] * (1.f - s.rg[q]);
+            dzp[q] = dz * s.zg[q] * (1.f - s.zg[q]);
+            dghn[q] = dnp[q] * s.rg[q];
         }
-        float* gi = sgi + col * LDG;
-        float* gh = sgh + col * LDG;
-        *reinterpret_cast<floatx4*>(gi + f0) = drp;
-        *reinterpret_cast<floatx4*>(gi + H + f0) = dzp;
-        *reinterpret_cast<floatx4*>(gi + 2 * H + f0) = dnp;
+        float* gh = sgh[cur] + col * LDG;
         *reinterpret_cast<floatx4*>(gh + f0) = drp;
         *reinterpret_cast<floatx4*>(gh + H + f0) = dzp;
         *reinterpret_cast<floatx4*>(gh + 2 * H + f0) = dghn;
@@ -652,17 +730,37 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
             *reinterpret_cast<floatx4*>(dgh + o3 + 2 * H) = dghn;
         }
         __syncthreads();
-        // dh_{t-1} = dh * z + W_hh^T dGH ;  dA = (W_ih^T dGI) * (x > 0)
-        floatx4 dprev = tile_mm_lds(whhT, 3 * H, w * 16, sgh, LDG, 3 * H / 16, dhd, lane);
-        floatx4 dx = tile_mm_lds(wihT, 3 * H, w * 16, sgi, LDG, 3 * H / 16, floatx4{0.f, 0.f, 0.f, 0.f}, lane);
-        if (valid) {
-            const floatx4 xv = ld4(ws_x + o);
+        floatx4 dprev = dhd;
+        const float* ghr = sgh[cur] + col * LDG + 4 * g;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) dx[q] = xv[q] > 0.f ? dx[q] : 0.f;
-            *reinterpret_cast<floatx4*>(da + o) = dx;
-        }
+        for (int kc = 0; kc < KC; ++kc) dprev = mfma_chunk(wt[kc], ld4(ghr + kc * 16), dprev);
         dh = dprev;
-        __syncthreads();
+        cur ^= 1;
+    }
+}
+
+// dA = (W_ih^T dGI) * (x > 0) for every (t, row): grid (ntiles, T), HC waves (wave = feature chunk).
+template <int H>
+__global__ void __launch_bounds__(512) agent_dx_kernel(LCfg c, const float* __restrict__ wihT,
+                                                       const float* __restrict__ ws_x, const float* __restrict__ dgi,
+                                                       float* __restrict__ da) {
+    const int tile = blockIdx.x, t = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int r = tile * 16 + col;
+    const bool valid = r < c.R;
+    const int64_t row = (int64_t)t * c.R + (valid ? r : 0);
+    const float* wrow = wihT + (int64_t)(w * 16 + col) * 3 * H + 4 * g;
+    const float* grow = dgi + row * 3 * H + 4 * g;
+    floatx4 dx = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < 3 * H / 16; ++kc) dx = mfma_chunk(ld4(wrow + kc * 16), ld4(grow + kc * 16), dx);
+    if (valid) {
+        const int64_t o = row * H + w * 16 + 4 * g;
+        const floatx4 xv = ld4(ws_x + o);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dx[q] = xv[q] > 0.f ? dx[q] : 0.f;
+        *reinterpret_cast<floatx4*>(da + o) = dx;
     }
 }
 
@@ -722,9 +820,27 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WJobs J, float* __restrict__
 }
 
 // fixed-order sum over chunks -> dW, db
-__global__ void wgrad_reduce_kernel(WJobs J, const float* __restrict__ slab) {
+__device__ __forceinline__ float block_sum_1024(float v, float* red) {
+    // deterministic tree sum over blockDim.x (power of two <= 1024) threads; result in every thread
+    const int tid = threadIdx.x;
+    red[tid] = v;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (tid < w) red[tid] += red[tid + w];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// slab partials -> dW / db; every block also emits the sum of squares of the gradients it wrote
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(WJobs J, const float* __restrict__ slab,
+                                                           float* __restrict__ nrm_part) {
+    __shared__ float red[256];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (job, tile, 272)
     int64_t acc = 0;
+    float sq = 0.f;
     for (int q = 0; q < J.n; ++q) {
         const WJob& jb = J.j[q];
         const int64_t n_el = (int64_t)jb.mt * jb.nt * 272;
@@ -737,66 +853,66 @@ __global__ void wgrad_reduce_kernel(WJobs J, const float* __restrict__ slab) {
             for (int ch = 0; ch < jb.chunks; ++ch) s += base[(int64_t)ch * 272];
             if (e < 256) {
                 const int m = mt * 16 + e / 16, k = nt * 16 + e % 16;
-                if (m < jb.M && k < jb.K) jb.dw[(int64_t)m * jb.K + k] = s;
+                if (m < jb.M && k < jb.K) {
+                    jb.dw[(int64_t)m * jb.K + k] = s;
+                    sq = s * s;
+                }
             } else if (nt == 0 && jb.db) {
                 const int m = mt * 16 + (e - 256);
-                if (m < jb.M) jb.db[m] = s;
+                if (m < jb.M) {
+                    jb.db[m] = s;
+                    sq = s * s;
+                }
             }
-            return;
+            break;
         }
         acc += n_el;
     }
+    const float bs = block_sum_1024(sq, red);
+    if (threadIdx.x == 0) nrm_part[blockIdx.x] = bs;
 }
 
 // ================================================================================================
-// loss/stats, clip_grad_norm_, RMSprop (single workgroup; deterministic)
+// clip_grad_norm_ + RMSprop over all parameters (grid-wide; every block derives the same norm from the
+// per-block partials in a fixed order), loss/stat reduction in block 0.
 __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ part, int n_part,
                                                       const float* __restrict__ msum_p, float* __restrict__ params,
                                                       float* __restrict__ grads, float* __restrict__ sq, int64_t n_params,
                                                       float lr, float alpha, float eps, float max_norm, int N,
-                                                      float* __restrict__ stats) {
+                                                      float* __restrict__ stats, const float* __restrict__ nrm_part,
+                                                      int n_nrm) {
     __shared__ float red[1024];
-    __shared__ float s4[4];
     const int tid = threadIdx.x;
-    for (int k = 0; k < 4; ++k) {
-        float s = 0.f;
-        for (int i = tid; i < n_part; i += blockDim.x) s += part[(int64_t)i * 4 + k];
-        red[tid] = s;
-        __syncthreads();
-        for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-            if (tid < w) red[tid] += red[tid + w];
-            __syncthreads();
-        }
-        if (tid == 0) s4[k] = red[0];
-        __syncthreads();
-    }
     float s = 0.f;
-    for (int64_t i = tid; i < n_params; i += blockDim.x) s += grads[i] * grads[i];
-    red[tid] = s;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (tid < w) red[tid] += red[tid + w];
-        __syncthreads();
-    }
-    const float norm = sqrtf(red[0]);
+    for (int i = tid; i < n_nrm; i += blockDim.x) s += nrm_part[i];
+    const float norm = sqrtf(block_sum_1024(s, red));
     const float coef = fminf(max_norm / (norm + 1e-6f), 1.f);  // torch clip_grad_norm_ (clamped coef)
-    for (int64_t i = tid; i < n_params; i += blockDim.x) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
+    if (i < n_params) {
         const float gi = grads[i] * coef;
         grads[i] = gi;
         const float a = alpha * sq[i] + (1.f - alpha) * gi * gi;  // RMSprop square_avg
         sq[i] = a;
         params[i] -= lr * gi / (sqrtf(a) + eps);
     }
-    if (tid == 0) {
-        const float ms = msum_p[0];
-        stats[0] = s4[0] / ms;
-        stats[1] = norm;
-        stats[2] = s4[1] / ms;
-        stats[3] = s4[2] / (ms * N);
-        stats[4] = s4[3] / (ms * N);
-        stats[5] = ms;
-        stats[6] = ms;
-        stats[7] = 0.f;
+    if (blockIdx.x == 0) {
+        float s4[4];
+        for (int k = 0; k < 4; ++k) {
+            float v = 0.f;
+            for (int j = tid; j < n_part; j += blockDim.x) v += part[(int64_t)j * 4 + k];
+            s4[k] = block_sum_1024(v, red);
+        }
+        if (tid == 0) {
+            const float ms = msum_p[0];
+            stats[0] = s4[0] / ms;
+            stats[1] = norm;
+            stats[2] = s4[1] / ms;
+            stats[3] = s4[2] / (ms * N);
+            stats[4] = s4[3] / (ms * N);
+            stats[5] = ms;
+            stats[6] = ms;
+            stats[7] = 0.f;
+        }
     }
 }
 
@@ -863,12 +979,14 @@ Plan make_plan(const MlgLearnerCfg* cfg, int T1) {
     w.p_on = take(p.L.total);
     w.p_tg = take(p.L.total);
     w.wihT = take(3 * H * H);
-    w.whhT = take(3 * H * H);
     w.mix_on = take(p.mp.total);
     w.mix_tg = take(p.mp.total);
     w.in = take(T * R * c.d_in);
     w.x = take(T * R * H);
     w.hs = take((T + 1) * R * H);
+    w.hs_tg = take((T + 1) * R * H);
+    w.gi_on = take(T * R * 3 * H);
+    w.gi_tg = take(T * R * 3 * H);
     w.gr = take(T * R * H);
     w.gz = take(T * R * H);
     w.gn = take(T * R * H);
@@ -889,6 +1007,7 @@ Plan make_plan(const MlgLearnerCfg* cfg, int T1) {
     w.n_mix_tiles = (int)((RM + 15) / 16);
     w.part = take((int64_t)w.n_mix_tiles * 4);
     w.msum = take(4);
+    w.nrm = 0;  // placed after the slab (size known once the jobs are built)
     w.slab = o;
     w.total = o;  // + slab size, filled by make_jobs
     return p;
@@ -950,7 +1069,10 @@ WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
         tasks += J.j[q].mt * J.j[q].nt * J.j[q].chunks;
         slab += (int64_t)J.j[q].mt * J.j[q].nt * J.j[q].chunks * 272;
     }
-    *slab_floats = slab;
+    int64_t n_red = 0;
+    for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
+    *slab_floats = a4(slab) + a4((n_red + 255) / 256);  // slab partials + per-block norm partials
+    p.w.nrm = p.w.slab + a4(slab);
     *n_tasks = tasks;
     return J;
 }
@@ -972,7 +1094,6 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     if (pack_agent(params, ws + p.w.p_on) || pack_agent(tparams, ws + p.w.p_tg)) return 1;
     const int n3 = 3 * c.H * c.H;
     hipLaunchKernelGGL(transpose_kernel, dim3((n3 + 255) / 256), dim3(256), 0, s, params + p.ao.wih, ws + p.w.wihT, 3 * c.H, c.H);
-    hipLaunchKernelGGL(transpose_kernel, dim3((n3 + 255) / 256), dim3(256), 0, s, params + p.ao.whh, ws + p.w.whhT, 3 * c.H, c.H);
     MixPtrs Mon{}, Mtg{};
     if (c.mixer == 2) {
         const int64_t g0 = p.n_agent;
@@ -1002,26 +1123,35 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + p.w.msum);
     const int ntiles = (c.R + 15) / 16;
     const int threads = (c.H / 16) * 64;
-    hipLaunchKernelGGL((agent_fwd_kernel<H>), dim3(2 * ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on, ws + p.w.p_tg,
-                       ws + p.w.in, ws + p.w.x, ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn,
-                       ws + p.w.mac, ws + p.w.tmac);
+    hipLaunchKernelGGL((agent_in_kernel<H>), dim3(ntiles, c.T, 2), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
+                       ws + p.w.p_tg, ws + p.w.in, ws + p.w.x, ws + p.w.gi_on, ws + p.w.gi_tg);
+    hipLaunchKernelGGL((agent_rec_kernel<H>), dim3(2 * ntiles), dim3(threads), 0, s, c, p.L, ws + p.w.p_on, ws + p.w.p_tg,
+                       ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.gr, ws + p.w.gz,
+                       ws + p.w.gn, ws + p.w.ghn);
+    hipLaunchKernelGGL((agent_q_kernel<H>), dim3(ntiles, c.T, 2), dim3(64 * (c.Ap / 16)), 0, s, c, p.L, ws + p.w.p_on,
+                       ws + p.w.p_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.mac, ws + p.w.tmac);
     MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
               ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
     hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(64), 0, s, c, bt, Mon, Mtg, p.mp,
                        ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
-    hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on, ws + p.w.wihT,
-                       ws + p.w.whhT, ws + p.w.x, ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn,
-                       ws + p.w.dq, ws + p.w.dgi, ws + p.w.dgh, ws + p.w.da);
+    hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on, ws + p.w.hs,
+                       ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi, ws + p.w.dgh);
+    hipLaunchKernelGGL((agent_dx_kernel<H>), dim3(ntiles, c.T), dim3(threads), 0, s, c, ws + p.w.wihT, ws + p.w.x,
+                       ws + p.w.dgi, ws + p.w.da);
     int64_t slab_floats;
     int n_tasks;
     WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks);
     hipLaunchKernelGGL(wgrad_kernel, dim3((n_tasks + 3) / 4), dim3(256), 0, s, J, ws + p.w.slab);
-    int64_t n_red = 0;
+    int64_t n_red = 0;  // same count as make_jobs
     for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n_red + 255) / 256)), dim3(256), 0, s, J, ws + p.w.slab);
-    hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(1024), 0, s, ws + p.w.part, p.w.n_mix_tiles, ws + p.w.msum,
-                       bufs->params, bufs->grads, bufs->square_avg, p.n_agent + p.n_mixer, cfg->lr, cfg->optim_alpha,
-                       cfg->optim_eps, cfg->grad_norm_clip, c.N, bufs->stats);
+    const int n_red_blocks = (int)((n_red + 255) / 256);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + p.w.slab,
+                       ws + p.w.nrm);
+    const int64_t n_par = p.n_agent + p.n_mixer;
+    hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + p.w.part,
+                       p.w.n_mix_tiles, ws + p.w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr,
+                       cfg->optim_alpha, cfg->optim_eps, cfg->grad_norm_clip, c.N, bufs->stats, ws + p.w.nrm,
+                       n_red_blocks);
     return mlg::check_launch("qlearner_train");
 }
 

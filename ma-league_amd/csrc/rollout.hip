@@ -381,7 +381,7 @@ __device__ void ro_finish(const MlgEnvState& st, const RoEnv& R, const MlgRunInf
 // action_selectors.py:44-62) and records it: LDS pending action, batch actions / actions_onehot.
 __device__ __forceinline__ void ro_record_action(const MlgEnvSpec& spec, const RoEnv& R, const MlgBatch& bt, int act,
                                                  const int32_t* av, int e, int n, int b, int t, float eps,
-                                                 int test_mode) {
+                                                 int test_mode, bool onehot_row) {
     const int N = spec.n_agents, A = spec.n_actions;
     if (!test_mode && eps > 0.f) {
         const uint64_t key = mlg_env_key(spec.seed, b);
@@ -394,9 +394,9 @@ __device__ __forceinline__ void ro_record_action(const MlgEnvSpec& spec, const R
     R.pact[e * N + n] = act;
     const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
     bt.actions[bt_off] = act;
-    if (bt.full_write)
+    if (onehot_row)
         for (int k = 0; k < A; ++k) bt.actions_onehot[bt_off * A + k] = k == act ? 1.0f : 0.0f;
-    else
+    else if (!bt.full_write)
         bt.actions_onehot[bt_off * A + act] = 1.0f;
 }
 
@@ -483,7 +483,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                 argmax_accumulate(as, q, av, at, A, lane);
             }
             const int act = argmax_reduce(as);
-            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, e, n, e0 + e, t, eps, test_mode);
+            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, e, n, e0 + e, t, eps, test_mode, bt.full_write);
         }
         sp.mark(0);
         __syncthreads();
@@ -503,6 +503,37 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     __syncthreads();
     if (bt.full_write && last_t + 2 < T1) zero_slots(bt, R, e0, last_t + 2, T1, N, A, S, DO);
     ro_finish(st, R, info, e0, bt.B, U);
+}
+
+// Zero bytes [b0, b1) of base with nl lanes: 16-byte stores for the aligned interior, bytes at the ends.
+__device__ inline void zero_bytes_lanes(unsigned char* base, int64_t b0, int64_t b1, int lane, int nl) {
+    const int64_t a0 = (b0 + 15) & ~int64_t(15), a1 = b1 & ~int64_t(15);
+    if (a0 >= a1) {
+        for (int64_t x = b0 + lane; x < b1; x += nl) base[x] = 0;
+        return;
+    }
+    for (int64_t x = b0 + lane; x < a0; x += nl) base[x] = 0;
+    for (int64_t x = a0 + 16 * (int64_t)lane; x < a1; x += 16 * (int64_t)nl)
+        *reinterpret_cast<uint4*>(base + x) = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t x = a1 + lane; x < b1; x += nl) base[x] = 0;
+}
+
+// Full-write (ring) mode: zero timesteps [z0, z1) of every key of batch slot `slot`.
+__device__ inline void zero_slot_steps(const MlgBatch& bt, int slot, int z0, int z1, int N, int A, int S, int DO,
+                                       int lane, int nl) {
+    if (z0 >= z1) return;
+    const int64_t r0 = (int64_t)slot * bt.T1 + z0, r1 = (int64_t)slot * bt.T1 + z1;
+    auto z = [&](void* p, int64_t per) {
+        zero_bytes_lanes(reinterpret_cast<unsigned char*>(p), r0 * per, r1 * per, lane, nl);
+    };
+    z(bt.obs, (int64_t)N * DO * 4);
+    z(bt.state, (int64_t)S * 4);
+    z(bt.avail, (int64_t)N * A * 4);
+    z(bt.actions_onehot, (int64_t)N * A * 4);
+    z(bt.actions, (int64_t)N * 8);
+    z(bt.reward, 4);
+    z(bt.terminated, 1);
+    z(bt.filled, 8);
 }
 
 // ================================================================================================
@@ -752,7 +783,7 @@ __global__ void __launch_bounds__(512) rollout_v2_kernel(MlgEnvSpec spec, MlgEnv
     const int e = wave * 2 + half, b = e0 + e;
     const bool uvalid = hl < U;
     UnitLane UL{0, 0, 0, 0u, 0u, 0};
-    int ust = 2, uslot = 0, ulen = 0;
+    int ust = 2, uslot = 0, ulen = 0, zcur = T1;  // zcur: full-write tail zeroed below this step
     uint32_t uep = 0;
     float uret = 0.f;
     if (b < B) {  // reset (parallel_stepper.py:82-104; env_worker_process.py:54-60)
@@ -883,7 +914,7 @@ __global__ void __launch_bounds__(512) rollout_v2_kernel(MlgEnvSpec spec, MlgEnv
                 argmax_accumulate(as, q, av, at, A, lane);
             }
             const int act = argmax_reduce(as);
-            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, ee, n, e0 + ee, t, eps, test_mode);
+            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, ee, n, e0 + ee, t, eps, test_mode, false);
         }
         sp.mark(2);
         __syncthreads();
@@ -891,8 +922,20 @@ __global__ void __launch_bounds__(512) rollout_v2_kernel(MlgEnvSpec spec, MlgEnv
         // ---- env phase: half-wave per env (env_worker_process.py:32-53 batched) ----
         if (ust != 2) {
             if (hl < N) R.prev[e * N + hl] = R.pact[e * N + hl];
+            if (bt.full_write) {  // whole one-hot rows of the recorded actions
+                const int64_t oh = ((int64_t)uslot * T1 + t) * N * A;
+                for (int k = hl; k < N * A; k += 32) {
+                    const int pt = avtab[k];
+                    bt.actions_onehot[oh + k] = (pt & 255) == R.pact[e * N + (pt >> 8)] ? 1.0f : 0.0f;
+                }
+            }
             if (ust == 1) {  // final action recorded; env done (parallel_stepper.py:153)
                 ust = 2;
+                zcur = t + 1;
+                if (bt.full_write && hl == 0) {
+                    bt.reward[(int64_t)uslot * T1 + t] = 0.f;
+                    bt.terminated[(int64_t)uslot * T1 + t] = 0;
+                }
             } else {
                 // E1: executed action -- validated policy action or the scripted AI choice (spec §3.4)
                 int act = 0;
@@ -965,14 +1008,19 @@ __global__ void __launch_bounds__(512) rollout_v2_kernel(MlgEnvSpec spec, MlgEnv
                 sp.mark(7);
             }
             if (hl == 0) R.status[e] = ust;
+        } else if (bt.full_write && zcur < T1 && b < B) {  // idle half-wave: zero a few tail steps
+            const int z1 = zcur + 4 < T1 ? zcur + 4 : T1;
+            zero_slot_steps(bt, uslot, zcur, z1, N, A, 6 * U, 8 * U, hl, 32);
+            zcur = z1;
         }
         sp.mark(8);
         __syncthreads();
         sp.mark(10);
     }
     sp.flush();
-    // ---- per-env summary + env state write-back ----
+    // ---- per-env summary + env state write-back (+ the rest of the tail in full-write mode) ----
     if (b < B) {
+        if (bt.full_write) zero_slot_steps(bt, uslot, zcur, T1, N, A, 6 * U, 8 * U, hl, 32);
         if (hl == 0) {
             info.ep_len[b] = ulen;
             info.ret[b] = uret;
@@ -1146,7 +1194,7 @@ bool use_rollout_v2(const AgentLayout& L, const MlgEnvSpec& spec, const MlgBatch
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
     if (k && k[0] == 'v' && k[1] == '1') return false;
     if (L.H != 64 && L.H != 32) return false;
-    if (spec.U > 32 || bt.full_write) return false;
+    if (spec.U > 32) return false;
     *lay = make_rollout_lds2(L, spec.U, spec.n_agents);
     return lay->total * 4 <= LDS_LIMIT_BYTES;
 }

@@ -8,7 +8,6 @@ summary (episode length, return, won/draw) for t_env and the logger.
 """
 from __future__ import annotations
 
-import ctypes
 from collections.abc import Sequence
 from functools import partial
 
@@ -161,11 +160,9 @@ class ParallelStepper(EnvStepper):
         if ring is not None:
             slot0 = ring.buffer_index
             mb, keep = mlg_batch(ring)
-            # pre-zero the B ring slots in one launch (replaces the zero EpisodeBatch), then sparse writes
-            sb = (ctypes.c_int64 * 8)(*[t[0].numel() * t.element_size() for t in keep])
-            _native.call("mlg_zero_slots_bytes", _native.byref(mb), sb, slot0, self.batch_size, ring.buffer_size,
-                         _native.stream_ptr(self.device))
-            mb.B, mb.ring_slot0, mb.ring_size, mb.full_write = self.batch_size, slot0, ring.buffer_size, 0
+            # full-write mode: the kernel writes every byte of the B ring slots (zeros past each episode's end,
+            # by the idle lanes of finished envs), so nothing is zero-initialised or copied
+            mb.B, mb.ring_slot0, mb.ring_size, mb.full_write = self.batch_size, slot0, ring.buffer_size, 1
             self._launch_mb(mb, eps, test_mode)
             del keep
             self.home_batch = RingEpisodeBatch(ring, slot0, self.batch_size)

@@ -282,12 +282,14 @@ def test_rollout_headline_config_properties(device):
             np.testing.assert_array_equal(nb["obs"][b, t + 1], r.obs())
 
 
-def test_rollout_ring_mode_zero_copy_insert(device):
+@pytest.mark.parametrize("kernel", ["v2", "v1"])
+def test_rollout_ring_mode_zero_copy_insert(device, kernel, monkeypatch):
     """Train-mode rollouts written straight into the replay ring (full-write mode, wrap-around, garbage in the
     slots beforehand) equal the ordinary zero-initialised EpisodeBatch bit for bit, and the buffer indices
     advance exactly like ReplayBuffer.insert_episode_batch."""
     from maleague.components.replay_buffer import ReplayBuffer
     from maleague.envs.teams_env import VecEnvState
+    monkeypatch.setenv("MLG_ROLLOUT_KERNEL", kernel)
     stepper, mac, args = _build_stepper(device, plan="medium_1h_4t", B=48, episode_limit=30, seed=2)
     info = stepper.get_env_info()
     scheme, groups, preprocess = scheme_for(info, torch)
