@@ -82,19 +82,18 @@ def main():
     # rollout-kernel timing with HIP events on the stream the kernel is launched on
     stepper.timing = []
     t0_env = stepper.t_env
-    lens = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         exp._train_episode(episode)
         episode += B
-        lens.append(stepper.last_run["ep_len"])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     env_steps = stepper.t_env - t0_env
+    local_env_steps = env_steps
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -111,7 +110,8 @@ def main():
     N, A = info["n_agents"], info["n_actions"]
     d_in = info["obs_shape"] + A + N
     fl = agent_flops_per_forward(N, d_in, 64, A)
-    forwards = sum(int((l + 1).sum()) for l in lens) / len(lens)  # agent forwards per launch (env steps + final)
+    # agent forwards per launch: every env steps len times and records one final action (len + 1 forwards)
+    forwards = (local_env_steps + a.steps * B) / a.steps
     avg_kernel_s = sum(ev_ms) / len(ev_ms) / 1e3
     achieved = fl * forwards / avg_kernel_s
     traffic = None

@@ -75,6 +75,9 @@ typedef struct {
      * ring_size slots (the replay buffer itself -- zero-copy insert); full_write = 1 makes the kernel write
      * every byte of the slots it owns (zeros included), so the caller need not zero-initialise them. */
     int32_t ring_slot0, ring_size, full_write;
+    /* Sampled view (learner entry points only): episode b lives in slot rows[b] of tensors holding more
+     * slots (the replay buffer itself -- no gather copy); nullptr = identity. */
+    const int32_t *rows;
 } MlgBatch;
 
 /* Per-run episode summary written by mlg_rollout. */

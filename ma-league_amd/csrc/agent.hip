@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(256) agent_forward_kernel(AgentLayout L, const
         in.agent = 0;
     } else {
         const int N = L.N, b = row / N, n = row % N;
-        const int64_t off = ((int64_t)b * bt.T1 + t) * N + n;
+        const int64_t off = ((bt.rows ? (int64_t)bt.rows[b] : (int64_t)b) * bt.T1 + t) * N + n;
         in.x = valid ? bt.obs + off * L.d_obs : nullptr;
         in.onehot = (valid && t > 0) ? bt.actions_onehot + (off - N) * L.A : nullptr;
         in.agent = valid ? n : 0;

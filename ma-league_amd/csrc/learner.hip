@@ -154,10 +154,13 @@ __global__ void pack_mixer_kernel(MixPack mp, MixOffs mo, const float* __restric
     out[i] = v;
 }
 
+// episode b of the batch -> its slot in the tensors (sampled view of the replay buffer: rows[b])
+__device__ __forceinline__ int64_t bslot(const MlgBatch& bt, int b) { return bt.rows ? (int64_t)bt.rows[b] : (int64_t)b; }
+
 // ================================================================================================
 // mask: mask[b][t] = filled[b][t] * (t > 0 ? 1 - terminated[b][t-1] : 1), t < T-1
 __device__ __forceinline__ float mask_at(const MlgBatch& bt, int b, int t) {
-    const int64_t base = (int64_t)b * bt.T1;
+    const int64_t base = bslot(bt, b) * bt.T1;
     float m = (float)bt.filled[base + t];
     if (t > 0) m *= 1.f - (float)bt.terminated[base + t - 1];
     return m;
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(512) agent_in_kernel(LCfg c, MlgBatch bt, Agen
     const int r = tile * 16 + col;
     const bool valid = r < R;
     const int b = valid ? r / N : 0, n = valid ? r % N : 0;
-    const int64_t boff = ((int64_t)b * bt.T1 + t) * N + n;
+    const int64_t boff = (bslot(bt, b) * bt.T1 + t) * N + n;
     {
         floatx4 acc = ld4(P + L.b1 + w * 16 + 4 * g);
         if (valid) {
@@ -243,7 +246,7 @@ __global__ void __launch_bounds__(512) agent_in_kernel(LCfg c, MlgBatch bt, Agen
             const int rr = tile * 16 + i / c.d_in, k = i % c.d_in;
             if (rr >= R) continue;
             const int bb = rr / N, nn = rr % N;
-            const int64_t bo = ((int64_t)bb * bt.T1 + t) * N + nn;
+            const int64_t bo = (bslot(bt, bb) * bt.T1 + t) * N + nn;
             float v;
             if (k < c.d_obs) v = bt.obs[bo * c.d_obs + k];
             else if (L.last_action && k < c.d_obs + A) v = t > 0 ? bt.actions_onehot[(bo - N) * A + (k - c.d_obs)] : 0.f;
@@ -467,9 +470,9 @@ __device__ __forceinline__ void gather_q(const LCfg& c, const MlgBatch& bt, cons
     const int N = c.N, A = c.A, R = c.R;
     for (int n = 0; n < N; ++n) {
         const int r = b * N + n;
-        const int a = (int)bt.actions[((int64_t)b * bt.T1 + t) * N + n];
+        const int a = (int)bt.actions[(bslot(bt, b) * bt.T1 + t) * N + n];
         cq[n] = mac[((int64_t)t * R + r) * A + a];
-        const int32_t* av = bt.avail + ((int64_t)b * bt.T1 + t + 1) * N * A + (int64_t)n * A;
+        const int32_t* av = bt.avail + (bslot(bt, b) * bt.T1 + t + 1) * N * A + (int64_t)n * A;
         const float* qn = mac + ((int64_t)(t + 1) * R + r) * A;
         const float* tn = tmac + ((int64_t)(t + 1) * R + r) * A;
         if (c.double_q) {
@@ -512,11 +515,11 @@ __global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs
     for (int n = 0; n < N; ++n) cq[n] = tq[n] = 0.f;
     if (valid) gather_q(c, bt, mac, tmac, b, t, cq, tq);
     const float m = valid ? mask_at(bt, b, t) : 0.f;
-    const float rwd = valid ? bt.reward[(int64_t)b * bt.T1 + t] : 0.f;
-    const float term = valid ? (float)bt.terminated[(int64_t)b * bt.T1 + t] : 0.f;
+    const float rwd = valid ? bt.reward[bslot(bt, b) * bt.T1 + t] : 0.f;
+    const float term = valid ? (float)bt.terminated[bslot(bt, b) * bt.T1 + t] : 0.f;
     const float msum = msum_p[0];
-    const float* s0 = valid ? bt.state + ((int64_t)b * bt.T1 + t) * S : nullptr;
-    const float* s1 = valid ? bt.state + ((int64_t)b * bt.T1 + t + 1) * S : nullptr;
+    const float* s0 = valid ? bt.state + (bslot(bt, b) * bt.T1 + t) * S : nullptr;
+    const float* s1 = valid ? bt.state + (bslot(bt, b) * bt.T1 + t + 1) * S : nullptr;
     float qtot, tgt;
     floatx4 l1[Mx::L1T], pre[Mx::TE], hid[Mx::TE], wfp[Mx::TE];
     if (c.mixer == 2) {
@@ -643,7 +646,7 @@ __global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs
         for (int n = 0; n < N; ++n) {
             const int r = b * N + n;
             o.dq[(int64_t)t * c.R + r] = dq[n];
-            const int a = (int)bt.actions[((int64_t)b * bt.T1 + t) * N + n];
+            const int a = (int)bt.actions[(bslot(bt, b) * bt.T1 + t) * N + n];
             o.d2[((int64_t)t * c.R + r) * c.A + a] = dq[n];
         }
     }
@@ -692,7 +695,7 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
         s.w2 = floatx4{0.f, 0.f, 0.f, 0.f};
         if (t < c.T - 1) {
             s.dq = dqv[(int64_t)t * R + rr];
-            const int a = (int)bt.actions[((int64_t)b * bt.T1 + t) * N + n];
+            const int a = (int)bt.actions[(bslot(bt, b) * bt.T1 + t) * N + n];
             s.w2 = ld4(P + L.w2 + (int64_t)a * H + f0);
         }
         return s;

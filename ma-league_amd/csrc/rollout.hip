@@ -1306,6 +1306,7 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
                 "rollout: batch has null tensors");
     MLG_REQUIRE(info->ep_len && info->ret && info->won && info->draw, "rollout: run info has null tensors");
     MLG_REQUIRE(batch->B == st->B, "rollout: batch B=%d != env B=%d", batch->B, st->B);
+    MLG_REQUIRE(batch->rows == nullptr, "rollout: sampled (rows) views are read-only; use ring mode to write slots");
     MLG_REQUIRE(batch->T1 == spec->episode_limit + 1, "rollout: batch T1=%d != episode_limit+1=%d", batch->T1,
                 spec->episode_limit + 1);
     MLG_REQUIRE(dims->n_agents == spec->n_agents && dims->n_actions == spec->n_actions && dims->d_obs == 8 * spec->U,

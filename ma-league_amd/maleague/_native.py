@@ -39,7 +39,7 @@ class MlgBatch(ctypes.Structure):
                 ("avail", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
                 ("actions_onehot", ctypes.c_void_p), ("filled", ctypes.c_void_p), ("B", ctypes.c_int32),
                 ("T1", ctypes.c_int32), ("ring_slot0", ctypes.c_int32), ("ring_size", ctypes.c_int32),
-                ("full_write", ctypes.c_int32)]
+                ("full_write", ctypes.c_int32), ("rows", ctypes.c_void_p)]
 
 
 class MlgRunInfo(ctypes.Structure):

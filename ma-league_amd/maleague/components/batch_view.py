@@ -28,7 +28,13 @@ def _time_stride_ok(t: torch.Tensor, T1: int) -> bool:
 def mlg_batch(batch, required=KEYS):
     """Build an MlgBatch for `batch` (EpisodeBatch), making tensors contiguous when the layout is not
     a plain [B][T1][...] array. Returns (MlgBatch, keepalive-list)."""
-    data = batch.data.transition_data
+    rows = None
+    if getattr(batch, "rows", None) is not None and getattr(batch, "_data", None) is None:
+        # sampled view of a replay buffer: point at the buffer itself, episodes through the slot map
+        rows = batch.rows
+        data = batch.ring.data.transition_data
+    else:
+        data = batch.data.transition_data
     B = batch.batch_size
     ref = data["obs"]
     T1 = ref.stride(0) // max(1, ref.stride(1)) if ref.dim() > 1 and ref.stride(1) > 0 else ref.shape[1]
@@ -50,5 +56,5 @@ def mlg_batch(batch, required=KEYS):
         T1 = batch.max_seq_length
     p = lambda k: None if tensors[k] is None else tensors[k].data_ptr()  # noqa: E731
     mb = _native.MlgBatch(p("state"), p("obs"), p("actions"), p("avail_actions"), p("reward"), p("terminated"),
-                          p("actions_onehot"), p("filled"), B, T1, 0, 0, 0)
-    return mb, list(tensors.values())
+                          p("actions_onehot"), p("filled"), B, T1, 0, 0, 0, None if rows is None else rows.data_ptr())
+    return mb, list(tensors.values()) + [rows]

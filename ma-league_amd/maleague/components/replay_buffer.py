@@ -5,6 +5,7 @@ Lives on the training device (HBM) so sampling and training never cross PCIe.
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 from .episode_batch import EpisodeBatch
 
@@ -70,11 +71,18 @@ class ReplayBuffer(EpisodeBatch):
     def can_sample(self, batch_size: int) -> bool:
         return self.episodes_in_buffer >= batch_size
 
-    def sample(self, batch_size: int) -> EpisodeBatch:
+    def sample(self, batch_size: int, view: bool = False) -> EpisodeBatch:
+        """replay_buffer.py:50-57. view=True (device buffers): return a SampledEpisodeBatch that the kernels
+        read in place through a slot map instead of a gathered copy -- valid until those slots are rewritten."""
         assert self.can_sample(batch_size)
         if self.episodes_in_buffer == batch_size:
-            return self[:batch_size]
-        ep_ids = np.random.choice(self.episodes_in_buffer, batch_size, replace=False)
+            ep_ids = np.arange(batch_size)
+            if not view:
+                return self[:batch_size]
+        else:
+            ep_ids = np.random.choice(self.episodes_in_buffer, batch_size, replace=False)
+        if view and torch.device(self.device).type == "cuda":
+            return SampledEpisodeBatch(self, ep_ids)
         return self[ep_ids]
 
     def __repr__(self):
@@ -107,6 +115,38 @@ class RingEpisodeBatch(EpisodeBatch):
             self._data = SimpleNamespace(
                 transition_data={k: sel(v) for k, v in self.ring.data.transition_data.items()},
                 episode_data={k: sel(v) for k, v in self.ring.data.episode_data.items()})
+        return self._data
+
+    @data.setter
+    def data(self, value):
+        self._data = value
+
+
+class SampledEpisodeBatch(EpisodeBatch):
+    """`batch_size` episodes of a device ReplayBuffer, addressed through a slot map (MlgBatch.rows): the
+    learner kernels read the buffer in place, nothing is gathered. Host reads materialise a gathered copy.
+    The episodes keep the buffer's full length (max_seq_length); the filled mask makes the steps past each
+    episode inert in QLearner.train, exactly like the reference's [:, :max_t_filled] truncation."""
+
+    def __init__(self, ring: ReplayBuffer, ep_ids):
+        self.ring = ring
+        self.scheme, self.groups, self.preprocess = ring.scheme, ring.groups, ring.preprocess
+        self.batch_size, self.max_seq_length, self.device = len(ep_ids), ring.max_seq_length, ring.device
+        self.ep_ids = np.asarray(ep_ids, dtype=np.int64)
+        host = torch.from_numpy(self.ep_ids.astype(np.int32))
+        if torch.device(self.device).type == "cuda":
+            host = host.pin_memory()
+        self.rows = host.to(self.device, non_blocking=True)
+        self._data = None
+
+    @property
+    def data(self):
+        if self._data is None:
+            from types import SimpleNamespace
+            idx = self.rows.long()
+            self._data = SimpleNamespace(
+                transition_data={k: v.index_select(0, idx) for k, v in self.ring.data.transition_data.items()},
+                episode_data={k: v.index_select(0, idx) for k, v in self.ring.data.episode_data.items()})
         return self._data
 
     @data.setter

@@ -62,7 +62,7 @@ class BasicMAC(MultiAgentController):
         return q
 
     def update_trained_steps(self, update):
-        self.agent.trained_steps += update
+        self.agent.add_trained_steps(update)
 
     def init_hidden(self, batch_size):
         self.hidden_states = self.agent.init_hidden().unsqueeze(0).expand(batch_size, self.n_agents, -1)

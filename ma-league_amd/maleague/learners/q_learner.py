@@ -81,7 +81,8 @@ class QLearner(Learner):
         self.device = torch.device(getattr(args, "device", "cuda"))
         self._ws = None
         self._stats = None
-        self.last_stats = None
+        self._last_stats = None
+        self._stats_fresh = False
         self.train_calls = 0
 
     def parameters(self):
@@ -132,7 +133,9 @@ class QLearner(Learner):
                              optim_alpha=float(a.optim_alpha), optim_eps=float(a.optim_eps),
                              grad_norm_clip=float(a.grad_norm_clip))
 
-    def train(self, batch, t_env: int, episode_num: int):
+    def train(self, batch, t_env, episode_num: int):
+        """q_learner.py:34-131. `t_env` may also be a zero-argument callable, resolved after the device work
+        is queued (lets the caller avoid a host sync before the launch)."""
         if self.optimiser is None:
             raise RuntimeError("call build_optimizer() before train()")
         lib = _native.load(require_gpu=True)
@@ -153,14 +156,26 @@ class QLearner(Learner):
         if (episode_num - self.last_target_update_episode) / self.args.target_update_interval >= 1.0:
             self.update_targets()
             self.last_target_update_episode = episode_num
-        st = self._stats.cpu()  # one small D2H per train (the reference syncs here too, q_learner.py:112-113)
-        self.mac.update_trained_steps(int(st[6].item()))
-        self.last_stats = {"loss": float(st[0]), "grad_norm": float(st[1]), "td_error_abs": float(st[2]),
-                           "q_taken_mean": float(st[3]), "target_mean": float(st[4])}
+        # no host sync per train step: trained steps accumulate on the device, stats are read when logged
+        self.mac.update_trained_steps(self._stats[6])
+        self._stats_fresh = True
+        if callable(t_env):  # lazily resolved t_env: the kernels above are already queued
+            t_env = t_env()
         if t_env - self.log_stats_t >= self.args.learner_log_interval:
             for k, v in self.last_stats.items():
                 self.logger.log_stat(self.name + k, v, t_env)
             self.log_stats_t = t_env
+
+    @property
+    def last_stats(self):
+        """Stats of the latest train() (q_learner.py:115-124 values); reading them syncs the stream."""
+        if self._stats is None or not self._stats_fresh:
+            return self._last_stats
+        st = self._stats.cpu()
+        self._last_stats = {"loss": float(st[0]), "grad_norm": float(st[1]), "td_error_abs": float(st[2]),
+                            "q_taken_mean": float(st[3]), "target_mean": float(st[4])}
+        self._stats_fresh = False
+        return self._last_stats
 
     def update_targets(self):
         self._tflat.flat.copy_(self._flat.flat)

@@ -17,7 +17,29 @@ class AgentNetwork(nn.Module):
         super().__init__()
         self.args = args
         self.input_shape = input_shape
+        self._trained_host = 0
+        self._trained_dev = None  # device-side running count (no host sync per train step)
         self.trained_steps = 0
+
+    @property
+    def trained_steps(self) -> int:
+        """Agent.trained_steps (agent_network.py:15): env steps trained on; device counts resolve on read."""
+        extra = 0 if self._trained_dev is None else int(round(float(self._trained_dev.item())))
+        return self._trained_host + extra
+
+    @trained_steps.setter
+    def trained_steps(self, value: int):
+        self._trained_host = int(value)
+        self._trained_dev = None
+
+    def add_trained_steps(self, update):
+        if torch.is_tensor(update):
+            if self._trained_dev is None:
+                self._trained_dev = update.detach().to(torch.float64).clone()
+            else:
+                self._trained_dev.add_(update.detach())
+        else:
+            self._trained_host += int(update)
 
     def init_hidden(self):
         raise NotImplementedError()

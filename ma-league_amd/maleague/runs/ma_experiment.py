@@ -127,6 +127,7 @@ class MultiAgentExperiment:
             it += 1
             if max_iterations is not None and it >= max_iterations:
                 break
+        self.stepper.flush()
         self.logger.log_stat("episode", episode, self.stepper.t_env)
         self.stepper.close_env()
         return self.stepper.log_t
@@ -137,6 +138,13 @@ class MultiAgentExperiment:
             self.on_episode_end(env_info)
         self.home_buffer.insert_episode_batch(episode_batch)
         if self.home_buffer.can_sample(self.args.batch_size):
+            if str(self.home_buffer.device) == str(self.args.device) and getattr(self.args, "sample_in_place", True):
+                # device buffer: the learner reads the sampled episodes in place over their full stored length
+                # (steps past max_t_filled are masked out, so loss and gradients equal the truncated batch's),
+                # and t_env resolves only after the learner is queued -- no host sync between the launches
+                sample = self.home_buffer.sample(self.args.batch_size, view=True)
+                self.home_learner.train(sample, lambda: self.stepper.t_env, episode_num)
+                return
             sample = self.home_buffer.sample(self.args.batch_size)
             max_ep_t = int(sample.max_t_filled())
             sample = sample[:, :max_ep_t]

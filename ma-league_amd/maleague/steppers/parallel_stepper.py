@@ -49,6 +49,24 @@ class EnvInfos(Sequence):
         return {"battle_won": [bool(self.won[i, 0]), bool(self.won[i, 1])], "draw": bool(self.draw[i])}
 
 
+class LazyEnvInfos(Sequence):
+    """env_infos of a run whose summary is still in flight: resolves (waits for the rollout) on first use."""
+
+    def __init__(self, stepper, run_id):
+        self._stepper, self._run_id, self._infos = stepper, run_id, None
+
+    def _get(self):
+        if self._infos is None:
+            self._infos = self._stepper._env_infos_of(self._run_id)
+        return self._infos
+
+    def __len__(self):
+        return self._stepper.batch_size
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+
 class EnvStepper:
     def __init__(self, args, logger, log_start_t=0):
         self.args = args
@@ -79,12 +97,17 @@ class ParallelStepper(EnvStepper):
         B = self.batch_size
         # one int32 buffer for the per-run summary -> one D2H copy per run
         self._info = torch.zeros(5 * B, dtype=torch.int32, device=self.device)
-        self.t = 0
+        pin = self.device.type == "cuda"
+        self._info_host = torch.zeros(5 * B, dtype=torch.int32, pin_memory=pin)
+        self._pending = None  # (run_id, event, test_mode): summary copy in flight
+        self._post = []       # resolved runs awaiting host post-processing (logger, env_infos)
+        self._runs = {}       # run_id -> (last_run dict, EnvInfos), the latest two
+        self._run_id = 0
+        self._t = 0
         self.env_steps_this_run = 0
         self.new_batch_fn = None
         self.home_mac = None
         self.home_batch = None
-        self.last_run = None
         self.timing = None  # list -> (start, end) HIP events around every rollout launch (bench.py)
         self._ring = None   # ReplayBuffer written in place (zero-copy insert), see attach_replay()
 
@@ -98,6 +121,82 @@ class ParallelStepper(EnvStepper):
 
     def get_env_info(self):
         return self.env_info
+
+    # ---- the run summary travels back asynchronously; host state resolves on first use --------------
+    @property
+    def t_env(self) -> int:
+        self._resolve()
+        return self._t_env
+
+    @t_env.setter
+    def t_env(self, value: int):
+        if getattr(self, "_pending", None) is not None:
+            self._resolve()
+        self._t_env = int(value)
+
+    @property
+    def t(self) -> int:
+        self._resolve()
+        return self._t
+
+    @t.setter
+    def t(self, value: int):
+        self._t = int(value)
+
+    @property
+    def last_run(self):
+        self._resolve()
+        self._finish_post()
+        return self._runs[self._run_id][0] if self._run_id in self._runs else None
+
+    def _resolve(self):
+        """Wait for the latest rollout's summary (t_env, t); the rest of the host work is deferred."""
+        if getattr(self, "_pending", None) is None:
+            return
+        run_id, ev, test_mode = self._pending
+        self._pending = None
+        ev.synchronize()
+        B = self.batch_size
+        host = self._info_host.numpy().copy()
+        ep_len = host[0:B]
+        self._t = int(ep_len.max())
+        if not test_mode:
+            self.env_steps_this_run = int(ep_len.sum())
+            self._t_env += self.env_steps_this_run
+        self._post.append((run_id, host, self._t, self._t_env))
+
+    def _finish_post(self):
+        B = self.batch_size
+        for run_id, host, t_max, t_env in self._post:
+            ep_len = host[0:B]
+            won = host[B:3 * B].reshape(B, 2).astype(bool)
+            draw = host[3 * B:4 * B].astype(bool)
+            ret = host[4 * B:5 * B].view(np.float32)
+            # env_infos in order of termination (parallel_stepper.py:124,183-184): by episode length, then index
+            order = np.lexsort((np.arange(B), ep_len))
+            infos = EnvInfos(won[order], draw[order])
+            last = {"ep_len": torch.from_numpy(ep_len.copy()), "returns": torch.from_numpy(ret.copy()), "order": order}
+            self._runs[run_id] = (last, infos)
+            self._runs.pop(run_id - 2, None)
+            self.logger.collect(Collectibles.RETURN, ret.astype(np.float64), origin=Originator.HOME, parallel=True)
+            self.logger.collect(Collectibles.WON, won[order, 0], origin=Originator.HOME, parallel=True)
+            self.logger.collect(Collectibles.WON, won[order, 1], origin=Originator.AWAY, parallel=True)
+            self.logger.collect(Collectibles.DRAW, draw[order], parallel=True)
+            self.logger.collect(Collectibles.STEPS, t_max, parallel=True)
+            self.logger.log(t_env)
+        self._post = []
+
+    def _env_infos_of(self, run_id):
+        self._resolve()
+        self._finish_post()
+        if run_id not in self._runs:
+            raise RuntimeError("env_infos of an old run are no longer available")
+        return self._runs[run_id][1]
+
+    def flush(self):
+        """Resolve and post-process every run launched so far."""
+        self._resolve()
+        self._finish_post()
 
     def attach_replay(self, buffer) -> bool:
         """Let train-mode runs write their episodes straight into `buffer`'s next slots (the buffer's
@@ -117,7 +216,8 @@ class ParallelStepper(EnvStepper):
         pass
 
     def reset(self):
-        self.t = 0
+        self._resolve()
+        self._t = 0
         self.env_steps_this_run = 0
 
     def _launch(self, batch: EpisodeBatch, epsilon: float, test_mode: bool):
@@ -169,28 +269,15 @@ class ParallelStepper(EnvStepper):
         else:
             self.home_batch = self.new_batch_fn()
             self._launch(self.home_batch, eps, test_mode)
-        B = self.batch_size
-        host = self._info.cpu().numpy()
-        ep_len = host[0:B]
-        won = host[B:3 * B].reshape(B, 2).astype(bool)
-        draw = host[3 * B:4 * B].astype(bool)
-        ret = host[4 * B:5 * B].view(np.float32)
-        self.t = int(ep_len.max())
-        if not test_mode:
-            self.env_steps_this_run = int(ep_len.sum())
-            self.t_env += self.env_steps_this_run
-        # env_infos in order of termination (parallel_stepper.py:124,183-184): by episode length, then env index
-        order = np.lexsort((np.arange(B), ep_len))
-        env_infos = EnvInfos(won[order], draw[order])
-        self.last_run = {"ep_len": torch.from_numpy(ep_len.copy()), "returns": torch.from_numpy(ret.copy()),
-                         "order": order}
-        self.logger.collect(Collectibles.RETURN, ret.astype(np.float64), origin=Originator.HOME, parallel=True)
-        self.logger.collect(Collectibles.WON, won[order, 0], origin=Originator.HOME, parallel=True)
-        self.logger.collect(Collectibles.WON, won[order, 1], origin=Originator.AWAY, parallel=True)
-        self.logger.collect(Collectibles.DRAW, draw[order], parallel=True)
-        self.logger.collect(Collectibles.STEPS, self.t, parallel=True)
-        self.logger.log(self.t_env)
-        return self.home_batch, env_infos
+        # summary of this run: async D2H into pinned memory; t_env / env_infos resolve on first use, the
+        # previous run's host post-processing runs now, while this rollout is on the GPU
+        self._info_host.copy_(self._info, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._run_id += 1
+        self._pending = (self._run_id, ev, test_mode)
+        self._finish_post()
+        return self.home_batch, LazyEnvInfos(self, self._run_id)
 
 
 class EpisodeStepper(ParallelStepper):

@@ -126,3 +126,55 @@ def test_qlearner_vs_oracle_on_rollout(device):
     for t in range(T):
         q = learner.mac.forward(sample, t)
         np.testing.assert_allclose(q.cpu().numpy(), q_ref[:, t].numpy(), atol=1e-4, rtol=0)
+
+
+def test_qlearner_sampled_view_equals_truncated_copy(device):
+    """QLearner.train on a SampledEpisodeBatch (in-place slot-map read of the device replay buffer, full stored
+    length) matches train on the reference path's gathered copy truncated to max_t_filled: same loss, stats,
+    updated parameters (fp32 summation order only) and trained_steps."""
+    from maleague.components.episode_batch import EpisodeBatch
+    from maleague.components.replay_buffer import ReplayBuffer
+    from maleague.controllers import BasicMAC
+    from maleague.custom_logging import MainLogger
+    from maleague.learners import QLearner
+    from maleague.steppers import ParallelStepper
+    args = qmix_args(batch_size_run=48, seed=4, env_args={"match_build_plan": "medium_1h_4t", "grid_size": 20,
+                                                          "stochastic_spawns": True, "episode_limit": 50})
+    stepper = ParallelStepper(args, MainLogger())
+    info = stepper.get_env_info()
+    args.n_agents, args.n_actions, args.state_shape = info["n_agents"], info["n_actions"], info["state_shape"]
+    scheme, groups, preprocess = scheme_for(info, torch)
+    buf = ReplayBuffer(scheme, groups, 100, 64, preprocess=preprocess, device=device)  # longer than episodes
+    torch.manual_seed(5)
+    learners = []
+    for _ in range(2):
+        torch.manual_seed(5)
+        mac = BasicMAC(buf.scheme, groups, args)
+        lrn = QLearner(mac, buf.scheme, _Log(), args, name="home")
+        lrn.build_optimizer()
+        learners.append(lrn)
+    stepper.initialize(scheme, groups, preprocess, learners[0].mac)
+    assert not stepper.attach_replay(buf)  # different length: plain inserts
+    stepper.t_env = 20000
+    for _ in range(3):  # 144 episodes into a 100-slot ring (wraps)
+        b, _ = stepper.run(test_mode=False)
+        buf.insert_episode_batch(b)
+    np.random.seed(0)
+    view = buf.sample(32, view=True)
+    assert view.max_seq_length == 64 and view.rows.dtype == torch.int32
+    copy_ = buf[view.ep_ids]
+    T = int(copy_.max_t_filled())
+    assert T <= 51
+    learners[0].train(view, lambda: 1, 0)
+    learners[1].train(copy_[:, :T], 1, 0)
+    s0, s1 = learners[0].last_stats, learners[1].last_stats
+    for k in s0:
+        np.testing.assert_allclose(s0[k], s1[k], rtol=1e-5, atol=1e-7, err_msg=k)
+    for (k, v0), v1 in zip(learners[0].mac.agent.state_dict().items(), learners[1].mac.agent.state_dict().values()):
+        np.testing.assert_allclose(v0.cpu().numpy(), v1.cpu().numpy(), atol=1e-6, rtol=0, err_msg=k)
+    for (k, v0), v1 in zip(learners[0].mixer.state_dict().items(), learners[1].mixer.state_dict().values()):
+        np.testing.assert_allclose(v0.cpu().numpy(), v1.cpu().numpy(), atol=1e-6, rtol=0, err_msg=k)
+    assert learners[0].mac.agent.trained_steps == learners[1].mac.agent.trained_steps > 0
+    # host reads of the view materialise the same episodes
+    for k in ("obs", "actions", "filled"):
+        assert torch.equal(view[k], copy_[k]), k
