@@ -505,35 +505,32 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     ro_finish(st, R, info, e0, bt.B, U);
 }
 
-// Zero bytes [b0, b1) of base with nl lanes: 16-byte stores for the aligned interior, bytes at the ends.
-__device__ inline void zero_bytes_lanes(unsigned char* base, int64_t b0, int64_t b1, int lane, int nl) {
-    const int64_t a0 = (b0 + 15) & ~int64_t(15), a1 = b1 & ~int64_t(15);
-    if (a0 >= a1) {
-        for (int64_t x = b0 + lane; x < b1; x += nl) base[x] = 0;
-        return;
-    }
-    for (int64_t x = b0 + lane; x < a0; x += nl) base[x] = 0;
-    for (int64_t x = a0 + 16 * (int64_t)lane; x < a1; x += 16 * (int64_t)nl)
-        *reinterpret_cast<uint4*>(base + x) = make_uint4(0u, 0u, 0u, 0u);
-    for (int64_t x = a1 + lane; x < b1; x += nl) base[x] = 0;
-}
-
 // Full-write (ring) mode: zero timesteps [z0, z1) of every key of batch slot `slot`.
 __device__ inline void zero_slot_steps(const MlgBatch& bt, int slot, int z0, int z1, int N, int A, int S, int DO,
                                        int lane, int nl) {
     if (z0 >= z1) return;
-    const int64_t r0 = (int64_t)slot * bt.T1 + z0, r1 = (int64_t)slot * bt.T1 + z1;
-    auto z = [&](void* p, int64_t per) {
-        zero_bytes_lanes(reinterpret_cast<unsigned char*>(p), r0 * per, r1 * per, lane, nl);
+    const int64_t r0 = (int64_t)slot * bt.T1 + z0, n = z1 - z0;
+    // obs and state rows are whole 16-byte multiples (8U and 6U floats, U even) when DO % 4 == 0 and S % 4 == 0
+    auto z16 = [&](float* p, int64_t per) {
+        if (per % 4 == 0) {
+            uint4* q = reinterpret_cast<uint4*>(p + r0 * per);
+            for (int64_t x = lane; x < n * per / 4; x += nl) q[x] = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            for (int64_t x = lane; x < n * per; x += nl) p[r0 * per + x] = 0.f;
+        }
     };
-    z(bt.obs, (int64_t)N * DO * 4);
-    z(bt.state, (int64_t)S * 4);
-    z(bt.avail, (int64_t)N * A * 4);
-    z(bt.actions_onehot, (int64_t)N * A * 4);
-    z(bt.actions, (int64_t)N * 8);
-    z(bt.reward, 4);
-    z(bt.terminated, 1);
-    z(bt.filled, 8);
+    z16(bt.obs, (int64_t)N * DO);
+    z16(bt.state, S);
+    for (int64_t x = lane; x < n * N * A; x += nl) {
+        bt.avail[r0 * N * A + x] = 0;
+        bt.actions_onehot[r0 * N * A + x] = 0.f;
+    }
+    for (int64_t x = lane; x < n * N; x += nl) bt.actions[r0 * N + x] = 0;
+    for (int64_t x = lane; x < n; x += nl) {
+        bt.reward[r0 + x] = 0.f;
+        bt.terminated[r0 + x] = 0;
+        bt.filled[r0 + x] = 0;
+    }
 }
 
 // ================================================================================================
@@ -580,36 +577,57 @@ struct UnitLane {
 // One pass over all units j of the env for unit u (every lane of the half-wave runs all U iterations):
 // attack/heal availability, sight, and the scripted AI choice (lowest-hp target in range, else nearest
 // ally for a healer when one is alive, else nearest enemy) -- spec §3.2-3.3 in mask form.
-__device__ __forceinline__ void v2_pair_pass(const UnitMasks& M, int U, int hbase, int u, UnitLane& L) {
+__device__ __forceinline__ void v2_pair_pass(const UnitMasks& M, int U, int u, UnitLane& L, int* spk) {
+    const uint32_t all = U >= 32 ? 0xFFFFFFFFu : ((1u << U) - 1u);
     const int my_team = (M.team1 >> u) & 1;
     const bool healer = (M.healer >> u) & 1;
     const int r2 = ((M.melee >> u) & 1) ? 2 : 9;
     const bool alive = L.hp > 0;
-    const int pk = pk_unit(L.x, L.y, L.hp);
-    int best = -1, besthp = 0, na = -1, nda = 0, ne = -1, nde = 0, adx = 0, ady = 0, edx = 0, edy = 0;
-    uint32_t tgt = 0, sight = 0;
-    for (int j = 0; j < U; ++j) {
-        const int q = __shfl(pk, hbase + j, 64);
+    const int hbase = (threadIdx.x & 63) & 32;
+    // alive units of the env (bit j) and this unit's ally / enemy candidate sets (spec §3.2-3.3)
+    const uint32_t alive_m = (uint32_t)(__ballot(u < U && L.hp > 0) >> hbase) & all;
+    const uint32_t mates = (my_team ? M.team1 : ~M.team1) & all;
+    const uint32_t cand_a = alive ? (mates & alive_m & ~(1u << u)) : 0u;
+    const uint32_t cand_e = alive ? (~mates & alive_m & all) : 0u;
+    const uint32_t seen = alive ? alive_m : 0u;
+    // packed unit states of the env through LDS (written and read by this half-wave only: in-order LDS
+    // queue of one wave, no barrier), read back four units per 16-byte broadcast load
+    spk[u] = pk_unit(L.x, L.y, L.hp);
+    // min-keys (value << 5 | j) give "smallest value, then lowest j" -- the spec's tie rule -- without branches
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    uint32_t kbest = NONE, kally = NONE, kenemy = NONE, tgt = 0, sight = 0;
+    auto visit = [&](int j, int q) {
         const int hj = pk_hp(q);
-        const int dx = pk_x(q) - L.x, dy = pk_y(q) - L.y, d2 = dx * dx + dy * dy;
-        const int tj = (M.team1 >> j) & 1;
-        const int mxj = ((M.tank >> j) & 1) ? 64 : 32;
-        if (alive && hj > 0) {
-            if (d2 <= MLG_SIGHT2) sight |= 1u << j;
-            const bool cond = healer ? (j != u && tj == my_team && hj < mxj) : (tj != my_team);
-            if (d2 <= r2 && cond) {
-                tgt |= 1u << j;
-                if (best < 0 || hj < besthp) { best = j; besthp = hj; }
-            }
-            if (j != u && tj == my_team && (na < 0 || d2 < nda)) { na = j; nda = d2; adx = dx; ady = dy; }
-            if (tj != my_team && (ne < 0 || d2 < nde)) { ne = j; nde = d2; edx = dx; edy = dy; }
-        }
+        const int dx = pk_x(q) - L.x, dy = pk_y(q) - L.y;
+        const uint32_t d2 = (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
+        const uint32_t bit = 1u << j;
+        const bool vis = (seen & bit) && d2 <= MLG_SIGHT2;
+        const bool inr = d2 <= (uint32_t)r2;
+        const int mxj = (M.tank & bit) ? 64 : 32;
+        const bool tg = inr && (healer ? ((cand_a & bit) && hj < mxj) : (cand_e & bit) != 0);
+        sight |= vis ? bit : 0u;
+        tgt |= tg ? bit : 0u;
+        kbest = min(kbest, tg ? ((uint32_t)hj << 5 | j) : NONE);
+        kally = min(kally, (cand_a & bit) ? (d2 << 5 | j) : NONE);
+        kenemy = min(kenemy, (cand_e & bit) ? (d2 << 5 | j) : NONE);
+    };
+    for (int j0 = 0; j0 < U; j0 += 4) {
+        const int4 q4 = *reinterpret_cast<const int4*>(spk + j0);
+        visit(j0, q4.x);
+        if (j0 + 1 < U) visit(j0 + 1, q4.y);
+        if (j0 + 2 < U) visit(j0 + 2, q4.z);
+        if (j0 + 3 < U) visit(j0 + 3, q4.w);
     }
     int ai = 0;
     if (alive) {
-        if (best >= 0) ai = MLG_ACT_BASE + best;
-        else if (healer && na >= 0) ai = nda > 2 ? move_toward_d(adx, ady) : 0;
-        else if (ne >= 0) ai = move_toward_d(edx, edy);
+        uint32_t k = NONE;
+        if (kbest != NONE) ai = MLG_ACT_BASE + (int)(kbest & 31);
+        else if (healer && kally != NONE) k = (kally >> 5) > 2 ? kally : NONE;
+        else k = kenemy;
+        if (ai == 0 && k != NONE) {
+            const int q = spk[k & 31];
+            ai = move_toward_d(pk_x(q) - L.x, pk_y(q) - L.y);
+        }
     }
     L.tgt = tgt;
     L.sight = sight;
@@ -631,7 +649,7 @@ __device__ __forceinline__ int v2_avail(const UnitMasks& M, int G, int x, int y,
 __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec& spec, const SpecShared& SS,
                                            const int* pairtab, const int* avtab, const MlgBatch& bt, int slot, int t,
                                            int e, int hbase, int hl, const UnitLane& L, float* lobs, int ldo,
-                                           int32_t* lavail, float inv_p) {
+                                           int32_t* lavail, float inv_p, Stamps& sp) {
     const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, G = spec.grid;
     const int64_t st_row = (int64_t)slot * bt.T1 + t;
     const int pk = pk_unit(L.x, L.y, L.hp);
@@ -659,6 +677,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
             *reinterpret_cast<floatx4*>(l + 4) = hi;
         }
     }
+    sp.mark(9);
     for (int k0 = 0; k0 < N * A; k0 += 32) {
         const int k = k0 + hl;
         const bool valid = k < N * A;
@@ -672,6 +691,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
             lavail[e * N * A + k] = v;
         }
     }
+    sp.mark(11);
     if (hl < U) {
         const int r = mask_role(M, hl);
         float* dst = bt.state + st_row * S + hl * 6;
@@ -679,6 +699,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
         *reinterpret_cast<float2*>(dst + 2) = make_float2((float)L.y * inv_p, (float)L.hp * inv_maxhp(r));
         *reinterpret_cast<float2*>(dst + 4) = make_float2((float)((M.team1 >> hl) & 1), (float)r * 0.5f);
     }
+    sp.mark(12);
 }
 
 // ================================================================================================
@@ -696,12 +717,12 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
 // Env phase: half-wave per env, lane per unit (v2 env above); wave w steps envs 2w and 2w + 1.
 // Barriers per step: A|B, B|C, C|env, env|A.
 struct RolloutLds2 {
-    int64_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, total;
+    int64_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, total;
     int ldo, ldh;
     RoEnvLds env;
 };
 
-__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N) {
+__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N, int rew) {
     RolloutLds2 r;
     r.ldo = L.Dob + 4;
     r.ldh = L.H + 4;
@@ -713,7 +734,7 @@ __host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, i
     r.w2 = ro_take(o, (int64_t)L.Ap * r.ldh);
     r.b2 = ro_take(o, L.Ap);
     r.gb = ro_take(o, 4 * L.H);
-    const int rows = RE * N, rows16 = (rows + 15) / 16 * 16;
+    const int rows = rew * N, rows16 = (rows + 15) / 16 * 16;
     r.obs = ro_take(o, (int64_t)rows * r.ldo);
     r.avail = ro_take(o, (int64_t)rows * L.A);
     r.xb = ro_take(o, (int64_t)rows16 * r.ldh);
@@ -721,6 +742,7 @@ __host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, i
     r.hb = ro_take(o, 2 * r.hsz);
     r.pairtab = ro_take(o, (int64_t)N * U);
     r.avtab = ro_take(o, (int64_t)N * L.A);
+    r.pk = ro_take(o, (int64_t)rew * 32);
     r.env = make_env_lds(o, U, N);
     r.total = o;
     return r;
@@ -731,308 +753,563 @@ __device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
     return __builtin_ctz(m);
 }
 
-template <int H>
-__global__ void __launch_bounds__(512) rollout_v2_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
-                                                        const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
-                                                        float eps, int test_mode, RolloutLds2 lay) {
-    constexpr int HC = H / 16;
-    constexpr int NW = 8;        // waves per workgroup
-    constexpr int G = NW / HC;   // waves sharing one feature chunk
-    extern __shared__ __attribute__((aligned(16))) int smem[];
+// Workgroup-wide prologue of the v2/v4 kernels: spec tables, small weights -> LDS (padded rows), activation
+// buffers zeroed (the obs pad columns stay zero), index tables.
+__device__ void v2_prologue(const MlgEnvSpec& spec, const AgentLayout& L, const float* __restrict__ P,
+                            const RolloutLds2& lay, int* smem, int rows) {
     float* fm = reinterpret_cast<float*>(smem);
     SpecShared& SS = *reinterpret_cast<SpecShared*>(smem + lay.env.spec);
-    RoEnv R = env_view(smem, lay.env);
-    float* lobs = fm + lay.obs;
-    int32_t* lavail = smem + lay.avail;
-    int* pairtab = smem + lay.pairtab;
-    int* avtab = smem + lay.avtab;
-    const int U = spec.U, N = spec.n_agents, A = spec.n_actions;
-    const int tid = threadIdx.x, nthr = blockDim.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int col = lane & 15, g = lane >> 4;
-    const int e0 = blockIdx.x * RE;
-    const int B = bt.B, T1 = bt.T1, ldo = lay.ldo, ldh = lay.ldh;
-    const int rows = RE * N;
-
+    const int tid = threadIdx.x, nthr = blockDim.x, H = L.H, N = spec.n_agents, U = spec.U, A = spec.n_actions;
     load_spec_tables(spec, SS);
-    // small weights -> LDS (padded rows), activation buffers zeroed (obs pad columns stay zero), index tables
-    {
-        auto rows_cp = [&](int64_t src, int64_t dst, int nr, int nc, int ld) {
-            for (int i = tid; i < nr * nc; i += nthr) fm[dst + (int64_t)(i / nc) * ld + i % nc] = P[src + i];
-        };
-        for (int64_t i = tid; i < (int64_t)rows * ldo; i += nthr) fm[lay.obs + i] = 0.f;
-        for (int64_t i = tid; i < 2 * lay.hsz; i += nthr) fm[lay.hb + i] = 0.f;
-        rows_cp(L.w1o, lay.w1o, H, L.Dob, ldo);
-        if (L.last_action) rows_cp(L.w1a, lay.w1a, L.A, H, ldh);
-        if (L.agent_id) rows_cp(L.w1n, lay.w1n, N, H, ldh);
-        rows_cp(L.b1, lay.b1, 1, H, H);
-        rows_cp(L.w2, lay.w2, L.Ap, H, ldh);
-        rows_cp(L.b2, lay.b2, 1, L.Ap, L.Ap);
-        rows_cp(L.brz, lay.gb, 1, 2 * H, 2 * H);
-        rows_cp(L.bih + 2 * H, lay.gb + 2 * H, 1, H, H);
-        rows_cp(L.bhh + 2 * H, lay.gb + 3 * H, 1, H, H);
-        for (int k = tid; k < N * U; k += nthr) pairtab[k] = ((k / U) << 8) | (k % U);
-        for (int k = tid; k < N * A; k += nthr) avtab[k] = ((k / A) << 8) | (k % A);
-    }
+    auto rows_cp = [&](int64_t src, int64_t dst, int nr, int nc, int ld) {
+        for (int i = tid; i < nr * nc; i += nthr) fm[dst + (int64_t)(i / nc) * ld + i % nc] = P[src + i];
+    };
+    for (int64_t i = tid; i < (int64_t)rows * lay.ldo; i += nthr) fm[lay.obs + i] = 0.f;
+    for (int64_t i = tid; i < 2 * lay.hsz; i += nthr) fm[lay.hb + i] = 0.f;
+    rows_cp(L.w1o, lay.w1o, H, L.Dob, lay.ldo);
+    if (L.last_action) rows_cp(L.w1a, lay.w1a, L.A, H, lay.ldh);
+    if (L.agent_id) rows_cp(L.w1n, lay.w1n, N, H, lay.ldh);
+    rows_cp(L.b1, lay.b1, 1, H, H);
+    rows_cp(L.w2, lay.w2, L.Ap, H, lay.ldh);
+    rows_cp(L.b2, lay.b2, 1, L.Ap, L.Ap);
+    rows_cp(L.brz, lay.gb, 1, 2 * H, 2 * H);
+    rows_cp(L.bih + 2 * H, lay.gb + 2 * H, 1, H, H);
+    rows_cp(L.bhh + 2 * H, lay.gb + 3 * H, 1, H, H);
+    for (int k = tid; k < N * U; k += nthr) smem[lay.pairtab + k] = ((k / U) << 8) | (k % U);
+    for (int k = tid; k < N * A; k += nthr) smem[lay.avtab + k] = ((k / A) << 8) | (k % A);
     __syncthreads();
-    const UnitMasks M = make_unit_masks(SS, U);
-    const float inv_p = 1.0f / (float)pow2_at_least(spec.grid);
+}
 
-    // ---- env lanes: half-wave h of wave w owns env e = 2w + h, lane hl = unit ----
-    const int half = lane >> 5, hl = lane & 31, hbase = half * 32;
-    const int e = wave * 2 + half, b = e0 + e;
-    const bool uvalid = hl < U;
-    UnitLane UL{0, 0, 0, 0u, 0u, 0};
-    int ust = 2, uslot = 0, ulen = 0, zcur = T1;  // zcur: full-write tail zeroed below this step
-    uint32_t uep = 0;
-    float uret = 0.f;
-    if (b < B) {  // reset (parallel_stepper.py:82-104; env_worker_process.py:54-60)
-        uep = st.episode[b];
-        ust = 0;
-        uslot = bt.ring_size > 0 ? (bt.ring_slot0 + b) % bt.ring_size : b;
-        if (uvalid) {
-            const int tm = SS.team[hl];
-            env_spawn_xyh(make_tables(spec, SS), mlg_env_key(spec.seed, b), uep, hl, SS.team_first[tm],
-                          SS.team_size[tm], UL.x, UL.y, UL.hp);
-        }
-        if (hl == 0) {
-            st.episode[b] = uep + 1;
-            bt.filled[(int64_t)uslot * T1] = 1;
-        }
-    }
-    if (hl == 0) {
-        R.status[e] = ust;
-        R.slot[e] = uslot;
-        R.episode[e] = uep;
-    }
-    if (b < B) {
-        v2_pair_pass(M, U, hbase, hl, UL);
-        v2_observe(M, spec, SS, pairtab, avtab, bt, uslot, 0, e, hbase, hl, UL, lobs, ldo, lavail, inv_p);
-    }
+// ---- agent phase pieces (shared by v2 and v4) -----------------------------------------------------
+// The wave's GRU weight rows for feature chunk j (3 gates x 16 features x H, A-operand layout) + biases.
+template <int H>
+struct GruChunk {
+    floatx4 wi[3][H / 16], wh[3][H / 16];
+    floatx4 br, bz, bin, bhn;
+};
 
-    // this wave's GRU weight rows (chunk j, all three gates), A-operand layout, for the whole episode
-    const int j = wave % HC, gi = wave / HC;
-    floatx4 wi[3][HC], wh[3][HC];
+template <int H>
+__device__ inline void load_gru_chunk(GruChunk<H>& W, const float* __restrict__ P, const AgentLayout& L, const float* fm,
+                                      const RolloutLds2& lay, int j, int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4;
 #pragma unroll
     for (int q = 0; q < 3; ++q)
 #pragma unroll
         for (int kc = 0; kc < HC; ++kc) {
             const int64_t r = (int64_t)(q * H + j * 16 + col) * H + kc * 16 + 4 * g;
-            wi[q][kc] = ld4(P + L.wih + r);
-            wh[q][kc] = ld4(P + L.whh + r);
+            W.wi[q][kc] = ld4(P + L.wih + r);
+            W.wh[q][kc] = ld4(P + L.whh + r);
         }
-    const floatx4 br = ld4(fm + lay.gb + j * 16 + 4 * g), bz = ld4(fm + lay.gb + H + j * 16 + 4 * g);
-    const floatx4 bin = ld4(fm + lay.gb + 2 * H + j * 16 + 4 * g), bhn = ld4(fm + lay.gb + 3 * H + j * 16 + 4 * g);
+    W.br = ld4(fm + lay.gb + j * 16 + 4 * g);
+    W.bz = ld4(fm + lay.gb + H + j * 16 + 4 * g);
+    W.bin = ld4(fm + lay.gb + 2 * H + j * 16 + 4 * g);
+    W.bhn = ld4(fm + lay.gb + 3 * H + j * 16 + 4 * g);
+}
+
+// Compacted agent rows of one step: rows_run = (running envs in `run`) * N; row cr -> env ebase + k-th set
+// bit of run, agent n.
+struct StepRows {
+    uint32_t run;
+    int ebase, rows_run, tiles, N;
+    __device__ bool at(int cr, int& e, int& n) const {
+        const bool v = cr < rows_run;
+        const int k = v ? cr / N : 0;
+        n = v ? cr - k * N : 0;
+        e = ebase + nth_set_bit(run, k);
+        return v;
+    }
+};
+
+__device__ inline StepRows make_rows(uint32_t run, int ebase, int N) {
+    StepRows s;
+    s.run = run;
+    s.ebase = ebase;
+    s.N = N;
+    s.rows_run = __builtin_popcount(run) * N;
+    s.tiles = (s.rows_run + 15) / 16;
+    return s;
+}
+
+// A: fc1 + ReLU for (tile, chunk j) over tiles ti0, ti0 + dt, ...  -> x (compact rows)
+template <int H>
+__device__ inline void ph_fc1(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* prev,
+                              const StepRows& SR, int j, int ti0, int dt, int t, int lane) {
+    const int col = lane & 15, g = lane >> 4, N = SR.N, ldo = lay.ldo, ldh = lay.ldh, KO = L.Dob / 16;
+    const float* lobs = fm + lay.obs;
+    for (int ti = ti0; ti < SR.tiles; ti += dt) {
+        int zero = 0;
+        asm volatile("" : "+s"(zero));
+        const int cr = ti * 16 + col;
+        int e, n;
+        const bool valid = SR.at(cr, e, n);
+        const int er = e * N + n;
+        floatx4 acc = ld4(fm + lay.b1 + zero + j * 16 + 4 * g);
+        const int pa = (valid && t > 0) ? prev[er] : -1;
+        if (L.last_action && pa >= 0) acc += ld4(fm + lay.w1a + (int64_t)pa * ldh + j * 16 + 4 * g);
+        if (L.agent_id) acc += ld4(fm + lay.w1n + (int64_t)n * ldh + j * 16 + 4 * g);
+        const float* orow = lobs + (int64_t)er * ldo + 4 * g;
+        const float* wrow = fm + lay.w1o + zero + (int64_t)(j * 16 + col) * ldo + 4 * g;
+        for (int kc = 0; kc < KO; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), ld4(orow + kc * 16), acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.f);
+        *reinterpret_cast<floatx4*>(fm + lay.xb + (int64_t)cr * ldh + j * 16 + 4 * g) = acc;
+    }
+}
+
+// B: GRU cell for (tile, chunk j) -> h' (rows of running envs, hidden state indexed by env row)
+template <int H>
+__device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, float* fm, const float* hc, float* hn,
+                              const StepRows& SR, int j, int ti0, int dt, int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4, N = SR.N, ldh = lay.ldh;
+    for (int ti = ti0; ti < SR.tiles; ti += dt) {
+        const int cr = ti * 16 + col;
+        int e, n;
+        const bool valid = SR.at(cr, e, n);
+        const int er = e * N + n;
+        const float* xr = fm + lay.xb + (int64_t)cr * ldh + 4 * g;
+        const float* hr = hc + (int64_t)er * ldh + 4 * g;
+        floatx4 ar = W.br, az = W.bz, ain = W.bin, ahn = W.bhn;
+#pragma unroll
+        for (int kc = 0; kc < HC; ++kc) {
+            const floatx4 xin = ld4(xr + kc * 16), hin = ld4(hr + kc * 16);
+            ar = mfma_chunk(W.wi[0][kc], xin, ar);
+            az = mfma_chunk(W.wi[1][kc], xin, az);
+            ain = mfma_chunk(W.wi[2][kc], xin, ain);
+            ar = mfma_chunk(W.wh[0][kc], hin, ar);
+            az = mfma_chunk(W.wh[1][kc], hin, az);
+            ahn = mfma_chunk(W.wh[2][kc], hin, ahn);
+        }
+        const floatx4 ho = ld4(hr + j * 16);
+        floatx4 hv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float rg = 1.f / (1.f + expf(-ar[r]));
+            const float zg = 1.f / (1.f + expf(-az[r]));
+            const float ng = tanhf(ain[r] + rg * ahn[r]);
+            hv[r] = ng + zg * (ho[r] - ng);
+        }
+        if (valid) *reinterpret_cast<floatx4*>(hn + (int64_t)er * ldh + j * 16 + 4 * g) = hv;
+    }
+}
+
+// C: fc2 + masked argmax + epsilon-greedy per tile; records the actions (batch + LDS pending actions)
+template <int H>
+__device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, const RolloutLds2& lay, float* fm,
+                              const RoEnv& R, const MlgBatch& bt, const float* hn, const StepRows& SR, int ti0, int dt,
+                              int e0, int t, float eps, int test_mode, int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4, N = SR.N, ldh = lay.ldh, A = spec.n_actions, n_at = L.Ap / 16;
+    const int32_t* lavail = reinterpret_cast<const int32_t*>(fm) + lay.avail;
+    for (int ti = ti0; ti < SR.tiles; ti += dt) {
+        int zero = 0;
+        asm volatile("" : "+s"(zero));
+        const int cr = ti * 16 + col;
+        int e, n;
+        const bool valid = SR.at(cr, e, n);
+        const int er = e * N + n;
+        const float* hr = hn + (int64_t)er * ldh + 4 * g;
+        const int32_t* av = lavail + er * A;
+        ArgmaxState as{-INFINITY, 1 << 30};
+        for (int at = 0; at < n_at; ++at) {
+            floatx4 q = ld4(fm + lay.b2 + zero + at * 16 + 4 * g);
+            const float* w2r = fm + lay.w2 + zero + (int64_t)(at * 16 + col) * ldh + 4 * g;
+#pragma unroll
+            for (int kc = 0; kc < HC; ++kc) q = mfma_chunk(ld4(w2r + kc * 16), ld4(hr + kc * 16), q);
+            argmax_accumulate(as, q, av, at, A, lane);
+        }
+        const int act = argmax_reduce(as);
+        if (valid && g == 0) ro_record_action(spec, R, bt, act, av, e, n, e0 + e, t, eps, test_mode, false);
+    }
+}
+
+// ---- env lanes (half-wave per env; shared by v2 and v4) -------------------------------------------
+struct EnvLane {
+    UnitLane u;
+    int e, b, st, slot, len, zcur, h0, act;
+    uint32_t ep;
+    float ret;
+    bool stepped;
+};
+
+struct EnvCtx {
+    const MlgEnvSpec* spec;
+    const SpecShared* SS;
+    UnitMasks M;
+    RoEnv R;
+    MlgBatch bt;
+    MlgRunInfo info;
+    const int* pairtab;
+    const int* avtab;
+    int* pk;  // [envs][32]
+    float* lobs;
+    int32_t* lavail;
+    int ldo, B;
+    float inv_p;
+};
+
+__device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, EnvLane& E, int e, int e0, int hl) {
+    const MlgEnvSpec& spec = *C.spec;
+    const int hbase = (threadIdx.x & 63) & 32;
+    E.e = e;
+    E.b = e0 + e;
+    E.u = UnitLane{0, 0, 0, 0u, 0u, 0};
+    E.st = 2;
+    E.slot = 0;
+    E.len = 0;
+    E.zcur = C.bt.T1;
+    E.h0 = 0;
+    E.act = 0;
+    E.ep = 0;
+    E.ret = 0.f;
+    E.stepped = false;
+    if (E.b < C.B) {  // reset (parallel_stepper.py:82-104; env_worker_process.py:54-60)
+        E.ep = st.episode[E.b];
+        E.st = 0;
+        E.slot = C.bt.ring_size > 0 ? (C.bt.ring_slot0 + E.b) % C.bt.ring_size : E.b;
+        if (hl < spec.U) {
+            const int tm = C.SS->team[hl];
+            env_spawn_xyh(make_tables(spec, *C.SS), mlg_env_key(spec.seed, E.b), E.ep, hl, C.SS->team_first[tm],
+                          C.SS->team_size[tm], E.u.x, E.u.y, E.u.hp);
+        }
+        if (hl == 0) {
+            st.episode[E.b] = E.ep + 1;
+            C.bt.filled[(int64_t)E.slot * C.bt.T1] = 1;
+        }
+    }
+    if (hl == 0) {
+        C.R.status[e] = E.st;
+        C.R.slot[e] = E.slot;
+        C.R.episode[e] = E.ep;
+    }
+    if (E.b < C.B) {
+        Stamps none;
+        v2_pair_pass(C.M, spec.U, hl, E.u, C.pk + e * 32);
+        v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, 0, e, hbase, hl, E.u, C.lobs, C.ldo, C.lavail,
+                   C.inv_p, none);
+    }
+}
+
+// First half of env step t: record bookkeeping, executed actions (E1), resolution + moves (E2).
+__device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl) {
+    E.stepped = false;
+    if (E.st == 2) return;
+    const MlgEnvSpec& spec = *C.spec;
+    const int N = spec.n_agents, A = spec.n_actions, U = spec.U, T1 = C.bt.T1;
+    const int hbase = (threadIdx.x & 63) & 32;
+    const int* pact = C.R.pact + E.e * N;
+    if (hl < N) C.R.prev[E.e * N + hl] = pact[hl];
+    if (C.bt.full_write) {  // whole one-hot rows of the recorded actions
+        const int64_t oh = ((int64_t)E.slot * T1 + t) * N * A;
+        for (int k = hl; k < N * A; k += 32) {
+            const int pt = C.avtab[k];
+            C.bt.actions_onehot[oh + k] = (pt & 255) == pact[pt >> 8] ? 1.0f : 0.0f;
+        }
+    }
+    if (E.st == 1) {  // final action recorded; env done (parallel_stepper.py:153)
+        E.st = 2;
+        E.zcur = t + 1;
+        if (C.bt.full_write && hl == 0) {
+            C.bt.reward[(int64_t)E.slot * T1 + t] = 0.f;
+            C.bt.terminated[(int64_t)E.slot * T1 + t] = 0;
+        }
+        if (hl == 0) C.R.status[E.e] = E.st;
+        return;
+    }
+    // E1: executed action -- validated policy action or the scripted AI choice (spec §3.4)
+    const bool uvalid = hl < U;
+    int act = 0;
+    if (uvalid) {
+        const int ag = C.SS->agent[hl];
+        if (ag) {
+            const int a = pact[ag - 1];
+            act = (a >= 0 && a < MLG_ACT_BASE + U && v2_avail(C.M, spec.grid, E.u.x, E.u.y, E.u.hp, E.u.tgt, a)) ? a : 0;
+        } else {
+            act = E.u.ai;
+        }
+    }
+    // E2: simultaneous resolution on the pre-step state, then moves (spec §3.4)
+    const int pk = pk_unit(E.u.x, E.u.y, E.u.hp);
+    int dmg = 0, heal = 0;
+    for (int i = 0; i < U; ++i) {
+        const int qi = __shfl(pk, hbase + i, 64), ai = __shfl(act, hbase + i, 64);
+        const bool hit = pk_hp(qi) > 0 && ai == MLG_ACT_BASE + hl;
+        const int ri = mask_role(C.M, i);
+        heal += (hit && ri == 1) ? role_power(1) : 0;
+        dmg += (hit && ri != 1) ? role_power(ri) : 0;
+    }
+    E.h0 = E.u.hp;
+    if (uvalid && E.h0 > 0) {
+        const int v = E.h0 - dmg + heal, mx = role_maxhp(mask_role(C.M, hl));
+        E.u.hp = v < 0 ? 0 : (v > mx ? mx : v);
+        E.u.x += (act == 3) - (act == 4);  // env_apply_move on registers
+        E.u.y += (act == 1) - (act == 2);
+    }
+    E.act = act;
+    E.stepped = true;
+}
+
+// Second half of env step t (envs that stepped): per-env reduction (E3), reward / termination, the
+// observation of t + 1.
+__device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl, Stamps& sp) {
+    if (!E.stepped) return;
+    const MlgEnvSpec& spec = *C.spec;
+    const int U = spec.U, T1 = C.bt.T1;
+    const int hbase = (threadIdx.x & 63) & 32;
+    const bool uvalid = hl < U;
+    const int h0 = E.h0, h1 = E.u.hp;
+    const int my_team = (C.M.team1 >> hl) & 1;
+    const uint32_t alive_m = (uint32_t)(__ballot(uvalid && h1 > 0) >> hbase);
+    const uint32_t kill_m = (uint32_t)(__ballot(uvalid && h0 > 0 && h1 == 0) >> hbase);
+    int lostv = (uvalid && h0 > 0 && h0 > h1) ? (h0 - h1) << (16 * my_team) : 0;
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) lostv += __shfl_xor(lostv, m, 64);
+    const int alive0 = __builtin_popcount(alive_m & ~C.M.team1), alive1 = __builtin_popcount(alive_m & C.M.team1);
+    const int kills0 = __builtin_popcount(kill_m & C.M.team1), kills1 = __builtin_popcount(kill_m & ~C.M.team1);
+    const int lost0 = lostv & 0xFFFF, lost1 = lostv >> 16;
+    const int done = alive0 == 0 || alive1 == 0 || t + 1 >= spec.episode_limit;
+    const int won0 = alive1 == 0 && alive0 > 0, won1 = alive0 == 0 && alive1 > 0;
+    const int pt = spec.policy_team;
+    const int wpt = pt ? won1 : won0, wop = pt ? won0 : won1;
+    const int r_int = (pt ? lost0 : lost1) + 10 * (pt ? kills1 : kills0) + 200 * wpt;
+    const float r = (float)r_int * 0.0625f;
+    E.ret += r;
+    if (hl == 0) {
+        const int64_t sl = (int64_t)E.slot * T1 + t;
+        C.bt.reward[sl] = r;
+        C.bt.terminated[sl] = (uint8_t)done;
+        C.bt.filled[sl + 1] = 1;
+        if (done) {
+            C.info.won[2 * E.b] = wpt;
+            C.info.won[2 * E.b + 1] = wop;
+            C.info.draw[E.b] = !won0 && !won1;
+        }
+    }
+    if (done) {
+        E.st = 1;
+        E.len = t + 1;
+    }
+    if (hl == 0) C.R.status[E.e] = E.st;
+    sp.mark(6);
+    // observation at t + 1 (incl. envs that just terminated)
+    v2_pair_pass(C.M, U, hl, E.u, C.pk + E.e * 32);
+    sp.mark(7);
+    v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavail,
+               C.inv_p, sp);
+}
+
+// Full-write mode: a finished env's half-wave zeroes a few more steps of its slot's tail.
+__device__ inline void env_lane_tail(const EnvCtx& C, EnvLane& E, int steps, int hl) {
+    if (!C.bt.full_write || E.st != 2 || E.zcur >= C.bt.T1 || E.b >= C.B) return;
+    const MlgEnvSpec& spec = *C.spec;
+    const int z1 = E.zcur + steps < C.bt.T1 ? E.zcur + steps : C.bt.T1;
+    zero_slot_steps(C.bt, E.slot, E.zcur, z1, spec.n_agents, spec.n_actions, 6 * spec.U, 8 * spec.U, hl, 32);
+    E.zcur = z1;
+}
+
+// Per-env summary + env state write-back (+ the rest of the tail in full-write mode).
+__device__ inline void env_lane_finish(const EnvCtx& C, const MlgEnvState& st, EnvLane& E, int hl) {
+    if (E.b >= C.B) return;
+    const int U = C.spec->U;
+    if (C.bt.full_write) env_lane_tail(C, E, C.bt.T1, hl);
+    if (hl == 0) {
+        C.info.ep_len[E.b] = E.len;
+        C.info.ret[E.b] = E.ret;
+        st.t[E.b] = E.len;
+    }
+    if (hl < U) {
+        st.x[(int64_t)E.b * U + hl] = E.u.x;
+        st.y[(int64_t)E.b * U + hl] = E.u.y;
+        st.hp[(int64_t)E.b * U + hl] = E.u.hp;
+    }
+}
+
+__device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2& lay, int* smem, const MlgBatch& bt,
+                                      const MlgRunInfo& info) {
+    EnvCtx C;
+    float* fm = reinterpret_cast<float*>(smem);
+    C.spec = &spec;
+    C.SS = reinterpret_cast<const SpecShared*>(smem + lay.env.spec);
+    C.M = make_unit_masks(*C.SS, spec.U);
+    C.R = env_view(smem, lay.env);
+    C.bt = bt;
+    C.info = info;
+    C.pairtab = smem + lay.pairtab;
+    C.avtab = smem + lay.avtab;
+    C.pk = smem + lay.pk;
+    C.lobs = fm + lay.obs;
+    C.lavail = smem + lay.avail;
+    C.ldo = lay.ldo;
+    C.B = bt.B;
+    C.inv_p = 1.0f / (float)pow2_at_least(spec.grid);
+    return C;
+}
+
+// ================================================================================================
+// v2 kernel: 8 waves, 16 envs; every wave does agent work (chunk j = w % HC of tiles w / HC, ...) and then
+// the env step of envs 2w, 2w + 1. Barriers per step: A|B, B|C, C|env, env|A.
+template <int H>
+__global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
+                                                           const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
+                                                           float eps, int test_mode, RolloutLds2 lay) {
+    constexpr int HC = H / 16, NW = 8, REW = 16, G = NW / HC;
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    float* fm = reinterpret_cast<float*>(smem);
+    const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
+    const int e0 = blockIdx.x * REW, T1 = bt.T1;
+    v2_prologue(spec, L, P, lay, smem, REW * N);
+    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info);
+    EnvLane E;
+    env_lane_reset(C, st, E, wave * 2 + (lane >> 5), e0, hl);
+    const int j = wave % HC, gi = wave / HC;
+    GruChunk<H> W;
+    load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
     __syncthreads();
     Stamps sp;
     sp.init();
-    const int n_at = L.Ap / 16, KO = L.Dob / 16;
     for (int t = 0; t < T1; ++t) {
-        // running envs (status < 2), uniform over the workgroup
-        const uint32_t run = (uint32_t)__ballot(lane < RE && R.status[lane & (RE - 1)] < 2);
+        const uint32_t run = (uint32_t)__ballot(lane < REW && C.R.status[lane & (REW - 1)] < 2);
         if (run == 0) break;
-        const int rows_run = __builtin_popcount(run) * N;
-        const int tiles = (rows_run + 15) / 16;
+        const StepRows SR = make_rows(run, 0, N);
         const float* hc = fm + lay.hb + (t & 1) * lay.hsz;
         float* hn = fm + lay.hb + ((t & 1) ^ 1) * lay.hsz;
-        auto row_of = [&](int cr, int& ee, int& nn) {
-            const bool v = cr < rows_run;
-            const int k = v ? cr / N : 0;
-            nn = v ? cr - k * N : 0;
-            ee = nth_set_bit(run, k);
-            return v;
-        };
-        // ---- A: fc1 + ReLU for (tile, chunk j) ----
-        for (int ti = gi; ti < tiles; ti += G) {
-            int zero = 0;
-            asm volatile("" : "+s"(zero));
-            const int cr = ti * 16 + col;
-            int ee, n;
-            const bool valid = row_of(cr, ee, n);
-            const int er = ee * N + n;
-            floatx4 acc = ld4(fm + lay.b1 + zero + j * 16 + 4 * g);
-            const int pa = (valid && t > 0) ? R.prev[er] : -1;
-            if (L.last_action && pa >= 0) acc += ld4(fm + lay.w1a + (int64_t)pa * ldh + j * 16 + 4 * g);
-            if (L.agent_id) acc += ld4(fm + lay.w1n + (int64_t)n * ldh + j * 16 + 4 * g);
-            const float* wrow = fm + lay.w1o + zero + (int64_t)(j * 16 + col) * ldo + 4 * g;
-            const float* orow = lobs + (int64_t)er * ldo + 4 * g;
-            for (int kc = 0; kc < KO; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), ld4(orow + kc * 16), acc);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.f);
-            *reinterpret_cast<floatx4*>(fm + lay.xb + (int64_t)cr * ldh + j * 16 + 4 * g) = acc;
-        }
+        ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
         sp.mark(0);
         __syncthreads();
-        // ---- B: GRU cell for (tile, chunk j) -> h' rows of running envs ----
-        for (int ti = gi; ti < tiles; ti += G) {
-            const int cr = ti * 16 + col;
-            int ee, n;
-            const bool valid = row_of(cr, ee, n);
-            const int er = ee * N + n;
-            const float* xr = fm + lay.xb + (int64_t)cr * ldh + 4 * g;
-            const float* hr = hc + (int64_t)er * ldh + 4 * g;
-            floatx4 ar = br, az = bz, ain = bin, ahn = bhn;
-#pragma unroll
-            for (int kc = 0; kc < HC; ++kc) {
-                const floatx4 xin = ld4(xr + kc * 16), hin = ld4(hr + kc * 16);
-                ar = mfma_chunk(wi[0][kc], xin, ar);
-                az = mfma_chunk(wi[1][kc], xin, az);
-                ain = mfma_chunk(wi[2][kc], xin, ain);
-                ar = mfma_chunk(wh[0][kc], hin, ar);
-                az = mfma_chunk(wh[1][kc], hin, az);
-                ahn = mfma_chunk(wh[2][kc], hin, ahn);
-            }
-            const floatx4 ho = ld4(hr + j * 16);
-            floatx4 hv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float rg = 1.f / (1.f + expf(-ar[r]));
-                const float zg = 1.f / (1.f + expf(-az[r]));
-                const float ng = tanhf(ain[r] + rg * ahn[r]);
-                hv[r] = ng + zg * (ho[r] - ng);
-            }
-            if (valid) *reinterpret_cast<floatx4*>(hn + (int64_t)er * ldh + j * 16 + 4 * g) = hv;
-        }
+        ph_gru<H>(W, lay, fm, hc, hn, SR, j, gi, G, lane);
         sp.mark(1);
         __syncthreads();
-        // ---- C: fc2 + masked argmax + epsilon-greedy per tile ----
-        for (int ti = wave; ti < tiles; ti += NW) {
-            int zero = 0;
-            asm volatile("" : "+s"(zero));
-            const int cr = ti * 16 + col;
-            int ee, n;
-            const bool valid = row_of(cr, ee, n);
-            const int er = ee * N + n;
-            const float* hr = hn + (int64_t)er * ldh + 4 * g;
-            const int32_t* av = lavail + er * A;
-            ArgmaxState as{-INFINITY, 1 << 30};
-            for (int at = 0; at < n_at; ++at) {
-                floatx4 q = ld4(fm + lay.b2 + zero + at * 16 + 4 * g);
-                const float* w2r = fm + lay.w2 + zero + (int64_t)(at * 16 + col) * ldh + 4 * g;
-#pragma unroll
-                for (int kc = 0; kc < HC; ++kc) q = mfma_chunk(ld4(w2r + kc * 16), ld4(hr + kc * 16), q);
-                argmax_accumulate(as, q, av, at, A, lane);
-            }
-            const int act = argmax_reduce(as);
-            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, ee, n, e0 + ee, t, eps, test_mode, false);
-        }
+        ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
         sp.mark(2);
         __syncthreads();
         sp.mark(3);
-        // ---- env phase: half-wave per env (env_worker_process.py:32-53 batched) ----
-        if (ust != 2) {
-            if (hl < N) R.prev[e * N + hl] = R.pact[e * N + hl];
-            if (bt.full_write) {  // whole one-hot rows of the recorded actions
-                const int64_t oh = ((int64_t)uslot * T1 + t) * N * A;
-                for (int k = hl; k < N * A; k += 32) {
-                    const int pt = avtab[k];
-                    bt.actions_onehot[oh + k] = (pt & 255) == R.pact[e * N + (pt >> 8)] ? 1.0f : 0.0f;
-                }
-            }
-            if (ust == 1) {  // final action recorded; env done (parallel_stepper.py:153)
-                ust = 2;
-                zcur = t + 1;
-                if (bt.full_write && hl == 0) {
-                    bt.reward[(int64_t)uslot * T1 + t] = 0.f;
-                    bt.terminated[(int64_t)uslot * T1 + t] = 0;
-                }
-            } else {
-                // E1: executed action -- validated policy action or the scripted AI choice (spec §3.4)
-                int act = 0;
-                if (uvalid) {
-                    const int ag = SS.agent[hl];
-                    if (ag) {
-                        const int a = R.pact[e * N + ag - 1];
-                        act = (a >= 0 && a < MLG_ACT_BASE + U && v2_avail(M, spec.grid, UL.x, UL.y, UL.hp, UL.tgt, a)) ? a : 0;
-                    } else {
-                        act = UL.ai;
-                    }
-                }
-                sp.mark(4);
-                // E2: simultaneous resolution on the pre-step state, then moves (spec §3.4)
-                const int pk = pk_unit(UL.x, UL.y, UL.hp);
-                int dmg = 0, heal = 0;
-                for (int i = 0; i < U; ++i) {
-                    const int qi = __shfl(pk, hbase + i, 64), ai = __shfl(act, hbase + i, 64);
-                    const bool hit = pk_hp(qi) > 0 && ai == MLG_ACT_BASE + hl;
-                    const int ri = mask_role(M, i);
-                    heal += (hit && ri == 1) ? role_power(1) : 0;
-                    dmg += (hit && ri != 1) ? role_power(ri) : 0;
-                }
-                const int h0 = UL.hp;
-                int h1 = h0;
-                if (uvalid && h0 > 0) {
-                    const int v = h0 - dmg + heal, mx = role_maxhp(mask_role(M, hl));
-                    h1 = v < 0 ? 0 : (v > mx ? mx : v);
-                    UL.x += (act == 3) - (act == 4);  // env_apply_move on registers
-                    UL.y += (act == 1) - (act == 2);
-                }
-                UL.hp = h1;
-                sp.mark(5);
-                // E3: per-env reduction over the half-wave (ballots + one packed shuffle sum)
-                const int my_team = (M.team1 >> hl) & 1;
-                const uint32_t alive_m = (uint32_t)(__ballot(uvalid && h1 > 0) >> hbase);
-                const uint32_t kill_m = (uint32_t)(__ballot(uvalid && h0 > 0 && h1 == 0) >> hbase);
-                int lostv = (uvalid && h0 > 0 && h0 > h1) ? (h0 - h1) << (16 * my_team) : 0;
-#pragma unroll
-                for (int m = 16; m >= 1; m >>= 1) lostv += __shfl_xor(lostv, m, 64);
-                const int alive0 = __builtin_popcount(alive_m & ~M.team1), alive1 = __builtin_popcount(alive_m & M.team1);
-                const int kills0 = __builtin_popcount(kill_m & M.team1), kills1 = __builtin_popcount(kill_m & ~M.team1);
-                const int lost0 = lostv & 0xFFFF, lost1 = lostv >> 16;
-                const int done = alive0 == 0 || alive1 == 0 || t + 1 >= spec.episode_limit;
-                const int won0 = alive1 == 0 && alive0 > 0, won1 = alive0 == 0 && alive1 > 0;
-                const int pt = spec.policy_team;
-                const int wpt = pt ? won1 : won0, wop = pt ? won0 : won1;
-                const int r_int = (pt ? lost0 : lost1) + 10 * (pt ? kills1 : kills0) + 200 * wpt;
-                const float r = (float)r_int * 0.0625f;
-                uret += r;
-                if (hl == 0) {
-                    const int64_t sl = (int64_t)uslot * T1 + t;
-                    bt.reward[sl] = r;
-                    bt.terminated[sl] = (uint8_t)done;
-                    bt.filled[sl + 1] = 1;
-                    if (done) {
-                        info.won[2 * b] = wpt;
-                        info.won[2 * b + 1] = wop;
-                        info.draw[b] = !won0 && !won1;
-                    }
-                }
-                if (done) {
-                    ust = 1;
-                    ulen = t + 1;
-                }
-                sp.mark(6);
-                // observation at t + 1 (incl. envs that just terminated)
-                v2_pair_pass(M, U, hbase, hl, UL);
-                v2_observe(M, spec, SS, pairtab, avtab, bt, uslot, t + 1, e, hbase, hl, UL, lobs, ldo, lavail, inv_p);
-                sp.mark(7);
-            }
-            if (hl == 0) R.status[e] = ust;
-        } else if (bt.full_write && zcur < T1 && b < B) {  // idle half-wave: zero a few tail steps
-            const int z1 = zcur + 4 < T1 ? zcur + 4 : T1;
-            zero_slot_steps(bt, uslot, zcur, z1, N, A, 6 * U, 8 * U, hl, 32);
-            zcur = z1;
-        }
+        env_lane_step1(C, E, t, hl);
+        sp.mark(4);
+        env_lane_step2(C, E, t, hl, sp);
+        if (!E.stepped && (t & 1)) env_lane_tail(C, E, 8, hl);
         sp.mark(8);
         __syncthreads();
         sp.mark(10);
     }
     sp.flush();
-    // ---- per-env summary + env state write-back (+ the rest of the tail in full-write mode) ----
-    if (b < B) {
-        if (bt.full_write) zero_slot_steps(bt, uslot, zcur, T1, N, A, 6 * U, 8 * U, hl, 32);
-        if (hl == 0) {
-            info.ep_len[b] = ulen;
-            info.ret[b] = uret;
-            st.t[b] = ulen;
+    env_lane_finish(C, st, E, hl);
+}
+
+// ================================================================================================
+// v4 kernel: wave-specialised, two env groups in flight. Waves 0-3 are agent waves (wave w owns GRU chunk
+// w % HC with its weights in VGPRs), waves 4-7 are env waves (half-wave per env: envs 0-7 form group 0,
+// 8-15 group 1; env wave v steps envs 2v, 2v + 1 of both groups). Phase p runs the agent step of group
+// X = p % 2 while the env waves run the env step of the other group, so the matrix cores work while the
+// envs step. Three barriers per phase (A|B, B|C, end); the env step is split to fit the agent segments:
+//   segment 1: agent A (fc1)        || env bookkeeping, executed actions, resolution
+//   segment 2: agent B (GRU)        || env reduction, reward, pair pass, observation
+//   segment 3: agent C (fc2+select) || tail zeroing (full-write mode)
+// Identical arithmetic to v1/v2 per env (bit-identical batches).
+template <int H>
+__global__ void __launch_bounds__(512, 2) rollout_v4_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
+                                                           const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
+                                                           float eps, int test_mode, RolloutLds2 lay) {
+    constexpr int HC = H / 16, AW = 4, REW = 16, G = AW / HC;
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    float* fm = reinterpret_cast<float*>(smem);
+    const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
+    const int e0 = blockIdx.x * REW, T1 = bt.T1;
+    v2_prologue(spec, L, P, lay, smem, REW * N);
+    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info);
+    // The two roles run separate copies of the phase loop (same uniform control state, same barrier count),
+    // so the agent waves' weight registers and the env waves' unit registers are allocated over each other.
+    // Phase state: tg[g] = next agent step of group g, pend[g] = env step tg[g] - 1 still to run.
+    struct PhaseState {  // scalar fields (no dynamically indexed local arrays)
+        int tg0, tg1;
+        bool pend0, pend1;
+        __device__ int tg(int x) const { return x ? tg1 : tg0; }
+        __device__ bool pend(int x) const { return x ? pend1 : pend0; }
+    };
+    auto phase_begin = [&](const PhaseState& ps, int p, uint32_t& runX, bool& done) {
+        const int X = p & 1;
+        const int sv = C.R.status[lane & 15];
+        const uint32_t run16 = (uint32_t)__ballot(lane < 16 && sv < 2);
+        runX = (run16 >> (8 * X)) & 0xFFu;
+        done = run16 == 0 && !ps.pend0 && !ps.pend1;
+    };
+    auto phase_end = [&](PhaseState& ps, int p, bool doAgent) {
+        const int X = p & 1;
+        if (X) {
+            ps.pend0 = false;
+            if (doAgent) { ps.pend1 = true; ps.tg1 += 1; }
+        } else {
+            ps.pend1 = false;
+            if (doAgent) { ps.pend0 = true; ps.tg0 += 1; }
         }
-        if (uvalid) {
-            st.x[(int64_t)b * U + hl] = UL.x;
-            st.y[(int64_t)b * U + hl] = UL.y;
-            st.hp[(int64_t)b * U + hl] = UL.hp;
+    };
+    Stamps sp;
+    if (wave < AW) {
+        const int j = wave % HC, gi = wave / HC;
+        GruChunk<H> W;
+        load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
+        __syncthreads();
+        sp.init();
+        PhaseState ps{0, 0, false, false};
+        for (int p = 0;; ++p) {
+            uint32_t runX;
+            bool done;
+            phase_begin(ps, p, runX, done);
+            if (done) break;
+            const int X = p & 1, tX = ps.tg(X);
+            const bool doAgent = runX != 0 && tX < T1;
+            const StepRows SR = make_rows(runX, 8 * X, N);
+            const float* hc = fm + lay.hb + (tX & 1) * lay.hsz;
+            float* hn = fm + lay.hb + ((tX & 1) ^ 1) * lay.hsz;
+            if (doAgent) ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, tX, lane);
+            sp.mark(0);
+            __syncthreads();
+            if (doAgent) ph_gru<H>(W, lay, fm, hc, hn, SR, j, gi, G, lane);
+            sp.mark(1);
+            __syncthreads();
+            if (doAgent) ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, AW, e0, tX, eps, test_mode, lane);
+            sp.mark(2);
+            __syncthreads();
+            sp.mark(10);
+            phase_end(ps, p, doAgent);
         }
+        sp.flush();
+    } else {
+        EnvLane E0, E1;  // this half-wave's env of group 0 and of group 1
+        const int v = wave - AW, h = lane >> 5;
+        env_lane_reset(C, st, E0, 2 * v + h, e0, hl);
+        env_lane_reset(C, st, E1, 8 + 2 * v + h, e0, hl);
+        __syncthreads();
+        sp.init();
+        PhaseState ps{0, 0, false, false};
+        for (int p = 0;; ++p) {
+            uint32_t runX;
+            bool done;
+            phase_begin(ps, p, runX, done);
+            if (done) break;
+            const int X = p & 1, Y = X ^ 1;
+            const bool doAgent = runX != 0 && ps.tg(X) < T1;
+            const bool pendY = ps.pend(Y);
+            const int tY = ps.tg(Y) - 1;
+            EnvLane& EY = Y ? E1 : E0;
+            if (pendY) env_lane_step1(C, EY, tY, hl);
+            sp.mark(4);
+            __syncthreads();
+            if (pendY) env_lane_step2(C, EY, tY, hl, sp);
+            sp.mark(5);
+            __syncthreads();
+            env_lane_tail(C, EY, 8, hl);
+            sp.mark(8);
+            __syncthreads();
+            sp.mark(10);
+            phase_end(ps, p, doAgent);
+        }
+        sp.flush();
+        env_lane_finish(C, st, E0, hl);
+        env_lane_finish(C, st, E1, hl);
     }
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // Standalone env kernels (one thread per env) -- the EnvWorker command set for host-side TeamsEnv use
@@ -1174,29 +1451,30 @@ int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec,
     return launch_rollout_t<H, TPW, false>(grid, threads, s, spec, st, L, P, bt, info, eps, tm, lay);
 }
 
-template <int H>
-int launch_rollout_v2(int grid, hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
+template <int H, bool V4>
+int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
                       const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
                       const RolloutLds2& lay) {
     const size_t bytes = (size_t)lay.total * 4;
-    auto kern = rollout_v2_kernel<H>;
+    auto kern = V4 ? rollout_v4_kernel<H> : rollout_v2_kernel<H>;
     if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)bytes);
         if (e != hipSuccess) return mlg::fail("rollout v2: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
+    hipLaunchKernelGGL(kern, dim3((bt.B + 15) / 16), dim3(512), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
     return 0;
 }
 
-// v2 when the shape allows it (H 32/64, LDS fits) unless MLG_ROLLOUT_KERNEL=v1.
-bool use_rollout_v2(const AgentLayout& L, const MlgEnvSpec& spec, const MlgBatch& bt, RolloutLds2* lay) {
+// v4 (wave-specialised) / v2 when the shape allows it (H 32/64, U <= 32, LDS fits), else v1.
+// MLG_ROLLOUT_KERNEL=v1|v2|v4 forces a variant.
+int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay) {
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
-    if (k && k[0] == 'v' && k[1] == '1') return false;
-    if (L.H != 64 && L.H != 32) return false;
-    if (spec.U > 32) return false;
-    *lay = make_rollout_lds2(L, spec.U, spec.n_agents);
-    return lay->total * 4 <= LDS_LIMIT_BYTES;
+    const int want = (k && k[0] == 'v') ? k[1] - '0' : 4;
+    if (want == 1 || (L.H != 64 && L.H != 32) || spec.U > 32) return 1;
+    *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
+    if (lay->total * 4 > LDS_LIMIT_BYTES) return 1;
+    return want == 2 ? 2 : 4;
 }
 
 }  // namespace
@@ -1322,9 +1600,15 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
     const float eps = test_mode ? 0.f : epsilon;
     int rc = 0;
     RolloutLds2 lay2;
-    if (use_rollout_v2(L, *spec, *batch, &lay2)) {
-        rc = dims->hidden == 64 ? launch_rollout_v2<64>(grid, s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
-                                : launch_rollout_v2<32>(grid, s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
+    const int variant = pick_rollout(L, *spec, &lay2);
+    if (variant > 1) {
+        const bool h64 = dims->hidden == 64;
+        if (variant == 4)
+            rc = h64 ? launch_rollout_v2<64, true>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
+                     : launch_rollout_v2<32, true>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
+        else
+            rc = h64 ? launch_rollout_v2<64, false>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
+                     : launch_rollout_v2<32, false>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
         if (rc) return rc;
         return mlg::check_launch("rollout_v2_kernel");
     }

@@ -28,18 +28,34 @@ for it in range(3):
 torch.cuda.synchronize()
 a = buf.view(grid, 8, 16).cpu().numpy().astype(np.float64)
 valid = a[:, :, 15] == 1
-if os.environ.get("MLG_ROLLOUT_KERNEL", "v2") == "v1":
+if os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v1":
     names = ["agent", "barrier_after_agent", "-", "-"]
     names += ["E1_exec_actions", "E2_resolve(+bar)", "E3_reduce(+bar)", "obs(+bar)", "state", "avail",
               "zero+list+barrier"]
 else:
     names = ["A_fc1", "B_gru(+barrier A)", "C_fc2_select(+barrier B)", "barrier_after_C", "E1_exec", "E2_resolve",
-             "E3_reduce", "pairs+obs/state/avail", "status", "-", "barrier_end"]
+             "E3_reduce", "pair_pass", "status/tail-zero", "obs", "barrier_end", "avail", "state"]
+if os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v4":
+    for role, ws in (("agent waves 0-3", slice(0, 4)), ("env waves 4-7", slice(4, 8))):
+        sub = a[:, ws, :]
+        vv = sub[:, :, 15] == 1
+        tt = sub[:, :, 14][vv].mean()
+        print(f"-- {role}: mean total {tt:.0f}")
+        for k in range(14):
+            m = sub[:, :, k][vv].mean()
+            if m > 0:
+                print(f"   slot {k:2d} mean={m:12.0f} share={m / tt * 100:6.1f}%")
 tot = a[:, :, 14][valid].mean()
 print(f"rollout waves={valid.sum()} mean total cycles/wave={tot:.0f} (~{tot / 2.1e3:.1f} us at 2.1GHz)")
 for k, n in enumerate(names):
     v = a[:, :, k][valid]
     print(f"{n:22s} mean={v.mean():12.0f} share={v.mean() / tot * 100:6.1f}%  max={v.max():.0f}")
+tw = a[:, 0, 14][valid[:, 0]]
+print("per-WG total cycles: min %.0f p10 %.0f p50 %.0f p90 %.0f max %.0f" % tuple(np.percentile(tw, [0, 10, 50, 90, 100])))
 lens = st.last_run["ep_len"].numpy()
+wmax = np.array([lens[i:i + 16].max() + 1 for i in range(0, B, 16)])
+print("per-WG iterations: min %d p10 %d p50 %d p90 %d max %d" % tuple(np.percentile(wmax, [0, 10, 50, 90, 100]).astype(int)))
+print("active env-steps per WG (sum len): p50 %d max %d" % (np.median([lens[i:i+16].sum() for i in range(0, B, 16)]),
+      max(lens[i:i+16].sum() for i in range(0, B, 16))))
 print("episode len mean", lens.mean(), "max", lens.max(), "iterations per WG (mean of max)",
       np.mean([lens[i:i + 16].max() + 1 for i in range(0, B, 16)]))

@@ -282,7 +282,7 @@ def test_rollout_headline_config_properties(device):
             np.testing.assert_array_equal(nb["obs"][b, t + 1], r.obs())
 
 
-@pytest.mark.parametrize("kernel", ["v2", "v1"])
+@pytest.mark.parametrize("kernel", ["v4", "v2", "v1"])
 def test_rollout_ring_mode_zero_copy_insert(device, kernel, monkeypatch):
     """Train-mode rollouts written straight into the replay ring (full-write mode, wrap-around, garbage in the
     slots beforehand) equal the ordinary zero-initialised EpisodeBatch bit for bit, and the buffer indices
@@ -320,14 +320,15 @@ def test_rollout_ring_mode_zero_copy_insert(device, kernel, monkeypatch):
         assert torch.equal(ring[k][:n], ref[k][:n]), k
 
 
+@pytest.mark.parametrize("kernel", ["v2", "v4"])
 @pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium_1h_2t_2a", "medium"])
-def test_rollout_v2_equals_v1(device, plan, monkeypatch):
+def test_rollout_v2_equals_v1(device, plan, kernel, monkeypatch):
     """The chunk-split, compacted headline kernel (v2) and the generic per-tile kernel (v1) compute in the same
     arithmetic order: the whole batch and the run summary must be bit-identical."""
     from maleague.envs.teams_env import VecEnvState
     stepper, mac, args = _build_stepper(device, plan=plan, B=100, episode_limit=60, seed=3)
     out = {}
-    for k in ("v1", "v2"):
+    for k in ("v1", kernel):
         monkeypatch.setenv("MLG_ROLLOUT_KERNEL", k)
         stepper.envs = VecEnvState(stepper.spec, 100, device)
         stepper.t_env = 30000
@@ -335,6 +336,6 @@ def test_rollout_v2_equals_v1(device, plan, monkeypatch):
         out[k] = ({kk: b[kk].clone() for kk in b.data.transition_data},
                   {kk: v.clone() for kk, v in stepper.last_run.items() if torch.is_tensor(v)})
     for kk, v in out["v1"][0].items():
-        assert torch.equal(v, out["v2"][0][kk]), kk
+        assert torch.equal(v, out[kernel][0][kk]), kk
     for kk, v in out["v1"][1].items():
-        assert torch.equal(v, out["v2"][1][kk]), kk
+        assert torch.equal(v, out[kernel][1][kk]), kk
