@@ -1466,15 +1466,15 @@ int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& 
     return 0;
 }
 
-// v4 (wave-specialised) / v2 when the shape allows it (H 32/64, U <= 32, LDS fits), else v1.
-// MLG_ROLLOUT_KERNEL=v1|v2|v4 forces a variant.
+// v2 when the shape allows it (H 32/64, U <= 32, LDS fits), else v1. MLG_ROLLOUT_KERNEL=v1|v2|v4 forces a
+// variant (v4: the wave-specialised experiment, slower than v2 on the headline shape so far).
 int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay) {
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
-    const int want = (k && k[0] == 'v') ? k[1] - '0' : 4;
+    const int want = (k && k[0] == 'v') ? k[1] - '0' : 2;
     if (want == 1 || (L.H != 64 && L.H != 32) || spec.U > 32) return 1;
     *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
     if (lay->total * 4 > LDS_LIMIT_BYTES) return 1;
-    return want == 2 ? 2 : 4;
+    return want == 4 ? 4 : 2;
 }
 
 }  // namespace
