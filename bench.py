@@ -42,7 +42,8 @@ def main():
     ap.add_argument("--plan", default="medium_1h_4t")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per rollout launch (profiles/)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per rollout launch (scripts/gpu_traffic.sh -> profiles/)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,6 +67,9 @@ def main():
                  "runner_log_interval=1000000000", "test_interval=1000000000000", "t_max=1000000000000",
                  "show_exp_parameters=False"]
     cfg = build_config("qmix", "ma", overrides=overrides, device_index=local_rank)
+    import numpy as np
+    np.random.seed(rank)  # replay sampling (reproducible learning curve -> reproducible episode lengths)
+    torch.manual_seed(rank)
     exp = MultiAgentExperiment(to_args(cfg), MainLogger(log_interval=10 ** 12))
     exp._init_stepper()
     stepper, learner = exp.stepper, exp.home_learner
@@ -139,7 +143,7 @@ def main():
                "env_steps": env_steps, "mean_episode_len": env_steps / max(1, a.steps * B * world),
                "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12,
                             "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic,
-                            "kernel": "rollout_kernel<64,1>", "avg_kernel_ms": avg_kernel_s * 1e3,
+                            "kernel": "rollout_v2_kernel<64>", "avg_kernel_ms": avg_kernel_s * 1e3,
                             "flops_per_launch": fl * forwards},
                "cpu_baseline": cpu}
         print(json.dumps(out))

@@ -1197,8 +1197,8 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
 }
 
 // ================================================================================================
-// v4 kernel: wave-specialised, two env groups in flight. Waves 0-3 are agent waves (wave w owns GRU chunk
-// w % HC with its weights in VGPRs), waves 4-7 are env waves (half-wave per env: envs 0-7 form group 0,
+// v4 kernel: wave-specialised, two env groups in flight. Waves 0..AW-1 are agent waves (wave w owns GRU chunk
+// w % HC of tiles w / HC, w / HC + AW / HC, ... with its weights in VGPRs), the last 4 waves are env waves (half-wave per env: envs 0-7 form group 0,
 // 8-15 group 1; env wave v steps envs 2v, 2v + 1 of both groups). Phase p runs the agent step of group
 // X = p % 2 while the env waves run the env step of the other group, so the matrix cores work while the
 // envs step. Three barriers per phase (A|B, B|C, end); the env step is split to fit the agent segments:
@@ -1206,11 +1206,11 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
 //   segment 2: agent B (GRU)        || env reduction, reward, pair pass, observation
 //   segment 3: agent C (fc2+select) || tail zeroing (full-write mode)
 // Identical arithmetic to v1/v2 per env (bit-identical batches).
-template <int H>
-__global__ void __launch_bounds__(512, 2) rollout_v4_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
-                                                           const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
-                                                           float eps, int test_mode, RolloutLds2 lay) {
-    constexpr int HC = H / 16, AW = 4, REW = 16, G = AW / HC;
+template <int H, int AW>
+__global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel(
+    MlgEnvSpec spec, MlgEnvState st, AgentLayout L, const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
+    float eps, int test_mode, RolloutLds2 lay) {
+    constexpr int HC = H / 16, REW = 16, G = AW / HC;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     float* fm = reinterpret_cast<float*>(smem);
     const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
@@ -1451,30 +1451,31 @@ int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec,
     return launch_rollout_t<H, TPW, false>(grid, threads, s, spec, st, L, P, bt, info, eps, tm, lay);
 }
 
-template <int H, bool V4>
+template <int H, int V>
 int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
                       const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
                       const RolloutLds2& lay) {
     const size_t bytes = (size_t)lay.total * 4;
-    auto kern = V4 ? rollout_v4_kernel<H> : rollout_v2_kernel<H>;
+    auto kern = V == 4 ? rollout_v4_kernel<H, 4> : (V == 5 ? rollout_v4_kernel<H, 8> : rollout_v2_kernel<H>);
+    const int threads = V == 4 ? 512 : (V == 5 ? 768 : 512);
     if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)bytes);
         if (e != hipSuccess) return mlg::fail("rollout v2: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
     }
-    hipLaunchKernelGGL(kern, dim3((bt.B + 15) / 16), dim3(512), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
+    hipLaunchKernelGGL(kern, dim3((bt.B + 15) / 16), dim3(threads), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
     return 0;
 }
 
 // v2 when the shape allows it (H 32/64, U <= 32, LDS fits), else v1. MLG_ROLLOUT_KERNEL=v1|v2|v4 forces a
-// variant (v4: the wave-specialised experiment, slower than v2 on the headline shape so far).
+// variant (v4 / v5: the wave-specialised kernel with 4 / 8 agent waves).
 int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay) {
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
     const int want = (k && k[0] == 'v') ? k[1] - '0' : 2;
     if (want == 1 || (L.H != 64 && L.H != 32) || spec.U > 32) return 1;
     *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
     if (lay->total * 4 > LDS_LIMIT_BYTES) return 1;
-    return want == 4 ? 4 : 2;
+    return (want == 4 || want == 5) ? want : 2;
 }
 
 }  // namespace
@@ -1603,12 +1604,12 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
     const int variant = pick_rollout(L, *spec, &lay2);
     if (variant > 1) {
         const bool h64 = dims->hidden == 64;
-        if (variant == 4)
-            rc = h64 ? launch_rollout_v2<64, true>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
-                     : launch_rollout_v2<32, true>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
-        else
-            rc = h64 ? launch_rollout_v2<64, false>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
-                     : launch_rollout_v2<32, false>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
+#define MLG_V(VV) rc = h64 ? launch_rollout_v2<64, VV>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2) \
+                           : launch_rollout_v2<32, VV>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
+        if (variant == 4) MLG_V(4);
+        else if (variant == 5) MLG_V(5);
+        else MLG_V(2);
+#undef MLG_V
         if (rc) return rc;
         return mlg::check_launch("rollout_v2_kernel");
     }
