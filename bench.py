@@ -86,6 +86,7 @@ def main():
     # rollout-kernel timing with HIP events on the stream the kernel is launched on
     stepper.timing = []
     t0_env = stepper.t_env
+    rows0 = int(stepper.agent_rows.item())
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -98,6 +99,7 @@ def main():
     elapsed = t1 - t0
     env_steps = stepper.t_env - t0_env
     local_env_steps = env_steps
+    rows_per_launch = (int(stepper.agent_rows.item()) - rows0) / a.steps
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -118,6 +120,8 @@ def main():
     forwards = (local_env_steps + a.steps * B) / a.steps
     avg_kernel_s = sum(ev_ms) / len(ev_ms) / 1e3
     achieved = fl * forwards / avg_kernel_s
+    # MFMA work actually issued: agent rows through the cell (living agents of running envs, tile padding incl.)
+    issued = fl / N * rows_per_launch / avg_kernel_s
     traffic = None
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
@@ -144,7 +148,9 @@ def main():
                "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12,
                             "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic,
                             "kernel": "rollout_v2_kernel<64>", "avg_kernel_ms": avg_kernel_s * 1e3,
-                            "flops_per_launch": fl * forwards},
+                            "flops_per_launch": fl * forwards,
+                            "issued_tflops": issued / 1e12, "issued_frac": issued / FP32_MFMA_PEAK,
+                            "issued_rows_per_launch": rows_per_launch},
                "cpu_baseline": cpu}
         print(json.dumps(out))
     if dist:

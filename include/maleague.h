@@ -86,6 +86,8 @@ typedef struct {
     float *ret;        /* [B] episode return of the policy team (reward[0]) */
     int32_t *won;      /* [B][2] battle_won, policy team first */
     int32_t *draw;     /* [B] */
+    uint64_t *agent_rows; /* optional [1], accumulated: agent rows the launch ran through the MFMA cell
+                             (16-row tiles, padding included; living agents of running envs only) */
 } MlgRunInfo;
 
 /* Agent weights in canonical nn.Module layout (state_dict of DRQNAgentNetwork). */

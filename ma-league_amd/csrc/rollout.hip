@@ -649,7 +649,7 @@ __device__ __forceinline__ int v2_avail(const UnitMasks& M, int G, int x, int y,
 __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec& spec, const SpecShared& SS,
                                            const int* pairtab, const int* avtab, const MlgBatch& bt, int slot, int t,
                                            int e, int hbase, int hl, const UnitLane& L, float* lobs, int ldo,
-                                           int32_t* lavail, float inv_p, Stamps& sp) {
+                                           uint64_t* lavm, float inv_p, Stamps& sp) {
     const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, G = spec.grid;
     const int64_t st_row = (int64_t)slot * bt.T1 + t;
     const int pk = pk_unit(L.x, L.y, L.hp);
@@ -678,17 +678,22 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
         }
     }
     sp.mark(9);
+    // avail: every unit lane forms its row as a bit mask (noop iff dead; moves in bounds; targets = tgt bits),
+    // agent lanes publish it for the agent phase (LDS), then the half-wave writes the int rows to the batch
+    {
+        const bool alive = L.hp > 0;
+        const uint64_t m = !alive ? 1ull
+                                  : (((uint64_t)L.tgt << MLG_ACT_BASE) | ((uint64_t)(L.y + 1 < G) << 1) |
+                                     ((uint64_t)(L.y - 1 >= 0) << 2) | ((uint64_t)(L.x + 1 < G) << 3) |
+                                     ((uint64_t)(L.x - 1 >= 0) << 4));
+        const int ag = hl < U ? SS.agent[hl] : 0;
+        if (ag) lavm[e * N + ag - 1] = m;
+    }
     for (int k0 = 0; k0 < N * A; k0 += 32) {
         const int k = k0 + hl;
-        const bool valid = k < N * A;
-        const int pt = avtab[valid ? k : 0];
-        const int a = pt >> 8, kk = pt & 255, i = SS.aunit[a];
-        const int qi = __shfl(pk, hbase + i, 64);
-        const uint32_t ti = __shfl((int)L.tgt, hbase + i, 64);
-        const int v = v2_avail(M, G, pk_x(qi), pk_y(qi), pk_hp(qi), ti, kk);
-        if (valid) {
-            bt.avail[st_row * N * A + k] = v;
-            lavail[e * N * A + k] = v;
+        if (k < N * A) {
+            const int pt = avtab[k];
+            bt.avail[st_row * N * A + k] = (int)((lavm[e * N + (pt >> 8)] >> (pt & 255)) & 1ull);
         }
     }
     sp.mark(11);
@@ -717,7 +722,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
 // Env phase: half-wave per env, lane per unit (v2 env above); wave w steps envs 2w and 2w + 1.
 // Barriers per step: A|B, B|C, C|env, env|A.
 struct RolloutLds2 {
-    int64_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, total;
+    int64_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, total;
     int ldo, ldh;
     RoEnvLds env;
 };
@@ -736,13 +741,15 @@ __host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, i
     r.gb = ro_take(o, 4 * L.H);
     const int rows = rew * N, rows16 = (rows + 15) / 16 * 16;
     r.obs = ro_take(o, (int64_t)rows * r.ldo);
-    r.avail = ro_take(o, (int64_t)rows * L.A);
+    r.avail = ro_take(o, (int64_t)rows * 2);  // uint64 avail mask per agent row
     r.xb = ro_take(o, (int64_t)rows16 * r.ldh);
     r.hsz = mlg_align4((int64_t)rows * r.ldh);
     r.hb = ro_take(o, 2 * r.hsz);
     r.pairtab = ro_take(o, (int64_t)N * U);
     r.avtab = ro_take(o, (int64_t)N * L.A);
     r.pk = ro_take(o, (int64_t)rew * 32);
+    r.act = ro_take(o, (int64_t)rew * 32);
+    r.am = ro_take(o, 16);
     r.env = make_env_lds(o, U, N);
     r.total = o;
     return r;
@@ -807,26 +814,44 @@ __device__ inline void load_gru_chunk(GruChunk<H>& W, const float* __restrict__ 
     W.bhn = ld4(fm + lay.gb + 3 * H + j * 16 + 4 * g);
 }
 
-// Compacted agent rows of one step: rows_run = (running envs in `run`) * N; row cr -> env ebase + k-th set
-// bit of run, agent n.
+// Compacted agent rows of one step: the living agents of the running envs ebase .. ebase + ne - 1 (amask[e]
+// bit n = agent n of env e needs a Q this step; dead agents' actions are forced to no-op by the spec, so their
+// cell is skipped and the env phase records the no-op). Row cr -> env of the first inclusive prefix P[l] > cr,
+// agent = (cr - P[l - 1])-th set bit of its mask. P is wave-uniform (readlane of a 16-lane scan).
 struct StepRows {
-    uint32_t run;
-    int ebase, rows_run, tiles, N;
+    int P[16];
+    const uint32_t* amask;
+    int ebase, rows_run, tiles;
     __device__ bool at(int cr, int& e, int& n) const {
         const bool v = cr < rows_run;
-        const int k = v ? cr / N : 0;
-        n = v ? cr - k * N : 0;
-        e = ebase + nth_set_bit(run, k);
+        const int c = v ? cr : 0;
+        int k = 0, base = 0;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) {
+            const bool le = P[l] <= c;
+            k += le;
+            base = le ? P[l] : base;
+        }
+        e = ebase + k;
+        n = nth_set_bit(amask[e], c - base);
         return v;
     }
 };
 
-__device__ inline StepRows make_rows(uint32_t run, int ebase, int N) {
+__device__ inline StepRows make_rows(const uint32_t* amask, int ebase, int ne, int lane) {
     StepRows s;
-    s.run = run;
+    s.amask = amask;
     s.ebase = ebase;
-    s.N = N;
-    s.rows_run = __builtin_popcount(run) * N;
+    const int l16 = lane & 15;
+    int c = l16 < ne ? __builtin_popcount(amask[ebase + l16]) : 0;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+        const int v = __shfl_up(c, d, 16);
+        if (l16 >= d) c += v;
+    }
+#pragma unroll
+    for (int l = 0; l < 16; ++l) s.P[l] = __builtin_amdgcn_readlane(c, l);
+    s.rows_run = s.P[15];
     s.tiles = (s.rows_run + 15) / 16;
     return s;
 }
@@ -835,7 +860,7 @@ __device__ inline StepRows make_rows(uint32_t run, int ebase, int N) {
 template <int H>
 __device__ inline void ph_fc1(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* prev,
                               const StepRows& SR, int j, int ti0, int dt, int t, int lane) {
-    const int col = lane & 15, g = lane >> 4, N = SR.N, ldo = lay.ldo, ldh = lay.ldh, KO = L.Dob / 16;
+    const int col = lane & 15, g = lane >> 4, N = L.N, ldo = lay.ldo, ldh = lay.ldh, KO = L.Dob / 16;
     const float* lobs = fm + lay.obs;
     for (int ti = ti0; ti < SR.tiles; ti += dt) {
         int zero = 0;
@@ -860,9 +885,9 @@ __device__ inline void ph_fc1(const AgentLayout& L, const RolloutLds2& lay, floa
 // B: GRU cell for (tile, chunk j) -> h' (rows of running envs, hidden state indexed by env row)
 template <int H>
 __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, float* fm, const float* hc, float* hn,
-                              const StepRows& SR, int j, int ti0, int dt, int lane) {
+                              const StepRows& SR, int N_, int j, int ti0, int dt, int lane) {
     constexpr int HC = H / 16;
-    const int col = lane & 15, g = lane >> 4, N = SR.N, ldh = lay.ldh;
+    const int col = lane & 15, g = lane >> 4, N = N_, ldh = lay.ldh;
     for (int ti = ti0; ti < SR.tiles; ti += dt) {
         const int cr = ti * 16 + col;
         int e, n;
@@ -900,8 +925,8 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
                               const RoEnv& R, const MlgBatch& bt, const float* hn, const StepRows& SR, int ti0, int dt,
                               int e0, int t, float eps, int test_mode, int lane) {
     constexpr int HC = H / 16;
-    const int col = lane & 15, g = lane >> 4, N = SR.N, ldh = lay.ldh, A = spec.n_actions, n_at = L.Ap / 16;
-    const int32_t* lavail = reinterpret_cast<const int32_t*>(fm) + lay.avail;
+    const int col = lane & 15, g = lane >> 4, N = L.N, ldh = lay.ldh, A = spec.n_actions, n_at = L.Ap / 16;
+    const uint64_t* lavm = reinterpret_cast<const uint64_t*>(fm + lay.avail);
     for (int ti = ti0; ti < SR.tiles; ti += dt) {
         int zero = 0;
         asm volatile("" : "+s"(zero));
@@ -910,17 +935,44 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
         const bool valid = SR.at(cr, e, n);
         const int er = e * N + n;
         const float* hr = hn + (int64_t)er * ldh + 4 * g;
-        const int32_t* av = lavail + er * A;
+        const uint64_t avm = lavm[er];
         ArgmaxState as{-INFINITY, 1 << 30};
         for (int at = 0; at < n_at; ++at) {
             floatx4 q = ld4(fm + lay.b2 + zero + at * 16 + 4 * g);
             const float* w2r = fm + lay.w2 + zero + (int64_t)(at * 16 + col) * ldh + 4 * g;
 #pragma unroll
             for (int kc = 0; kc < HC; ++kc) q = mfma_chunk(ld4(w2r + kc * 16), ld4(hr + kc * 16), q);
-            argmax_accumulate(as, q, av, at, A, lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // masked argmax (argmax_accumulate on the bit mask)
+                const int a = at * 16 + 4 * g + r;
+                if (a >= A) continue;
+                const float v = ((avm >> a) & 1ull) ? q[r] : -INFINITY;
+                if (amax_better(v, a, as.bv, as.bi)) { as.bv = v; as.bi = a; }
+            }
         }
-        const int act = argmax_reduce(as);
-        if (valid && g == 0) ro_record_action(spec, R, bt, act, av, e, n, e0 + e, t, eps, test_mode, false);
+        int act = argmax_reduce(as);
+        if (valid && g == 0) {
+            if (!test_mode && eps > 0.f) {  // epsilon-greedy (action_selectors.py:44-62), counter RNG of spec §3.7
+                const uint64_t key = mlg_env_key(spec.seed, e0 + e);
+                const uint64_t r1 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n));
+                if (mlg_u01(r1) < eps) {
+                    const uint64_t r2 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)n));
+                    const int na = __popcll(avm);  // random_available on the mask: k-th available action
+                    if (na == 0) {
+                        act = 0;
+                    } else {
+                        const int k = (int)(((r2 >> 40) * (uint64_t)na) >> 24);
+                        uint64_t m = avm;
+                        for (int i = 0; i < k; ++i) m &= m - 1;
+                        act = __ffsll((long long)m) - 1;
+                    }
+                }
+            }
+            R.pact[e * N + n] = act;
+            const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
+            bt.actions[bt_off] = act;
+            if (!bt.full_write) bt.actions_onehot[bt_off * A + act] = 1.0f;
+        }
     }
 }
 
@@ -942,9 +994,11 @@ struct EnvCtx {
     MlgRunInfo info;
     const int* pairtab;
     const int* avtab;
-    int* pk;  // [envs][32]
+    int* pk;   // [envs][32] packed unit states (pair pass)
+    int* act;  // [envs][32] executed actions of the step (resolution)
+    uint32_t* amask;  // [16] agents of env e that need a Q in the next agent phase (alive, env running)
     float* lobs;
-    int32_t* lavail;
+    uint64_t* lavm;  // [16 envs * N] avail bit masks of the agents' current step
     int ldo, B;
     float inv_p;
 };
@@ -982,11 +1036,12 @@ __device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, En
         C.R.status[e] = E.st;
         C.R.slot[e] = E.slot;
         C.R.episode[e] = E.ep;
+        C.amask[e] = E.b < C.B ? (spec.n_agents >= 32 ? 0xFFFFFFFFu : (1u << spec.n_agents) - 1u) : 0u;
     }
     if (E.b < C.B) {
         Stamps none;
         v2_pair_pass(C.M, spec.U, hl, E.u, C.pk + e * 32);
-        v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, 0, e, hbase, hl, E.u, C.lobs, C.ldo, C.lavail,
+        v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, 0, e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
                    C.inv_p, none);
     }
 }
@@ -997,8 +1052,13 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     if (E.st == 2) return;
     const MlgEnvSpec& spec = *C.spec;
     const int N = spec.n_agents, A = spec.n_actions, U = spec.U, T1 = C.bt.T1;
-    const int hbase = (threadIdx.x & 63) & 32;
-    const int* pact = C.R.pact + E.e * N;
+    int* pact = C.R.pact + E.e * N;
+    if (hl < N && !((C.amask[E.e] >> hl) & 1u)) {  // dead agent: no cell was run; its action is the no-op
+        pact[hl] = 0;
+        const int64_t off = ((int64_t)E.slot * T1 + t) * N + hl;
+        C.bt.actions[off] = 0;
+        if (!C.bt.full_write) C.bt.actions_onehot[off * A] = 1.0f;
+    }
     if (hl < N) C.R.prev[E.e * N + hl] = pact[hl];
     if (C.bt.full_write) {  // whole one-hot rows of the recorded actions
         const int64_t oh = ((int64_t)E.slot * T1 + t) * N * A;
@@ -1010,6 +1070,7 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     if (E.st == 1) {  // final action recorded; env done (parallel_stepper.py:153)
         E.st = 2;
         E.zcur = t + 1;
+        if (hl == 0) C.amask[E.e] = 0u;
         if (C.bt.full_write && hl == 0) {
             C.bt.reward[(int64_t)E.slot * T1 + t] = 0.f;
             C.bt.terminated[(int64_t)E.slot * T1 + t] = 0;
@@ -1029,15 +1090,25 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
             act = E.u.ai;
         }
     }
-    // E2: simultaneous resolution on the pre-step state, then moves (spec §3.4)
-    const int pk = pk_unit(E.u.x, E.u.y, E.u.hp);
+    // E2: simultaneous resolution on the pre-step state, then moves (spec §3.4). Pre-step unit states are in
+    // pk (written by the last pair pass), actions go through LDS too: 16-byte broadcast reads, no permutes.
+    int* sact = C.act + E.e * 32;
+    const int* spk = C.pk + E.e * 32;
+    sact[hl] = act;
     int dmg = 0, heal = 0;
-    for (int i = 0; i < U; ++i) {
-        const int qi = __shfl(pk, hbase + i, 64), ai = __shfl(act, hbase + i, 64);
-        const bool hit = pk_hp(qi) > 0 && ai == MLG_ACT_BASE + hl;
-        const int ri = mask_role(C.M, i);
-        heal += (hit && ri == 1) ? role_power(1) : 0;
-        dmg += (hit && ri != 1) ? role_power(ri) : 0;
+    const int me = MLG_ACT_BASE + hl;
+    for (int i0 = 0; i0 < U; i0 += 4) {
+        const int4 q4 = *reinterpret_cast<const int4*>(spk + i0);
+        const int4 a4 = *reinterpret_cast<const int4*>(sact + i0);
+        const int qs[4] = {q4.x, q4.y, q4.z, q4.w}, as[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + r;
+            const bool hit = i < U && pk_hp(qs[r]) > 0 && as[r] == me;
+            const bool hl_i = (C.M.healer >> i) & 1;
+            heal += (hit && hl_i) ? role_power(1) : 0;
+            dmg += (hit && !hl_i) ? role_power(mask_role(C.M, i)) : 0;
+        }
     }
     E.h0 = E.u.hp;
     if (uvalid && E.h0 > 0) {
@@ -1091,11 +1162,16 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
         E.len = t + 1;
     }
     if (hl == 0) C.R.status[E.e] = E.st;
+    {  // agents alive after the step need a Q for the next action (incl. the final one after termination)
+        const int N = spec.n_agents;
+        const uint32_t am = (uint32_t)(__ballot(hl < N && ((alive_m >> C.SS->aunit[hl < N ? hl : 0]) & 1u)) >> hbase);
+        if (hl == 0) C.amask[E.e] = am;
+    }
     sp.mark(6);
     // observation at t + 1 (incl. envs that just terminated)
     v2_pair_pass(C.M, U, hl, E.u, C.pk + E.e * 32);
     sp.mark(7);
-    v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavail,
+    v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
                C.inv_p, sp);
 }
 
@@ -1138,8 +1214,10 @@ __device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2&
     C.pairtab = smem + lay.pairtab;
     C.avtab = smem + lay.avtab;
     C.pk = smem + lay.pk;
+    C.act = smem + lay.act;
+    C.amask = reinterpret_cast<uint32_t*>(smem + lay.am);
     C.lobs = fm + lay.obs;
-    C.lavail = smem + lay.avail;
+    C.lavm = reinterpret_cast<uint64_t*>(smem + lay.avail);
     C.ldo = lay.ldo;
     C.B = bt.B;
     C.inv_p = 1.0f / (float)pow2_at_least(spec.grid);
@@ -1168,16 +1246,18 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
     __syncthreads();
     Stamps sp;
     sp.init();
+    uint64_t rows_issued = 0;  // agent rows issued to the MFMA cell (incl. tile padding)
     for (int t = 0; t < T1; ++t) {
         const uint32_t run = (uint32_t)__ballot(lane < REW && C.R.status[lane & (REW - 1)] < 2);
         if (run == 0) break;
-        const StepRows SR = make_rows(run, 0, N);
+        const StepRows SR = make_rows(C.amask, 0, 16, lane);
+        rows_issued += SR.tiles * 16;
         const float* hc = fm + lay.hb + (t & 1) * lay.hsz;
         float* hn = fm + lay.hb + ((t & 1) ^ 1) * lay.hsz;
         ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
         sp.mark(0);
         __syncthreads();
-        ph_gru<H>(W, lay, fm, hc, hn, SR, j, gi, G, lane);
+        ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
         sp.mark(1);
         __syncthreads();
         ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
@@ -1193,6 +1273,7 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
         sp.mark(10);
     }
     sp.flush();
+    if (threadIdx.x == 0 && info.agent_rows) atomicAdd(info.agent_rows, (unsigned long long)rows_issued);
     env_lane_finish(C, st, E, hl);
 }
 
@@ -1251,6 +1332,7 @@ __global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel
         __syncthreads();
         sp.init();
         PhaseState ps{0, 0, false, false};
+        uint64_t rows_issued = 0;
         for (int p = 0;; ++p) {
             uint32_t runX;
             bool done;
@@ -1258,13 +1340,14 @@ __global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel
             if (done) break;
             const int X = p & 1, tX = ps.tg(X);
             const bool doAgent = runX != 0 && tX < T1;
-            const StepRows SR = make_rows(runX, 8 * X, N);
+            const StepRows SR = make_rows(C.amask, 8 * X, 8, lane);
+            rows_issued += doAgent ? SR.tiles * 16 : 0;
             const float* hc = fm + lay.hb + (tX & 1) * lay.hsz;
             float* hn = fm + lay.hb + ((tX & 1) ^ 1) * lay.hsz;
             if (doAgent) ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, tX, lane);
             sp.mark(0);
             __syncthreads();
-            if (doAgent) ph_gru<H>(W, lay, fm, hc, hn, SR, j, gi, G, lane);
+            if (doAgent) ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
             sp.mark(1);
             __syncthreads();
             if (doAgent) ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, AW, e0, tX, eps, test_mode, lane);
@@ -1274,6 +1357,7 @@ __global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel
             phase_end(ps, p, doAgent);
         }
         sp.flush();
+        if (threadIdx.x == 0 && info.agent_rows) atomicAdd(info.agent_rows, (unsigned long long)rows_issued);
     } else {
         EnvLane E0, E1;  // this half-wave's env of group 0 and of group 1
         const int v = wave - AW, h = lane >> 5;

@@ -44,7 +44,7 @@ class MlgBatch(ctypes.Structure):
 
 class MlgRunInfo(ctypes.Structure):
     _fields_ = [("ep_len", ctypes.c_void_p), ("ret", ctypes.c_void_p), ("won", ctypes.c_void_p),
-                ("draw", ctypes.c_void_p)]
+                ("draw", ctypes.c_void_p), ("agent_rows", ctypes.c_void_p)]
 
 
 class MlgAgentParams(ctypes.Structure):

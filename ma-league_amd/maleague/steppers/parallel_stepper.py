@@ -97,6 +97,8 @@ class ParallelStepper(EnvStepper):
         B = self.batch_size
         # one int32 buffer for the per-run summary -> one D2H copy per run
         self._info = torch.zeros(5 * B, dtype=torch.int32, device=self.device)
+        # running count of agent rows the rollout kernels pushed through the MFMA cell (diagnostics / bench)
+        self.agent_rows = torch.zeros(1, dtype=torch.int64, device=self.device)
         pin = self.device.type == "cuda"
         self._info_host = torch.zeros(5 * B, dtype=torch.int32, pin_memory=pin)
         self._pending = None  # (run_id, event, test_mode): summary copy in flight
@@ -229,7 +231,8 @@ class ParallelStepper(EnvStepper):
         B = self.batch_size
         info = self._info
         run_info = _native.MlgRunInfo(info[0:B].data_ptr(), info[4 * B:5 * B].data_ptr(),
-                                      info[B:3 * B].data_ptr(), info[3 * B:4 * B].data_ptr())
+                                      info[B:3 * B].data_ptr(), info[3 * B:4 * B].data_ptr(),
+                                      self.agent_rows.data_ptr())
         agent = self.home_mac.agent
         d = agent.dims()
         st = self.envs.to_c()

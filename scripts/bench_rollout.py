@@ -41,6 +41,10 @@ for k in os.environ.get("MLG_BENCH_KERNELS", "v2").split(","):
         if r >= 2:
             ms.append(stepper.timing[0][0].elapsed_time(stepper.timing[0][1]))
     lens = stepper.last_run["ep_len"].numpy()
+    b = stepper.home_batch
+    fil = b["filled"][:, :, 0].bool()
+    dead = (b["avail_actions"][:, :, :, 0] == 1) & fil[:, :, None]
+    out[k + "_dead_agent_frac"] = float(dead.sum()) / float(fil.sum() * args.n_agents)
     out[k] = {"kernel_ms": sum(ms) / len(ms), "min_ms": min(ms), "env_steps": int(lens.sum()),
               "mean_len": float(lens.mean())}
 print(json.dumps(out))
