@@ -8,6 +8,9 @@
  *
  * Reference interfaces each entry point replaces (file:line in /root/reference):
  *   mlg_rollout        ParallelStepper.run / reset  src/steppers/parallel_stepper.py:82-216
+ *   mlg_rollout_selfplay SelfPlayParallelStepper.run src/steppers/self_play_parallel_stepper.py:73-201
+ *                      (+ SelfPlayStepper.run src/steppers/self_play_stepper.py:44-147,
+ *                         build_pre_transition_data src/steppers/utils/stepper_utils.py:4-24)
  *                      + EnvWorker step/reset       src/steppers/utils/env_worker_process.py:27-71
  *                      + BasicMAC.select_actions    src/marl/controllers/basic_controller.py:29-36
  *                      + EpsilonGreedy.select       src/marl/components/action_selectors.py:44-62
@@ -88,6 +91,7 @@ typedef struct {
     int32_t *draw;     /* [B] */
     uint64_t *agent_rows; /* optional [1], accumulated: agent rows the launch ran through the MFMA cell
                              (16-row tiles, padding included; living agents of running envs only) */
+    float *ret_away;   /* optional [B] (mlg_rollout_selfplay): episode return of the away team (reward[1]) */
 } MlgRunInfo;
 
 /* Agent weights in canonical nn.Module layout (state_dict of DRQNAgentNetwork). */
@@ -119,6 +123,16 @@ int mlg_env_observe(const MlgEnvSpec *spec, const MlgEnvState *st, float *obs /*
  * (DecayThenFlatSchedule.eval(t_env)); test_mode forces epsilon 0. */
 int mlg_rollout(const MlgEnvSpec *spec, MlgEnvState *st, const MlgAgentDims *dims, const float *packed,
                 MlgBatch *batch, MlgRunInfo *info, float epsilon, int32_t test_mode, void *stream);
+
+/* One full SelfPlayParallelStepper.run: both plan teams are policy-controlled (spec->n_agents = 2 * nh, the
+ * first nh agents are the home team). Home agents act with home_packed into `home`, away agents with
+ * away_packed into `away` (obs / avail of each side's own agents; state, terminated and filled in both;
+ * reward[0] -> home, reward[1] -> away, as stepper_utils.build_pre_transition_data splits them). dims
+ * describe ONE side's MAC (n_agents = nh). Epsilon per side; the epsilon RNG stream index is the global
+ * agent index (home 0..nh-1, away nh..2nh-1). info->ret_away receives the away returns. */
+int mlg_rollout_selfplay(const MlgEnvSpec *spec, MlgEnvState *st, const MlgAgentDims *dims, const float *home_packed,
+                         const float *away_packed, MlgBatch *home, MlgBatch *away, MlgRunInfo *info,
+                         float eps_home, float eps_away, int32_t test_mode, void *stream);
 
 /* Zero `count` EpisodeBatch slots starting at slot0 (mod ring_size) in every key -- one launch; the
  * ring-mode pre-fill that replaces constructing a zero EpisodeBatch. slot_bytes[8] = bytes per slot of

@@ -104,8 +104,9 @@ __device__ __forceinline__ EnvTables make_tables(const MlgEnvSpec& spec, const S
 // avail rows the agent phase reads, so the cell never reads back what the env phase wrote to HBM.
 struct RoEnv {
     int *x, *y, *hp, *nhp, *act, *pact, *prev, *status, *stepped, *len, *slot, *list, *misc;
+    int* slot2;  // batch slot of the away side (self-play, v1 only)
     uint32_t* episode;
-    float* ret;
+    float *ret, *ret2;  // episode return of side 0 (home / policy team) and side 1 (away)
     float* lobs;
     int32_t* lavail;
     int ldo;
@@ -113,7 +114,7 @@ struct RoEnv {
 
 // Dynamic-LDS carve of the env part (4-byte words).
 struct RoEnvLds {
-    int64_t spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, list, misc;
+    int64_t spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, list, misc, slot2, ret2;
 };
 
 __host__ __device__ inline int64_t ro_take(int64_t& o, int64_t n) {
@@ -141,6 +142,8 @@ __host__ __device__ inline RoEnvLds make_env_lds(int64_t& o, int U, int n_agents
     r.slot = ro_take(o, RE);
     r.list = ro_take(o, RE);
     r.misc = ro_take(o, 4);  // [0] any env running, [1] number of running envs
+    r.slot2 = ro_take(o, RE);
+    r.ret2 = ro_take(o, RE);
     return r;
 }
 
@@ -161,26 +164,44 @@ __device__ inline RoEnv env_view(int* smem, const RoEnvLds& l) {
     R.misc = smem + l.misc;
     R.episode = reinterpret_cast<uint32_t*>(smem + l.episode);
     R.ret = reinterpret_cast<float*>(smem + l.ret);
+    R.slot2 = smem + l.slot2;
+    R.ret2 = reinterpret_cast<float*>(smem + l.ret2);
     R.lobs = nullptr;
     R.lavail = nullptr;
     R.ldo = 0;
     return R;
 }
 
+// Policy sides of a rollout. ns = 1: one MAC acts for the policy team (ParallelStepper). ns = 2: self-play
+// (self_play_parallel_stepper.py:97-108): agents [0, nh) are the home team and act with P[0] into bt[0],
+// agents [nh, 2 nh) the away team with P[1] into bt[1]; stepper_utils.build_pre_transition_data
+// (stepper_utils.py:4-24) splits obs / avail the same way, state goes to both batches.
+struct Sides {
+    MlgBatch bt[2];
+    const float* P[2];
+    float eps[2];
+    int ns, nh;
+};
+
+// Field selects instead of dynamic indexing: keeps the kernel-argument struct in SGPRs (no scratch copy).
+__device__ __forceinline__ MlgBatch side_batch(const Sides& sd, int side) { return side ? sd.bt[1] : sd.bt[0]; }
+__device__ __forceinline__ int side_slot(const RoEnv& R, int side, int e) { return side ? R.slot2[e] : R.slot[e]; }
+
 // obs/state/avail of batch time index t for the envs selected by `sel` (0: not done at reset, 1: stepped).
-__device__ void ro_observe(const EnvTables& T, const MlgEnvSpec& spec, const RoEnv& R, const MlgBatch& bt, int t,
+__device__ void ro_observe(const EnvTables& T, const MlgEnvSpec& spec, const RoEnv& R, const Sides& sd, int t,
                            bool stepped_only, float inv_p, Stamps& sp) {
     const int tid = threadIdx.x, nthr = blockDim.x;
-    const int U = T.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, T1 = bt.T1;
+    const int U = T.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, T1 = sd.bt[0].T1, nh = sd.nh;
     auto on = [&](int e) { return stepped_only ? R.stepped[e] != 0 : R.status[e] != 2; };
     for (int i = tid; i < RE * N * U; i += nthr) {
         const int e = i / (N * U), r = i % (N * U);
         if (!on(e)) continue;
         const int a = r / U, j = r % U;
+        const int side = a >= nh, ln = a - side * nh;
         float o[8];
         env_obs_feat(T, R.x + e * U, R.y + e * U, R.hp + e * U, spec.agent_unit[a], j, inv_p, o);
         const floatx4 lo{o[0], o[1], o[2], o[3]}, hi{o[4], o[5], o[6], o[7]};
-        float* dst = bt.obs + (((int64_t)R.slot[e] * T1 + t) * N + a) * DO + j * 8;
+        float* dst = side_batch(sd, side).obs + (((int64_t)side_slot(R, side, e) * T1 + t) * nh + ln) * DO + j * 8;
         *reinterpret_cast<floatx4*>(dst) = lo;
         *reinterpret_cast<floatx4*>(dst + 4) = hi;
         if (R.lobs) {
@@ -195,38 +216,49 @@ __device__ void ro_observe(const EnvTables& T, const MlgEnvSpec& spec, const RoE
         if (!on(e)) continue;
         float o[6];
         env_state_feat(T, R.x + e * U, R.y + e * U, R.hp + e * U, j, inv_p, o);
-        float* dst = bt.state + ((int64_t)R.slot[e] * T1 + t) * S + j * 6;
+        for (int side = 0; side < sd.ns; ++side) {
+            float* dst = side_batch(sd, side).state + ((int64_t)side_slot(R, side, e) * T1 + t) * S + j * 6;
 #pragma unroll
-        for (int f = 0; f < 6; ++f) dst[f] = o[f];
+            for (int f = 0; f < 6; ++f) dst[f] = o[f];
+        }
     }
     sp.mark(8);
     for (int i = tid; i < RE * N * A; i += nthr) {
         const int e = i / (N * A), r = i % (N * A);
         if (!on(e)) continue;
-        const int v = env_avail_one(T, R.x + e * U, R.y + e * U, R.hp + e * U, spec.agent_unit[r / A], r % A);
-        bt.avail[((int64_t)R.slot[e] * T1 + t) * N * A + r] = v;
+        const int a = r / A, side = a >= nh;
+        const int v = env_avail_one(T, R.x + e * U, R.y + e * U, R.hp + e * U, spec.agent_unit[a], r % A);
+        side_batch(sd, side).avail[((int64_t)side_slot(R, side, e) * T1 + t) * nh * A + r - side * nh * A] = v;
         if (R.lavail) R.lavail[e * N * A + r] = v;
     }
     sp.mark(9);
 }
 
+__device__ __forceinline__ int ring_slot_of(const MlgBatch& b, int env) {
+    return b.ring_size > 0 ? (b.ring_slot0 + env) % b.ring_size : env;
+}
+
 // Reset of the RE envs (parallel_stepper.py:82-104; env_worker_process.py:54-60) + observation at t = 0.
 __device__ void ro_reset(const EnvTables& T, const SpecShared& SS, const MlgEnvSpec& spec, const MlgEnvState& st,
-                         const RoEnv& R, const MlgBatch& bt, int e0, float inv_p) {
-    const int tid = threadIdx.x, nthr = blockDim.x, U = T.U, B = bt.B;
+                         const RoEnv& R, const Sides& sd, int e0, float inv_p) {
+    const int tid = threadIdx.x, nthr = blockDim.x, U = T.U, B = sd.bt[0].B;
     for (int e = tid; e < RE; e += nthr) {
         const int b = e0 + e;
         R.len[e] = 0;
         R.ret[e] = 0.f;
+        R.ret2[e] = 0.f;
         R.stepped[e] = 0;
         if (b < B) {
             const uint32_t ep = st.episode[b];
             st.episode[b] = ep + 1;
             R.episode[e] = ep;
             R.status[e] = 0;
-            const int sl = bt.ring_size > 0 ? (bt.ring_slot0 + b) % bt.ring_size : b;
-            R.slot[e] = sl;
-            bt.filled[(int64_t)sl * bt.T1] = 1;
+            R.slot[e] = ring_slot_of(sd.bt[0], b);
+            R.slot2[e] = ring_slot_of(sd.bt[1], b);
+            for (int side = 0; side < sd.ns; ++side) {
+                const MlgBatch bt = side_batch(sd, side);
+                bt.filled[(int64_t)side_slot(R, side, e) * bt.T1] = 1;
+            }
         } else {
             R.status[e] = 2;
         }
@@ -241,7 +273,7 @@ __device__ void ro_reset(const EnvTables& T, const SpecShared& SS, const MlgEnvS
     }
     __syncthreads();
     Stamps none;
-    ro_observe(T, spec, R, bt, 0, false, inv_p, none);
+    ro_observe(T, spec, R, sd, 0, false, inv_p, none);
 }
 
 // Running-env list (status < 2, ascending) and count; single thread, caller syncs.
@@ -255,9 +287,10 @@ __device__ inline void ro_list_running(const RoEnv& R) {
 
 // Env phase of step t for the running envs (env_worker_process.py:32-53 batched): executed actions
 // (policy or scripted AI), simultaneous resolution, per-env reward / termination, then obs of t + 1.
+// Side s receives the reward of its own team (self-play: reward = (home, away), self_play_parallel_stepper.py:159).
 __device__ void ro_env_step(const EnvTables& T, const SpecShared& SS, const MlgEnvSpec& spec, const RoEnv& R,
-                            const MlgBatch& bt, const MlgRunInfo& info, int e0, int t, float inv_p, Stamps& sp) {
-    const int tid = threadIdx.x, nthr = blockDim.x, U = T.U, N = spec.n_agents, T1 = bt.T1;
+                            const Sides& sd, const MlgRunInfo& info, int e0, int t, float inv_p, Stamps& sp) {
+    const int tid = threadIdx.x, nthr = blockDim.x, U = T.U, N = spec.n_agents, T1 = sd.bt[0].T1;
     for (int i = tid; i < RE * U; i += nthr) {
         const int e = i / U, u = i % U;
         if (R.status[e] != 0) continue;
@@ -275,6 +308,7 @@ __device__ void ro_env_step(const EnvTables& T, const SpecShared& SS, const MlgE
     }
     sp.mark(5);
     __syncthreads();
+    const int pt = spec.policy_team;  // team of side 0; side 1 (self-play) is the other plan team
     for (int e = tid; e < RE; e += nthr) {
         const int b = e0 + e;
         const int status = R.status[e];
@@ -283,9 +317,12 @@ __device__ void ro_env_step(const EnvTables& T, const SpecShared& SS, const MlgE
         for (int n = 0; n < N; ++n) R.prev[e * N + n] = R.pact[e * N + n];
         if (status == 1) {  // final action recorded; env done (parallel_stepper.py:153)
             R.status[e] = 2;
-            if (bt.full_write) {
-                bt.reward[(int64_t)R.slot[e] * T1 + t] = 0.f;
-                bt.terminated[(int64_t)R.slot[e] * T1 + t] = 0;
+            for (int side = 0; side < sd.ns; ++side) {
+                const MlgBatch bt = side_batch(sd, side);
+                if (bt.full_write) {
+                    bt.reward[(int64_t)side_slot(R, side, e) * T1 + t] = 0.f;
+                    bt.terminated[(int64_t)side_slot(R, side, e) * T1 + t] = 0;
+                }
             }
             continue;
         }
@@ -304,13 +341,17 @@ __device__ void ro_env_step(const EnvTables& T, const SpecShared& SS, const MlgE
         int won[2];
         won[0] = alive[1] == 0 && alive[0] > 0;
         won[1] = alive[0] == 0 && alive[1] > 0;
-        const int pt = spec.policy_team;
-        const int r_int = lost[1 - pt] + 10 * kills[pt] + 200 * won[pt];
-        const float r = (float)r_int * 0.0625f;
-        bt.reward[(int64_t)R.slot[e] * T1 + t] = r;
-        bt.terminated[(int64_t)R.slot[e] * T1 + t] = (uint8_t)done;
-        bt.filled[(int64_t)R.slot[e] * T1 + t + 1] = 1;
-        R.ret[e] += r;
+        for (int side = 0; side < sd.ns; ++side) {
+            const int tm = side ? 1 - pt : pt;
+            const float r = (float)(lost[1 - tm] + 10 * kills[tm] + 200 * won[tm]) * 0.0625f;
+            const MlgBatch bt = side_batch(sd, side);
+            const int64_t sl = (int64_t)side_slot(R, side, e) * T1 + t;
+            bt.reward[sl] = r;
+            bt.terminated[sl] = (uint8_t)done;
+            bt.filled[sl + 1] = 1;
+            if (side) R.ret2[e] += r;
+            else R.ret[e] += r;
+        }
         R.stepped[e] = 1;
         if (done) {
             R.status[e] = 1;
@@ -323,22 +364,24 @@ __device__ void ro_env_step(const EnvTables& T, const SpecShared& SS, const MlgE
     sp.mark(6);
     __syncthreads();
     // observation at t + 1 for envs that stepped (incl. those that just terminated)
-    ro_observe(T, spec, R, bt, t + 1, true, inv_p, sp);
+    ro_observe(T, spec, R, sd, t + 1, true, inv_p, sp);
 }
 
 // Zero every key of slots [t0, t1) of the envs of this workgroup that are done and did not step
 // (status 2, or stepped == 0 with status 2 after the final action): the full-write (ring) mode's
-// replacement for zero-initialising the EpisodeBatch.
-__device__ void zero_slots(const MlgBatch& bt, const RoEnv& R, int e0, int t0, int t1, int N, int A, int S, int DO) {
-    const int T1 = bt.T1, B = bt.B;
+// replacement for zero-initialising the EpisodeBatch. Sides in full-write mode only.
+__device__ void zero_slots(const Sides& sd, const RoEnv& R, int e0, int t0, int t1, int A, int S, int DO) {
+    const int T1 = sd.bt[0].T1, B = sd.bt[0].B, N = sd.nh;
     const int per = S + N * DO + 2 * N * A + 2 * N + 3;  // words per slot (actions/filled are 2 words)
-    const int total = RE * (t1 - t0) * per;
+    const int total = sd.ns * RE * (t1 - t0) * per;
     for (int i = threadIdx.x; i < total; i += blockDim.x) {
-        const int e = i / ((t1 - t0) * per), rem = i % ((t1 - t0) * per);
+        const int side = i / (RE * (t1 - t0) * per), ii = i % (RE * (t1 - t0) * per);
+        const int e = ii / ((t1 - t0) * per), rem = ii % ((t1 - t0) * per);
         const int t = t0 + rem / per;
         int k = rem % per;
-        if (e0 + e >= B || R.status[e] != 2 || R.stepped[e]) continue;
-        const int64_t sl = (int64_t)R.slot[e] * T1 + t;
+        const MlgBatch bt = side_batch(sd, side);
+        if (!bt.full_write || e0 + e >= B || R.status[e] != 2 || R.stepped[e]) continue;
+        const int64_t sl = (int64_t)side_slot(R, side, e) * T1 + t;
         if (k < S) { bt.state[sl * S + k] = 0.f; continue; }
         k -= S;
         if (k < N * DO) { bt.obs[sl * N * DO + k] = 0.f; continue; }
@@ -365,6 +408,7 @@ __device__ void ro_finish(const MlgEnvState& st, const RoEnv& R, const MlgRunInf
         if (b >= B) continue;
         info.ep_len[b] = R.len[e];
         info.ret[b] = R.ret[e];
+        if (info.ret_away) info.ret_away[b] = R.ret2[e];
         st.t[b] = R.len[e];
     }
     for (int i = tid; i < RE * U; i += nthr) {
@@ -377,33 +421,37 @@ __device__ void ro_finish(const MlgEnvState& st, const RoEnv& R, const MlgRunInf
     }
 }
 
-// Picks the action of this lane's row from the masked argmax (EpsilonGreedyActionSelector.select,
-// action_selectors.py:44-62) and records it: LDS pending action, batch actions / actions_onehot.
-__device__ __forceinline__ void ro_record_action(const MlgEnvSpec& spec, const RoEnv& R, const MlgBatch& bt, int act,
-                                                 const int32_t* av, int e, int n, int b, int t, float eps,
-                                                 int test_mode, bool onehot_row) {
-    const int N = spec.n_agents, A = spec.n_actions;
+// Picks the action of agent a (global index; side a >= nh) from the masked argmax
+// (EpsilonGreedyActionSelector.select, action_selectors.py:44-62) and records it: LDS pending action,
+// the side's batch actions / actions_onehot. The epsilon RNG stream index is the global agent index.
+__device__ __forceinline__ void ro_record_action(const MlgEnvSpec& spec, const RoEnv& R, const Sides& sd, int act,
+                                                 const int32_t* av, int e, int a, int b, int t, int test_mode) {
+    const int N = spec.n_agents, A = spec.n_actions, nh = sd.nh;
+    const int side = a >= nh, ln = a - side * nh;
+    const float eps = side ? sd.eps[1] : sd.eps[0];
     if (!test_mode && eps > 0.f) {
         const uint64_t key = mlg_env_key(spec.seed, b);
-        const uint64_t r1 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n));
+        const uint64_t r1 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)a));
         if (mlg_u01(r1) < eps) {
-            const uint64_t r2 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)n));
+            const uint64_t r2 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)a));
             act = random_available(av, A, r2);
         }
     }
-    R.pact[e * N + n] = act;
-    const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
+    R.pact[e * N + a] = act;
+    const MlgBatch bt = side_batch(sd, side);
+    const int64_t bt_off = ((int64_t)side_slot(R, side, e) * bt.T1 + t) * nh + ln;
     bt.actions[bt_off] = act;
-    if (onehot_row)
+    if (bt.full_write)
         for (int k = 0; k < A; ++k) bt.actions_onehot[bt_off * A + k] = k == act ? 1.0f : 0.0f;
-    else if (!bt.full_write)
+    else
         bt.actions_onehot[bt_off * A + act] = 1.0f;
 }
 
 // ================================================================================================
-// v1: generic kernel (any H in {32, 64, 128}, weights in LDS or HBM). Workgroup = W waves
-// (W = min(tiles, 8)); wave w owns the 16-row agent tiles w, w + W, ... (row = env * N + agent) for the
-// whole episode with the GRU hidden state in VGPRs.
+// v1: generic kernel (any H in {32, 64, 128}, weights in LDS or HBM; the only kernel with self-play sides).
+// Workgroup = W waves (W = min(tiles, 8)); wave w owns the 16-row agent tiles w, w + W, ... for the whole
+// episode with the GRU hidden state in VGPRs. Tiles never mix sides: side s owns tiles [s tps, (s+1) tps),
+// row r of side s = env (r / nh), agent s nh + r % nh.
 struct RolloutLds {
     int64_t wts, total;
     RoEnvLds env;
@@ -423,23 +471,23 @@ __host__ __device__ inline RolloutLds make_rollout_lds(const AgentLayout& L, int
 }
 
 template <int H, int TPW, bool WLDS>
-__global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
-                                                     const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
-                                                     float eps, int test_mode, RolloutLds lay) {
+__global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L, Sides sd,
+                                                     MlgRunInfo info, int test_mode, RolloutLds lay) {
     constexpr int HC = H / 16;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     SpecShared& SS = *reinterpret_cast<SpecShared*>(smem + lay.env.spec);
     const RoEnv R = env_view(smem, lay.env);
-    const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U;
+    const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, nh = sd.nh;
     const int tid = threadIdx.x, nthr = blockDim.x;
     const int lane = tid & 63, wave = tid >> 6, W = nthr >> 6;
     const int e0 = blockIdx.x * RE;
-    const int T1 = bt.T1;
+    const int T1 = sd.bt[0].T1;
+    const bool any_full_write = sd.bt[0].full_write || (sd.ns > 1 && sd.bt[1].full_write);
     load_spec_tables(spec, SS);
-    if (WLDS) load_weights_to_lds(P, L, lay.lw, reinterpret_cast<float*>(smem + lay.wts));
+    if (WLDS) load_weights_to_lds(sd.P[0], L, lay.lw, reinterpret_cast<float*>(smem + lay.wts));
     const EnvTables T = make_tables(spec, SS);
     const float inv_p = 1.0f / (float)pow2_at_least(spec.grid);
-    ro_reset(T, SS, spec, st, R, bt, e0, inv_p);
+    ro_reset(T, SS, spec, st, R, sd, e0, inv_p);
     __syncthreads();
 
     floatx4 h[TPW][HC];
@@ -449,7 +497,7 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         for (int c = 0; c < HC; ++c) h[ti][c] = floatx4{0.f, 0.f, 0.f, 0.f};
     Stamps sp;
     sp.init();
-    const int n_tiles = (RE * N + 15) / 16;
+    const int tps = (RE * nh + 15) / 16, n_tiles = sd.ns * tps;
     const int col = lane & 15, g = lane >> 4;
     const int n_at = L.Ap / 16;
     int last_t = 0;
@@ -459,22 +507,25 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
         for (int ti = 0; ti < TPW; ++ti) {
             const int tile = wave + ti * W;
             if (tile >= n_tiles) continue;
-            const int row = tile * 16 + col;
-            const int e = row / N, n = row % N;
-            const bool valid = row < RE * N && R.status[e] < 2;
+            const int side = tile >= tps;
+            const int r = (tile - side * tps) * 16 + col;
+            const bool in_range = r < RE * nh;
+            const int e = in_range ? r / nh : 0, ln = r % nh, a = side * nh + ln;
+            const bool valid = in_range && R.status[e] < 2;
             if (!__any(valid)) continue;  // wave-uniform skip of finished tiles
             // Opaque zero offset per tile: stops LICM/CSE from keeping t- and tile-invariant weight loads
             // live across the episode loop in (spilled) registers.
             int zero = 0;
             asm volatile("" : "+s"(zero));
             const WView Wv = WLDS ? lds_view(reinterpret_cast<const float*>(smem + lay.wts) + zero, lay.lw, L)
-                                  : global_view(P + zero, L);
-            const int64_t bt_off = valid ? ((int64_t)R.slot[e] * T1 + t) * N + n : 0;
+                                  : global_view((side ? sd.P[1] : sd.P[0]) + zero, L);
+            const MlgBatch bt = side_batch(sd, side);
+            const int64_t bt_off = valid ? ((int64_t)side_slot(R, side, e) * T1 + t) * nh + ln : 0;
             RowIn in;
             in.x = valid ? bt.obs + bt_off * DO : nullptr;
             in.onehot = nullptr;
-            in.prev_action = (valid && t > 0) ? R.prev[e * N + n] : -1;
-            in.agent = valid ? n : 0;
+            in.prev_action = (valid && t > 0) ? R.prev[e * N + a] : -1;
+            in.agent = valid ? ln : 0;
             agent_cell_hidden<H>(Wv, L, in, h[ti], lane);
             const int32_t* av = valid ? bt.avail + bt_off * A : nullptr;
             ArgmaxState as{-INFINITY, 1 << 30};
@@ -483,14 +534,14 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
                 argmax_accumulate(as, q, av, at, A, lane);
             }
             const int act = argmax_reduce(as);
-            if (valid && g == 0) ro_record_action(spec, R, bt, act, av, e, n, e0 + e, t, eps, test_mode, bt.full_write);
+            if (valid && g == 0) ro_record_action(spec, R, sd, act, av, e, a, e0 + e, t, test_mode);
         }
         sp.mark(0);
         __syncthreads();
         sp.mark(1);
-        ro_env_step(T, SS, spec, R, bt, info, e0, t, inv_p, sp);
+        ro_env_step(T, SS, spec, R, sd, info, e0, t, inv_p, sp);
         // full-write mode: slot t+1 of envs that are done (t+1 > episode length) gets zeros
-        if (bt.full_write && t + 1 < T1) zero_slots(bt, R, e0, t + 1, t + 2, N, A, S, DO);
+        if (any_full_write && t + 1 < T1) zero_slots(sd, R, e0, t + 1, t + 2, A, S, DO);
         if (tid == 0) ro_list_running(R);
         __syncthreads();
         sp.mark(10);
@@ -501,8 +552,8 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     // full-write mode: the remaining slots of every env (all of them are done here)
     for (int e = tid; e < RE; e += nthr) R.stepped[e] = 0;
     __syncthreads();
-    if (bt.full_write && last_t + 2 < T1) zero_slots(bt, R, e0, last_t + 2, T1, N, A, S, DO);
-    ro_finish(st, R, info, e0, bt.B, U);
+    if (any_full_write && last_t + 2 < T1) zero_slots(sd, R, e0, last_t + 2, T1, A, S, DO);
+    ro_finish(st, R, info, e0, sd.bt[0].B, U);
 }
 
 // Full-write (ring) mode: zero timesteps [z0, z1) of every key of batch slot `slot`.
@@ -1512,8 +1563,7 @@ constexpr int LDS_LIMIT_BYTES = 160 * 1024;
 
 template <int H, int TPW, bool WLDS>
 int launch_rollout_t(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st,
-                     const AgentLayout& L, const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
-                     const RolloutLds& lay) {
+                     const AgentLayout& L, const Sides& sd, const MlgRunInfo& info, int tm, const RolloutLds& lay) {
     const size_t bytes = (size_t)lay.total * 4;
     auto kern = rollout_kernel<H, TPW, WLDS>;
     if (bytes > 64 * 1024) {
@@ -1521,18 +1571,19 @@ int launch_rollout_t(int grid, int threads, hipStream_t s, const MlgEnvSpec& spe
                                            (int)bytes);
         if (e != hipSuccess) return mlg::fail("rollout: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), bytes, s, spec, st, L, sd, info, tm, lay);
     return 0;
 }
 
+// Weights in LDS when one policy's image fits (self-play holds two policies: weights stay in HBM / L2).
 template <int H, int TPW>
 int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st,
-                   const AgentLayout& L, const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm) {
+                   const AgentLayout& L, const Sides& sd, const MlgRunInfo& info, int tm) {
     RolloutLds lay = make_rollout_lds(L, spec.U, spec.n_agents, true);
-    if (lay.total * 4 <= LDS_LIMIT_BYTES && !getenv("MLG_ROLLOUT_GLOBAL_WEIGHTS"))
-        return launch_rollout_t<H, TPW, true>(grid, threads, s, spec, st, L, P, bt, info, eps, tm, lay);
+    if (sd.ns == 1 && lay.total * 4 <= LDS_LIMIT_BYTES && !getenv("MLG_ROLLOUT_GLOBAL_WEIGHTS"))
+        return launch_rollout_t<H, TPW, true>(grid, threads, s, spec, st, L, sd, info, tm, lay);
     lay = make_rollout_lds(L, spec.U, spec.n_agents, false);
-    return launch_rollout_t<H, TPW, false>(grid, threads, s, spec, st, L, P, bt, info, eps, tm, lay);
+    return launch_rollout_t<H, TPW, false>(grid, threads, s, spec, st, L, sd, info, tm, lay);
 }
 
 template <int H, int V>
@@ -1660,34 +1711,76 @@ extern "C" int mlg_env_observe(const MlgEnvSpec* spec, const MlgEnvState* st, fl
     return mlg::check_launch("env_observe_kernel");
 }
 
+namespace {
+
+int check_rollout_batch(const MlgBatch* batch, const MlgEnvSpec* spec, const MlgEnvState* st, const char* who) {
+    MLG_REQUIRE(batch, "%s: null batch", who);
+    MLG_REQUIRE(batch->state && batch->obs && batch->actions && batch->avail && batch->reward && batch->terminated &&
+                    batch->actions_onehot && batch->filled,
+                "%s: batch has null tensors", who);
+    MLG_REQUIRE(batch->B == st->B, "%s: batch B=%d != env B=%d", who, batch->B, st->B);
+    MLG_REQUIRE(batch->rows == nullptr, "%s: sampled (rows) views are read-only; use ring mode to write slots", who);
+    MLG_REQUIRE(batch->T1 == spec->episode_limit + 1, "%s: batch T1=%d != episode_limit+1=%d", who, batch->T1,
+                spec->episode_limit + 1);
+    MLG_REQUIRE(batch->ring_size == 0 || (batch->ring_size >= batch->B && batch->ring_slot0 >= 0 &&
+                                          batch->ring_slot0 < batch->ring_size),
+                "%s: bad ring (slot0=%d size=%d B=%d)", who, batch->ring_slot0, batch->ring_size, batch->B);
+    return 0;
+}
+
+// The generic (v1) kernel: any H in {32, 64, 128}, one or two policy sides.
+int dispatch_rollout_v1(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
+                        const Sides& sd, const MlgRunInfo& info, int test_mode) {
+    const int tiles = sd.ns * ((RE * sd.nh + 15) / 16);
+    const int W = tiles < 8 ? tiles : 8;
+    const int tpw = (tiles + W - 1) / W;
+    const int grid = (st.B + RE - 1) / RE;
+    const int threads = W * 64;
+    int rc = 0;
+    MLG_REQUIRE(tpw <= 4, "rollout: %d agent tiles per wave > 4 (too many agents per env)", tpw);
+#define MLG_RO(HH, TT) rc = launch_rollout<HH, TT>(grid, threads, s, spec, st, L, sd, info, test_mode)
+    if (L.H == 64) {
+        if (tpw == 1) MLG_RO(64, 1);
+        else if (tpw == 2) MLG_RO(64, 2);
+        else if (tpw == 3) MLG_RO(64, 3);
+        else MLG_RO(64, 4);
+    } else if (L.H == 32) {
+        if (tpw == 1) MLG_RO(32, 1);
+        else if (tpw == 2) MLG_RO(32, 2);
+        else if (tpw == 3) MLG_RO(32, 3);
+        else MLG_RO(32, 4);
+    } else if (L.H == 128) {
+        if (tpw == 1) MLG_RO(128, 1);
+        else if (tpw == 2) MLG_RO(128, 2);
+        else if (tpw == 3) MLG_RO(128, 3);
+        else MLG_RO(128, 4);
+    } else {
+        return mlg::fail("rollout: rnn_hidden_dim=%d unsupported (32, 64, 128)", L.H);
+    }
+#undef MLG_RO
+    if (rc) return rc;
+    return mlg::check_launch("rollout_kernel");
+}
+
+}  // namespace
+
 extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAgentDims* dims, const float* packed,
                            MlgBatch* batch, MlgRunInfo* info, float epsilon, int32_t test_mode, void* stream) {
     if (check_spec(spec) || check_state(st) || check_agent_dims(dims)) return 1;
     MLG_REQUIRE(packed && batch && info, "rollout: null pointer");
-    MLG_REQUIRE(batch->state && batch->obs && batch->actions && batch->avail && batch->reward && batch->terminated &&
-                    batch->actions_onehot && batch->filled,
-                "rollout: batch has null tensors");
+    if (check_rollout_batch(batch, spec, st, "rollout")) return 1;
     MLG_REQUIRE(info->ep_len && info->ret && info->won && info->draw, "rollout: run info has null tensors");
-    MLG_REQUIRE(batch->B == st->B, "rollout: batch B=%d != env B=%d", batch->B, st->B);
-    MLG_REQUIRE(batch->rows == nullptr, "rollout: sampled (rows) views are read-only; use ring mode to write slots");
-    MLG_REQUIRE(batch->T1 == spec->episode_limit + 1, "rollout: batch T1=%d != episode_limit+1=%d", batch->T1,
-                spec->episode_limit + 1);
     MLG_REQUIRE(dims->n_agents == spec->n_agents && dims->n_actions == spec->n_actions && dims->d_obs == 8 * spec->U,
                 "rollout: agent dims do not match env spec (N=%d/%d A=%d/%d d_obs=%d/%d)", dims->n_agents,
                 spec->n_agents, dims->n_actions, spec->n_actions, dims->d_obs, 8 * spec->U);
     const AgentLayout L = make_agent_layout(*dims);
-    const int tiles = (RE * spec->n_agents + 15) / 16;
-    const int W = tiles < 8 ? tiles : 8;
-    const int tpw = (tiles + W - 1) / W;
-    const int grid = (st->B + RE - 1) / RE;
-    const int threads = W * 64;
     hipStream_t s = (hipStream_t)stream;
     const float eps = test_mode ? 0.f : epsilon;
-    int rc = 0;
     RolloutLds2 lay2;
     const int variant = pick_rollout(L, *spec, &lay2);
     if (variant > 1) {
         const bool h64 = dims->hidden == 64;
+        int rc = 0;
 #define MLG_V(VV) rc = h64 ? launch_rollout_v2<64, VV>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2) \
                            : launch_rollout_v2<32, VV>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
         if (variant == 4) MLG_V(4);
@@ -1697,26 +1790,45 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
         if (rc) return rc;
         return mlg::check_launch("rollout_v2_kernel");
     }
-#define MLG_RO(HH, TT) rc = launch_rollout<HH, TT>(grid, threads, s, *spec, *st, L, packed, *batch, *info, eps, test_mode)
-    if (dims->hidden == 64) {
-        if (tpw == 1) MLG_RO(64, 1);
-        else if (tpw == 2) MLG_RO(64, 2);
-        else if (tpw == 3) MLG_RO(64, 3);
-        else MLG_RO(64, 4);
-    } else if (dims->hidden == 32) {
-        if (tpw == 1) MLG_RO(32, 1);
-        else if (tpw == 2) MLG_RO(32, 2);
-        else if (tpw == 3) MLG_RO(32, 3);
-        else MLG_RO(32, 4);
-    } else if (dims->hidden == 128) {
-        if (tpw == 1) MLG_RO(128, 1);
-        else if (tpw == 2) MLG_RO(128, 2);
-        else if (tpw == 3) MLG_RO(128, 3);
-        else MLG_RO(128, 4);
-    } else {
-        return mlg::fail("rollout: rnn_hidden_dim=%d unsupported (32, 64, 128)", dims->hidden);
-    }
-#undef MLG_RO
-    if (rc) return rc;
-    return mlg::check_launch("rollout_kernel");
+    Sides sd;
+    sd.bt[0] = sd.bt[1] = *batch;
+    sd.P[0] = sd.P[1] = packed;
+    sd.eps[0] = sd.eps[1] = eps;
+    sd.ns = 1;
+    sd.nh = spec->n_agents;
+    return dispatch_rollout_v1(s, *spec, *st, L, sd, *info, test_mode);
+}
+
+extern "C" int mlg_rollout_selfplay(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAgentDims* dims,
+                                    const float* home_packed, const float* away_packed, MlgBatch* home, MlgBatch* away,
+                                    MlgRunInfo* info, float eps_home, float eps_away, int32_t test_mode, void* stream) {
+    if (check_spec(spec) || check_state(st) || check_agent_dims(dims)) return 1;
+    MLG_REQUIRE(home_packed && away_packed && info, "rollout_selfplay: null pointer");
+    if (check_rollout_batch(home, spec, st, "rollout_selfplay (home)") ||
+        check_rollout_batch(away, spec, st, "rollout_selfplay (away)"))
+        return 1;
+    MLG_REQUIRE(info->ep_len && info->ret && info->won && info->draw, "rollout_selfplay: run info has null tensors");
+    MLG_REQUIRE(spec->n_policy_teams == 2 && spec->n_agents % 2 == 0,
+                "rollout_selfplay: %d agents in %d policy teams do not fit the symmetric two-team scenario "
+                "(stepper_utils.py:9)", spec->n_agents, spec->n_policy_teams);
+    const int nh = spec->n_agents / 2;
+    MLG_REQUIRE(dims->n_agents == nh && dims->n_actions == spec->n_actions && dims->d_obs == 8 * spec->U,
+                "rollout_selfplay: agent dims do not match one side of the env (N=%d/%d A=%d/%d d_obs=%d/%d)",
+                dims->n_agents, nh, dims->n_actions, spec->n_actions, dims->d_obs, 8 * spec->U);
+    for (int a = 0; a < nh; ++a)
+        MLG_REQUIRE(spec->team[spec->agent_unit[a]] == spec->policy_team &&
+                        spec->team[spec->agent_unit[nh + a]] == 1 - spec->policy_team,
+                    "rollout_selfplay: agents 0..%d must be the home team, %d..%d the away team", nh - 1, nh,
+                    2 * nh - 1);
+    const AgentLayout L = make_agent_layout(*dims);
+    Sides sd;
+    sd.bt[0] = *home;
+    sd.bt[1] = *away;
+    sd.P[0] = home_packed;
+    sd.P[1] = away_packed;
+    sd.eps[0] = test_mode ? 0.f : eps_home;
+    sd.eps[1] = test_mode ? 0.f : eps_away;
+    sd.ns = 2;
+    sd.nh = nh;
+    return dispatch_rollout_v1((hipStream_t)stream, *spec, *st, L, sd, *info, test_mode);
 }

@@ -44,7 +44,7 @@ class MlgBatch(ctypes.Structure):
 
 class MlgRunInfo(ctypes.Structure):
     _fields_ = [("ep_len", ctypes.c_void_p), ("ret", ctypes.c_void_p), ("won", ctypes.c_void_p),
-                ("draw", ctypes.c_void_p), ("agent_rows", ctypes.c_void_p)]
+                ("draw", ctypes.c_void_p), ("agent_rows", ctypes.c_void_p), ("ret_away", ctypes.c_void_p)]
 
 
 class MlgAgentParams(ctypes.Structure):
@@ -84,6 +84,7 @@ SIGNATURES = {
     "mlg_env_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "mlg_env_observe": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "mlg_rollout": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P]),
+    "mlg_rollout_selfplay": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _I, _P]),
     "mlg_agent_forward": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _P]),
     "mlg_mac_forward": (ctypes.c_int, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "mlg_select_actions": (ctypes.c_int, [_P, _P, _I, _I, _I, _P, _P, _I, ctypes.c_float, _P, _P, _P]),

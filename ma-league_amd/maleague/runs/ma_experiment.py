@@ -37,7 +37,7 @@ class MultiAgentExperiment:
         self.learners = []
         self.start_time = time.time()
         self._play_time = None
-        self.stepper = stepper_REGISTRY[self.args.runner](args=self.args, logger=self.logger, log_start_t=log_start_t)
+        self.stepper = self._build_stepper(log_start_t)
         self.env_info = self.stepper.get_env_info()
         env_scheme = self._integrate_env_info()
         if hasattr(self.logger, "update_scheme"):
@@ -46,6 +46,9 @@ class MultiAgentExperiment:
         self._build_learners()
         for learner in self.learners:
             learner.build_optimizer()
+
+    def _build_stepper(self, log_start_t=0):
+        return stepper_REGISTRY[self.args.runner](args=self.args, logger=self.logger, log_start_t=log_start_t)
 
     def _update_args(self, update):
         self.args = SimpleNamespace(**{**vars(self.args), **update})
@@ -137,6 +140,10 @@ class MultiAgentExperiment:
         if self.on_episode_end is not None:
             self.on_episode_end(env_info)
         self.home_buffer.insert_episode_batch(episode_batch)
+        self._train_home(episode_num)
+
+    def _train_home(self, episode_num):
+        """Sample + one QLearner.train when the buffer can sample (ma_experiment.py:229-241)."""
         if self.home_buffer.can_sample(self.args.batch_size):
             if str(self.home_buffer.device) == str(self.args.device) and getattr(self.args, "sample_in_place", True):
                 # device buffer: the learner reads the sampled episodes in place over their full stored length

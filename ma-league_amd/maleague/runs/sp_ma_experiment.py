@@ -1,0 +1,79 @@
+"""Self-play training loop (API of src/runs/train/sp_ma_experiment.py:12-101 and the league's
+LeagueExperiment, src/runs/train/league_experiment.py:6-24).
+
+The opposing team is a second, frozen policy instead of the scripted AI: both MACs act in the same
+fused rollout launch (SelfPlayParallelStepper), only the home learner trains (sp_ma_experiment.py:81).
+"""
+from __future__ import annotations
+
+from typing import OrderedDict
+
+import torch
+
+from ..controllers import REGISTRY as mac_REGISTRY
+from ..steppers import SELF_REGISTRY as self_steppers_REGISTRY
+from .ma_experiment import MultiAgentExperiment
+
+
+class SelfPlayMultiAgentExperiment(MultiAgentExperiment):
+    def __init__(self, args, logger, on_episode_end=None, log_start_t=0):
+        super().__init__(args, logger, on_episode_end=on_episode_end, log_start_t=log_start_t)
+        # the away agent uses the home buffer's scheme (sp_ma_experiment.py:24-25)
+        self.away_mac = mac_REGISTRY[self.args.mac](self.home_buffer.scheme, self.groups, self.args)
+
+    def load_adversary(self, agent: OrderedDict):
+        """Frozen opponent parameters (a DRQN state_dict), sp_ma_experiment.py:27-29."""
+        self.away_mac.load_state_dict(agent=agent)
+        del agent
+
+    def _integrate_env_info(self):
+        total_n_agents = int(self.env_info["n_agents"])
+        if total_n_agents % 2:
+            raise ValueError(f"A total of {total_n_agents} agents in the env do not fit in the symmetric two-team "
+                             "scenario. Ensure the Self-Play scenario has two team set to is_scripted=False")
+        env_scheme = {"n_agents": total_n_agents // 2, "n_actions": int(self.env_info["n_actions"]),
+                      "state_shape": int(self.env_info["state_shape"]), "total_n_agents": total_n_agents}
+        self._update_args(env_scheme)
+        self.stepper.args = self.args
+        return env_scheme
+
+    def _build_stepper(self, log_start_t=0):
+        return self_steppers_REGISTRY[self.args.runner](args=self.args, logger=self.logger, log_start_t=log_start_t)
+
+    def _init_stepper(self):
+        # (re)initialised every call like the reference (sp_ma_experiment.py:54-58): the away MAC may change
+        self.stepper.initialize(scheme=self.scheme, groups=self.groups, preprocess=self.preprocess,
+                                home_mac=self.home_mac, away_mac=self.away_mac)
+        if getattr(self.args, "zero_copy_insert", True):
+            self.stepper.attach_replay(self.home_buffer)
+
+    def _train_episode(self, episode_num):
+        home_batch, _, env_info = self.stepper.run(test_mode=False)
+        if self.on_episode_end is not None:
+            self.on_episode_end(env_info)
+        self.home_buffer.insert_episode_batch(home_batch)
+        # only the learning (home) agent trains, never its frozen adversary (sp_ma_experiment.py:81)
+        self._train_home(episode_num)
+
+    def evaluate_mean_returns(self, episode_n=1):
+        """Mean home / away episode returns over episode_n test runs (sp_ma_experiment.py:86-101)."""
+        home = torch.zeros(episode_n)
+        away = torch.zeros(episode_n)
+        self._init_stepper()
+        for i in range(episode_n):
+            hb, ab, _ = self.stepper.run(test_mode=True)
+            home[i] = hb["reward"].sum().item() / hb.batch_size
+            away[i] = ab["reward"].sum().item() / ab.batch_size
+        self.stepper.close_env()
+        return home.mean(), away.mean()
+
+
+class LeagueExperiment(SelfPlayMultiAgentExperiment):
+    """league_experiment.py:6-24: self-play training whose home agent can be replaced between matches."""
+
+    def _test(self, n_test_runs):
+        self.last_test_T = self.stepper.t_env  # tests skipped in the league to save compute (:17-19)
+
+    def load_home_agent(self, agent: OrderedDict):
+        self.home_mac.load_state_dict(agent=agent)
+        del agent

@@ -95,12 +95,13 @@ class ParallelStepper(EnvStepper):
         self._cspec = self.spec.to_c()
         self.envs = VecEnvState(self.spec, self.batch_size, self.device)
         B = self.batch_size
-        # one int32 buffer for the per-run summary -> one D2H copy per run
-        self._info = torch.zeros(5 * B, dtype=torch.int32, device=self.device)
+        # one int32 buffer for the per-run summary -> one D2H copy per run:
+        # [ep_len B | won 2B | draw B | return B (f32 bits) | away return B (f32 bits, self-play)]
+        self._info = torch.zeros(6 * B, dtype=torch.int32, device=self.device)
         # running count of agent rows the rollout kernels pushed through the MFMA cell (diagnostics / bench)
         self.agent_rows = torch.zeros(1, dtype=torch.int64, device=self.device)
         pin = self.device.type == "cuda"
-        self._info_host = torch.zeros(5 * B, dtype=torch.int32, pin_memory=pin)
+        self._info_host = torch.zeros(6 * B, dtype=torch.int32, pin_memory=pin)
         self._pending = None  # (run_id, event, test_mode): summary copy in flight
         self._post = []       # resolved runs awaiting host post-processing (logger, env_infos)
         self._runs = {}       # run_id -> (last_run dict, EnvInfos), the latest two
@@ -110,6 +111,7 @@ class ParallelStepper(EnvStepper):
         self.new_batch_fn = None
         self.home_mac = None
         self.home_batch = None
+        self.away_mac = None  # self-play only (SelfPlayParallelStepper)
         self.timing = None  # list -> (start, end) HIP events around every rollout launch (bench.py)
         self._ring = None   # ReplayBuffer written in place (zero-copy insert), see attach_replay()
 
@@ -174,13 +176,19 @@ class ParallelStepper(EnvStepper):
             won = host[B:3 * B].reshape(B, 2).astype(bool)
             draw = host[3 * B:4 * B].astype(bool)
             ret = host[4 * B:5 * B].view(np.float32)
+            ret_away = host[5 * B:6 * B].view(np.float32)
             # env_infos in order of termination (parallel_stepper.py:124,183-184): by episode length, then index
             order = np.lexsort((np.arange(B), ep_len))
             infos = EnvInfos(won[order], draw[order])
             last = {"ep_len": torch.from_numpy(ep_len.copy()), "returns": torch.from_numpy(ret.copy()), "order": order}
+            if self.away_mac is not None:
+                last["away_returns"] = torch.from_numpy(ret_away.copy())
             self._runs[run_id] = (last, infos)
             self._runs.pop(run_id - 2, None)
             self.logger.collect(Collectibles.RETURN, ret.astype(np.float64), origin=Originator.HOME, parallel=True)
+            if self.away_mac is not None:
+                self.logger.collect(Collectibles.RETURN, ret_away.astype(np.float64), origin=Originator.AWAY,
+                                    parallel=True)
             self.logger.collect(Collectibles.WON, won[order, 0], origin=Originator.HOME, parallel=True)
             self.logger.collect(Collectibles.WON, won[order, 1], origin=Originator.AWAY, parallel=True)
             self.logger.collect(Collectibles.DRAW, draw[order], parallel=True)
@@ -227,12 +235,15 @@ class ParallelStepper(EnvStepper):
         self._launch_mb(mb, epsilon, test_mode)
         del keep
 
-    def _launch_mb(self, mb, epsilon: float, test_mode: bool):
+    def _run_info(self):
         B = self.batch_size
         info = self._info
-        run_info = _native.MlgRunInfo(info[0:B].data_ptr(), info[4 * B:5 * B].data_ptr(),
-                                      info[B:3 * B].data_ptr(), info[3 * B:4 * B].data_ptr(),
-                                      self.agent_rows.data_ptr())
+        return _native.MlgRunInfo(info[0:B].data_ptr(), info[4 * B:5 * B].data_ptr(), info[B:3 * B].data_ptr(),
+                                  info[3 * B:4 * B].data_ptr(), self.agent_rows.data_ptr(),
+                                  info[5 * B:6 * B].data_ptr())
+
+    def _launch_mb(self, mb, epsilon: float, test_mode: bool):
+        run_info = self._run_info()
         agent = self.home_mac.agent
         d = agent.dims()
         st = self.envs.to_c()

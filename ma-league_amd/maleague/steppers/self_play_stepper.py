@@ -1,0 +1,113 @@
+"""Self-play steppers (API of src/steppers/self_play_parallel_stepper.py:14-201 and
+src/steppers/self_play_stepper.py:9-147).
+
+Both plan teams are policy-controlled: the home MAC acts for the first team, a frozen away MAC for the
+second (the reference hands the opponent's actions to the env as ``cat(home, away)``,
+self_play_parallel_stepper.py:108). One launch of ``mlg_rollout_selfplay`` runs the whole batched
+episode with both policies: each side's agents use their own weights and epsilon and are recorded into
+their own EpisodeBatch (obs / avail of that side's agents, the shared global state, ``reward[0]`` for
+home and ``reward[1]`` for away; stepper_utils.build_pre_transition_data, stepper_utils.py:4-24).
+``run()`` returns ``(home_batch, away_batch, env_infos)`` like the reference.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from ..components.batch_view import mlg_batch
+from ..components.replay_buffer import RingEpisodeBatch
+from ..exceptions import MultiAgentControllerNotInitialized
+from .parallel_stepper import LazyEnvInfos, ParallelStepper
+
+
+class SelfPlayParallelStepper(ParallelStepper):
+    def __init__(self, args, logger, log_start_t=0):
+        super().__init__(args, logger, log_start_t)
+        if self.spec.n_policy_teams != 2 or self.spec.n_agents % 2:
+            raise ValueError(f"A total of {self.spec.n_agents} agents in the env do not fit in the symmetric "
+                             "two-team scenario. Ensure the Self-Play scenario has two teams set to is_scripted=False")
+        self.away_batch = None
+
+    def initialize(self, scheme, groups, preprocess, home_mac, away_mac=None):
+        if away_mac is None:
+            raise ValueError("self-play needs an away MAC (initialize(..., home_mac, away_mac))")
+        ParallelStepper.initialize(self, scheme, groups, preprocess, home_mac)
+        self.away_mac = away_mac
+
+    @property
+    def epsilons(self):
+        return (getattr(self.home_mac.action_selector, "epsilon", None),
+                getattr(self.away_mac.action_selector, "epsilon", None))
+
+    def _epsilon_of(self, mac, test_mode):
+        sel = mac.action_selector
+        sel.epsilon = sel.schedule.eval(self.t_env)
+        eps = 0.0 if test_mode else float(sel.epsilon)
+        if test_mode:
+            sel.epsilon = 0.0
+        return eps
+
+    def run(self, test_mode=False):
+        if self.home_mac is None or self.away_mac is None:
+            raise MultiAgentControllerNotInitialized()
+        self.reset()
+        self.logger.test_mode = test_mode
+        self.home_mac.init_hidden(batch_size=self.batch_size)
+        self.away_mac.init_hidden(batch_size=self.batch_size)
+        eps_h = self._epsilon_of(self.home_mac, test_mode)
+        eps_a = self._epsilon_of(self.away_mac, test_mode)
+        keep = []
+        ring = self._ring if not test_mode else None
+        if ring is not None:
+            slot0 = ring.buffer_index
+            mb_h, k = mlg_batch(ring)
+            keep.append(k)
+            mb_h.B, mb_h.ring_slot0, mb_h.ring_size, mb_h.full_write = self.batch_size, slot0, ring.buffer_size, 1
+            self.home_batch = RingEpisodeBatch(ring, slot0, self.batch_size)
+        else:
+            self.home_batch = self.new_batch_fn()
+            mb_h, k = mlg_batch(self.home_batch)
+            keep.append(k)
+        self.away_batch = self.new_batch_fn()
+        mb_a, k = mlg_batch(self.away_batch)
+        keep.append(k)
+        h_agent, a_agent = self.home_mac.agent, self.away_mac.agent
+        d, d_a = h_agent.dims(), a_agent.dims()
+        if any(getattr(d, f) != getattr(d_a, f) for f, _ in d._fields_):
+            raise ValueError("home and away agents must have the same architecture")
+        st = self.envs.to_c()
+        run_info = self._run_info()
+        ev = None
+        if self.timing is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        _native.call("mlg_rollout_selfplay", _native.byref(self._cspec), _native.byref(st), _native.byref(d),
+                     _native.ptr(h_agent.packed()), _native.ptr(a_agent.packed()), _native.byref(mb_h),
+                     _native.byref(mb_a), _native.byref(run_info), float(eps_h), float(eps_a),
+                     int(bool(test_mode)), _native.stream_ptr(self.device))
+        if ev is not None:
+            ev[1].record()
+            self.timing.append(ev)
+        del keep
+        self._info_host.copy_(self._info, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
+        self._run_id += 1
+        self._pending = (self._run_id, done, test_mode)
+        self._finish_post()
+        return self.home_batch, self.away_batch, LazyEnvInfos(self, self._run_id)
+
+
+class SelfPlayStepper(SelfPlayParallelStepper):
+    """Single-env self-play stepper (self_play_stepper.py:9-147): B = 1, returns the final env_info dict."""
+
+    def __init__(self, args, logger, log_start_t=0):
+        assert args.batch_size_run == 1
+        super().__init__(args, logger, log_start_t)
+
+    def run(self, test_mode=False):
+        home, away, infos = super().run(test_mode)
+        eh, ea = self.epsilons
+        self.logger.log_stat("home_epsilon", eh, self.log_t)
+        self.logger.log_stat("away_epsilon", ea, self.log_t)
+        return home, away, infos[-1]

@@ -67,6 +67,58 @@ def run(envs, policy, B, T1, N, A, d_obs, S, test_mode=False):
             "info_env": info_env}
 
 
+def run_self_play(envs, home_policy, away_policy, B, T1, N, A, d_obs, S, test_mode=False):
+    """SelfPlayParallelStepper.run bookkeeping (src/steppers/self_play_parallel_stepper.py:50-201, intended
+    semantics: the reference's .send/.recv on Queues is defect SURVEY App. A). Same loop as run(); the env
+    gets cat(home, away) actions (:108), obs / avail are split home = first N agents, away = the rest, state
+    goes to both (stepper_utils.py:4-24), reward (home, away) = reward[0], reward[1] (:159)."""
+    home, away = new_batch(B, T1, N, A, d_obs, S), new_batch(B, T1, N, A, d_obs, S)
+
+    def pre(i, t, st, av, ob):
+        for b, sl in ((home, slice(0, N)), (away, slice(N, 2 * N))):
+            b["state"][i, t], b["avail_actions"][i, t], b["obs"][i, t] = st, av[sl], ob[sl]
+            b["filled"][i, t] = 1
+
+    for i in range(B):
+        pre(i, 0, *envs.reset(i))
+    terminated = [False] * B
+    running = list(range(B))
+    returns = [[0.0] * B, [0.0] * B]
+    env_infos, info_env = [], []
+    steps_this_run = 0
+    t = 0
+    while True:
+        ah = np.asarray(home_policy(t, list(running), home), dtype=np.int64).reshape(len(running), N)
+        aa = np.asarray(away_policy(t, list(running), away), dtype=np.int64).reshape(len(running), N)
+        for b, acts in ((home, ah), (away, aa)):
+            for k, i in enumerate(running):
+                b["actions"][i, t, :, 0] = acts[k]
+                b["actions_onehot"][i, t] = 0
+                b["actions_onehot"][i, t, np.arange(N), acts[k]] = 1.0
+        sent = {i: np.concatenate([ah[k], aa[k]]) for k, i in enumerate(running) if not terminated[i]}
+        running = [i for i in range(B) if not terminated[i]]
+        if all(terminated):
+            break
+        for i in range(B):
+            if terminated[i]:
+                continue
+            rew, done, info, st, av, ob = envs.step(i, sent[i])
+            for side, b in enumerate((home, away)):
+                returns[side][i] += rew[side]
+                b["reward"][i, t, 0] = rew[side]
+                b["terminated"][i, t, 0] = done
+            if not test_mode:
+                steps_this_run += 1
+            if done:
+                env_infos.append(info)
+                info_env.append(i)
+            terminated[i] = done
+            pre(i, t + 1, st, av, ob)
+        t += 1
+    return {"home": home, "away": away, "t": t, "env_steps": steps_this_run, "returns": returns,
+            "env_infos": env_infos, "info_env": info_env}
+
+
 class RefVecEnv:
     """Adapter over oracle/envref.RefEnv instances for run()."""
 

@@ -1,0 +1,226 @@
+"""GPU parity of the self-play rollout (mlg_rollout_selfplay; SelfPlayParallelStepper, SelfPlayStepper,
+SelfPlayMultiAgentExperiment) against the CPU oracle.
+
+Env side, teacher forced: the GPU-recorded home and away actions drive oracle/stepper_ref.run_self_play over
+oracle/env_ref.c; both EpisodeBatches, returns, episode lengths and env_infos must be bit-identical.
+Agent side: every recorded action must be the oracle MAC's masked argmax for its own side's parameters
+(Q within 1e-4; near-ties accepted within that tolerance) or, in train mode, the oracle's epsilon draw
+(RNG stream index = global agent index: home 0..N-1, away N..2N-1).
+"""
+import numpy as np
+import pytest
+import torch
+
+import envref
+import learner_ref as LR
+import stepper_ref
+from helpers import np_batch, qmix_args, ref_envs_for, scheme_for
+
+pytestmark = pytest.mark.gpu
+
+Q_TOL = 1e-4
+
+
+def _sp_args(B, episode_limit, seed, plan="medium_1h_4t", **kw):
+    from maleague.envs.plans import builtin_plan
+    return qmix_args(batch_size_run=B, seed=seed,
+                     env_args={"match_build_plan": builtin_plan(plan, self_play=True), "grid_size": 20,
+                               "stochastic_spawns": True, "episode_limit": episode_limit}, **kw)
+
+
+def _build(device, plan="medium_1h_4t", B=48, episode_limit=40, seed=5):
+    from maleague.components.episode_batch import EpisodeBatch
+    from maleague.controllers import BasicMAC
+    from maleague.custom_logging import MainLogger
+    from maleague.steppers import SelfPlayParallelStepper
+    args = _sp_args(B, episode_limit, seed, plan)
+    stepper = SelfPlayParallelStepper(args, MainLogger())
+    info = stepper.get_env_info()
+    assert info["n_agents"] % 2 == 0
+    args.n_agents, args.n_actions, args.state_shape = info["n_agents"] // 2, info["n_actions"], info["state_shape"]
+    sinfo = dict(info, n_agents=args.n_agents)
+    scheme, groups, preprocess = scheme_for(sinfo, torch)
+    proto = EpisodeBatch(scheme, groups, 1, 2, preprocess=preprocess, device=device)
+    torch.manual_seed(seed)
+    home = BasicMAC(proto.scheme, groups, args)
+    away = BasicMAC(proto.scheme, groups, args)
+    stepper.initialize(scheme, groups, preprocess, home, away)
+    return stepper, home, away, args
+
+
+def _check_sides(stepper, macs, args, batches, infos, episode, test_mode, eps):
+    spec = stepper.spec
+    B, N, A, T1 = stepper.batch_size, spec.n_agents // 2, spec.n_actions, stepper.episode_limit + 1
+    nbs = [np_batch(b) for b in batches]
+    ep_len = stepper.last_run["ep_len"].numpy()
+    assert (ep_len >= 1).all() and (ep_len <= stepper.episode_limit).all()
+    # --- env side + bookkeeping, teacher forced through the oracle self-play stepper ---
+    refs = ref_envs_for(spec, B, seed=args.seed)
+    for r in refs:
+        r.episode = episode
+    pol = [lambda t, run, b, s=s: nbs[s]["actions"][run, t, :, 0] for s in range(2)]
+    out = stepper_ref.run_self_play(stepper_ref.RefVecEnv(refs), pol[0], pol[1], B, T1, N, A, 8 * spec.U,
+                                    6 * spec.U, test_mode=test_mode)
+    for s, key in enumerate(("home", "away")):
+        for k, v in out[key].items():
+            np.testing.assert_array_equal(nbs[s][k], v, err_msg=f"{key}[{k}]")
+    assert stepper.t == out["t"]
+    np.testing.assert_array_equal(stepper.last_run["returns"].numpy(), np.float32(out["returns"][0]))
+    np.testing.assert_array_equal(stepper.last_run["away_returns"].numpy(), np.float32(out["returns"][1]))
+    assert [infos[i] for i in range(B)] == out["env_infos"]
+    if not test_mode:
+        assert int(ep_len.sum()) == out["env_steps"]
+    # --- agent side per side: oracle Q on the recorded batch; greedy / epsilon picks bit-exact ---
+    n_random = 0
+    for s, (mac, nb) in enumerate(zip(macs, nbs)):
+        params = {k: v.detach().cpu() for k, v in mac.agent.state_dict().items()}
+        tb = {k: torch.from_numpy(v) for k, v in nb.items()}
+        with torch.no_grad():
+            q, _ = LR.mac_unroll(params, tb, N, T=int(ep_len.max()) + 1)
+        q = q.numpy()
+        for b in range(B):
+            for t in range(int(ep_len[b]) + 1):
+                for n in range(N):
+                    a = int(nb["actions"][b, t, n, 0])
+                    av = nb["avail_actions"][b, t, n]
+                    if not test_mode and eps[s] > 0:
+                        key = envref.env_key(args.seed, b)
+                        r1 = envref.rng(key, envref.ctr(episode, t, 2, s * N + n))
+                        if envref.u01(r1) < np.float32(eps[s]):
+                            r2 = envref.rng(key, envref.ctr(episode, t, 3, s * N + n))
+                            assert a == envref.random_available(av.tolist(), r2)
+                            n_random += 1
+                            continue
+                    m = np.where(av == 0, -np.inf, q[b, t, n])
+                    srt = np.sort(m)
+                    if srt[-1] - srt[-2] > Q_TOL:
+                        assert a == int(np.argmax(m)), (s, b, t, n)
+                    else:
+                        assert m[a] >= srt[-1] - Q_TOL
+    if not test_mode and max(eps) > 0.2:
+        assert n_random > 0
+
+
+@pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium_1h_2t_2a_melee"])
+def test_selfplay_rollout_parity(device, plan):
+    stepper, home, away, args = _build(device, plan=plan)
+    hb, ab, infos = stepper.run(test_mode=True)
+    _check_sides(stepper, (home, away), args, (hb, ab), infos, episode=0, test_mode=True, eps=(0.0, 0.0))
+    assert stepper.t_env == 0
+    stepper.t_env = 25000
+    eps = max(0.05, 1.0 - 0.95 / 50000 * 25000)
+    # different epsilon per side: the away policy is a frozen snapshot with its own selector state
+    away.action_selector.schedule.eval = lambda t_env: 0.3
+    hb, ab, infos = stepper.run(test_mode=False)
+    _check_sides(stepper, (home, away), args, (hb, ab), infos, episode=1, test_mode=False, eps=(eps, 0.3))
+    assert stepper.epsilons == (pytest.approx(eps), 0.3)
+
+
+def test_selfplay_identical_policies_symmetric(device):
+    """Same weights on both sides, mirrored plan: every recorded step is a valid action of its own side and
+    home + away batches share state / terminated / filled bit for bit."""
+    stepper, home, away, args = _build(device, B=64, episode_limit=50, seed=9)
+    away.load_state(home)
+    hb, ab, _ = stepper.run(test_mode=True)
+    for k in ("state", "terminated", "filled"):
+        assert torch.equal(hb[k], ab[k]), k
+    for b in (hb, ab):
+        nb = np_batch(b)
+        taken = np.take_along_axis(nb["avail_actions"], nb["actions"], axis=-1)[..., 0]
+        assert (taken[nb["filled"][:, :, 0] == 1] == 1).all()
+
+
+def test_selfplay_ring_mode_equals_plain(device):
+    """Home episodes written straight into the replay ring equal the zero-initialised EpisodeBatch."""
+    from maleague.components.replay_buffer import ReplayBuffer
+    from maleague.envs.teams_env import VecEnvState
+    stepper, home, away, args = _build(device, B=48, episode_limit=30, seed=2)
+    info = dict(stepper.get_env_info(), n_agents=args.n_agents)
+    scheme, groups, preprocess = scheme_for(info, torch)
+    ring = ReplayBuffer(scheme, groups, 100, 31, preprocess=preprocess, device=device)
+    for v in ring.data.transition_data.values():
+        v.fill_(7)
+    stepper.t_env = 20000
+    for it in range(3):
+        st0 = VecEnvState(stepper.spec, 48, device)
+        st0.episode.fill_(it)
+        stepper.envs = st0
+        stepper._ring = None
+        hp, ap, _ = stepper.run(test_mode=False)
+        stepper.t_env -= int(stepper.last_run["ep_len"].sum())
+        st1 = VecEnvState(stepper.spec, 48, device)
+        st1.episode.fill_(it)
+        stepper.envs = st1
+        assert stepper.attach_replay(ring)
+        hr, ar, _ = stepper.run(test_mode=False)
+        for k in hp.data.transition_data:
+            assert torch.equal(hp[k], hr[k]), (it, k)
+            assert torch.equal(ap[k], ar[k]), (it, k)
+        ring.insert_episode_batch(hr)
+
+
+def test_selfplay_headline_shape_properties(device):
+    """Config 3 shape per learner (5v5 self-play, 4096 envs, episode_limit 100): invariants + 64-env teacher-forced
+    spot check of both sides."""
+    stepper, home, away, args = _build(device, B=4096, episode_limit=100, seed=0)
+    stepper.t_env = 10 ** 6
+    hb, ab, _ = stepper.run(test_mode=False)
+    L = stepper.last_run["ep_len"].numpy()
+    nbs = [np_batch(hb), np_batch(ab)]
+    for nb in nbs:
+        assert nb["filled"].sum() == (L + 1).sum()
+        assert nb["terminated"].sum() == 4096
+        assert (nb["actions_onehot"].sum(-1)[nb["filled"][:, :, 0] == 1] == 1).all()
+    N = args.n_agents
+    refs = ref_envs_for(stepper.spec, 4096, seed=0)
+    for b in [int(i) for i in np.linspace(0, 4095, 64)]:
+        r = refs[b]
+        r.reset()
+        for t in range(int(L[b])):
+            rew, done, _ = r.step(np.concatenate([nbs[0]["actions"][b, t, :, 0], nbs[1]["actions"][b, t, :, 0]]))
+            assert nbs[0]["reward"][b, t, 0] == np.float32(rew[0]) and nbs[1]["reward"][b, t, 0] == np.float32(rew[1])
+            o = r.obs()
+            np.testing.assert_array_equal(nbs[0]["obs"][b, t + 1], o[:N])
+            np.testing.assert_array_equal(nbs[1]["obs"][b, t + 1], o[N:])
+
+
+def test_selfplay_episode_stepper(device):
+    from maleague.components.episode_batch import EpisodeBatch
+    from maleague.controllers import BasicMAC
+    from maleague.custom_logging import MainLogger
+    from maleague.steppers import SelfPlayStepper
+    args = _sp_args(1, 30, 4)
+    stepper = SelfPlayStepper(args, MainLogger())
+    info = stepper.get_env_info()
+    args.n_agents, args.n_actions, args.state_shape = info["n_agents"] // 2, info["n_actions"], info["state_shape"]
+    scheme, groups, preprocess = scheme_for(dict(info, n_agents=args.n_agents), torch)
+    proto = EpisodeBatch(scheme, groups, 1, 2, preprocess=preprocess, device=device)
+    home, away = BasicMAC(proto.scheme, groups, args), BasicMAC(proto.scheme, groups, args)
+    stepper.initialize(scheme, groups, preprocess, home, away)
+    hb, ab, env_info = stepper.run(test_mode=True)
+    assert set(env_info) == {"battle_won", "draw"}
+    _check_sides(stepper, (home, away), args, (hb, ab), [env_info], episode=0, test_mode=True, eps=(0.0, 0.0))
+
+
+def test_selfplay_experiment_trains_home_only(device):
+    """SelfPlayMultiAgentExperiment: one run + one train per iteration; the away MAC stays frozen."""
+    from maleague.custom_logging import MainLogger
+    from maleague.envs.plans import builtin_plan
+    from maleague.runs import SelfPlayMultiAgentExperiment
+    from maleague.utils.config import build_config, to_args
+    cfg = build_config("qmix", "ma", overrides=["batch_size_run=64", "runner=parallel", "buffer_cpu_only=False",
+                                                "buffer_size=128", "batch_size=32", "env_args.episode_limit=40",
+                                                "t_max=1000000", "test_interval=100000000"])
+    cfg["env_args"]["match_build_plan"] = builtin_plan("medium_1h_4t", self_play=True)
+    exp = SelfPlayMultiAgentExperiment(to_args(cfg), MainLogger())
+    assert exp.args.n_agents == 5 and exp.args.total_n_agents == 10
+    home0 = {k: v.clone() for k, v in exp.home_mac.agent.state_dict().items()}
+    exp.load_adversary(home0)
+    exp.start(max_iterations=3)
+    torch.cuda.synchronize()
+    assert exp.stepper.t_env > 0
+    for k, v in exp.away_mac.agent.state_dict().items():
+        assert torch.equal(v, home0[k]), k
+    assert any(not torch.equal(v, home0[k]) for k, v in exp.home_mac.agent.state_dict().items()), "home trained"
+    h, a = exp.evaluate_mean_returns(episode_n=1)
+    assert torch.isfinite(h) and torch.isfinite(a)
