@@ -1,12 +1,18 @@
-"""bench.py -- env-steps/sec (rollout + learn), 5v5 QMIX, 4096 envs per GPU (BASELINE.json config 2).
+"""bench.py -- env-steps/sec (rollout + learn), 5v5 QMIX, 4096 envs per GPU (BASELINE.json configs 2-4).
 
-One "step" = one iteration of MultiAgentExperiment.start (src/runs/train/ma_experiment.py:173-209 via
-_train_episode :224-241): one ParallelStepper.run over all envs (one fused rollout launch) + insert into
-the HBM replay buffer + one QLearner.train on 32 sampled episodes (fused learner pipeline).
-value = env steps (t_env increments, parallel_stepper.py:178-179) of all ranks / max-over-ranks time.
+One "step" = one training iteration of a learner: one batched rollout launch over its 4096 envs + insert into
+the HBM replay buffer + one QLearner.train on 32 sampled episodes (MultiAgentExperiment._train_episode,
+src/runs/train/ma_experiment.py:224-241). value = env steps (t_env increments, parallel_stepper.py:178-179)
+of all ranks / max-over-ranks time.
 
-N > 1: one process per GPU (torch.distributed.run), each an independent league learner with its own
-4096 envs and replay buffer -- no data-path collective; barrier + max-time all_reduce only.
+Modes (--mode auto picks by world size, as BASELINE.json's configs are defined):
+  ai        config 2: one learner vs the scripted AI per GPU (N = 1)
+  league    config 3 (N = 2: two PFSP self-play learners, opponent swap over RCCL) / config 4 (N >= 4:
+            AlphaStar roles, half main players, half main exploiters, historical snapshots): one league player
+            per GPU; every --match-len iterations a league iteration exchanges parameters (all_gather) and
+            payoff (all_reduce) over RCCL and picks the next opponent. Works at N = 1 too (the player faces
+            its own snapshots): the per-GPU cost of a league learner.
+N > 1: one process per GPU (torch.distributed.run); rollouts and learners never cross GPUs.
 """
 from __future__ import annotations
 
@@ -37,6 +43,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", default="auto", choices=["auto", "ai", "league"])
+    ap.add_argument("--match-len", type=int, default=5, help="league: training iterations per league iteration")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--episode-limit", type=int, default=100)
     ap.add_argument("--plan", default="medium_1h_4t")
@@ -49,6 +57,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    mode = a.mode if a.mode != "auto" else ("ai" if world == 1 else "league")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -65,21 +74,49 @@ def main():
                  f"env_args.match_build_plan={a.plan}", f"env_args.episode_limit={a.episode_limit}",
                  f"seed={rank}", "learner_log_interval=1000000000", "log_interval=1000000000",
                  "runner_log_interval=1000000000", "test_interval=1000000000000", "t_max=1000000000000",
-                 "show_exp_parameters=False"]
+                 "show_exp_parameters=False", "league_checkpoint_min_steps=20000", "league_checkpoint_max_steps=40000"]
     cfg = build_config("qmix", "ma", overrides=overrides, device_index=local_rank)
     import numpy as np
     np.random.seed(rank)  # replay sampling (reproducible learning curve -> reproducible episode lengths)
     torch.manual_seed(rank)
-    exp = MultiAgentExperiment(to_args(cfg), MainLogger(log_interval=10 ** 12))
-    exp._init_stepper()
-    stepper, learner = exp.stepper, exp.home_learner
+    args = to_args(cfg)
+    inst = None
+    if mode == "ai":
+        exp = MultiAgentExperiment(args, MainLogger(log_interval=10 ** 12))
+        exp._init_stepper()
+        workload = f"qmix_5v5_{a.plan}_{a.envs}envs_ep{a.episode_limit}"
+        parallelism = f"league{world}"
+    else:
+        from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
+        lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=8 * world)
+        if world >= 4:
+            roles = league_roles_for(world, args)
+            inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="rolebased", role=roles, seed=0)
+            n_main = roles.count("main")
+            workload = f"pfsp_league_{n_main}main_{world - n_main}exploiter_qmix_5v5_{a.plan}_{a.envs}envs_ep{a.episode_limit}"
+        else:
+            inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="matchmaking", seed=0)
+            workload = f"selfplay_pfsp_{world}learners_qmix_5v5_{a.plan}_{a.envs}envs_ep{a.episode_limit}"
+        exp = inst.experiment
+        parallelism = f"league{world}_rccl"
+    stepper = exp.stepper
     B = stepper.batch_size
     # steady-state exploration (epsilon floor 0.05), as SURVEY §8d prescribes for timing runs
     stepper.t_env = 10 ** 6
     episode = 0
-    for _ in range(a.warmup):
-        exp._train_episode(episode)
-        episode += B
+
+    def iteration(i):
+        nonlocal episode
+        if inst is None:
+            exp._train_episode(episode)
+            episode += B
+        else:
+            if i % a.match_len == 0:
+                inst.sync()  # league iteration: payoff all_reduce + parameter all_gather over RCCL, next match
+            inst.play(1)
+
+    for i in range(a.warmup):
+        iteration(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -89,9 +126,8 @@ def main():
     rows0 = int(stepper.agent_rows.item())
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        exp._train_episode(episode)
-        episode += B
+    for i in range(a.steps):
+        iteration(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -111,24 +147,25 @@ def main():
     stepper.timing = None
     value = env_steps / elapsed
 
-    # roofline of the dominant kernel (rollout_kernel): fp32 MFMA-bound agent cell
+    # roofline of the dominant kernel (the rollout): fp32 MFMA-bound agent cell
     info = stepper.get_env_info()
-    N, A = info["n_agents"], info["n_actions"]
+    sides = 1 if mode == "ai" else 2
+    N, A = info["n_agents"] // sides, info["n_actions"]
     d_in = info["obs_shape"] + A + N
-    fl = agent_flops_per_forward(N, d_in, 64, A)
+    fl = sides * agent_flops_per_forward(N, d_in, 64, A)
     # agent forwards per launch: every env steps len times and records one final action (len + 1 forwards)
     forwards = (local_env_steps + a.steps * B) / a.steps
     avg_kernel_s = sum(ev_ms) / len(ev_ms) / 1e3
     achieved = fl * forwards / avg_kernel_s
-    # MFMA work actually issued: agent rows through the cell (living agents of running envs, tile padding incl.)
-    issued = fl / N * rows_per_launch / avg_kernel_s
+    issued = fl / (sides * N) * rows_per_launch / avg_kernel_s if mode == "ai" else None
     traffic = None
+    kernel = "rollout_v2_kernel<64>" if mode == "ai" else "rollout_kernel<64,2,false> (self-play sides)"
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            traffic = json.load(f).get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and mode == "ai" and not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_baseline
         r = cpu_baseline.run(seconds=a.cpu_seconds, B=64, episode_limit=a.episode_limit,
@@ -141,17 +178,21 @@ def main():
                "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "f32", "data": "synthetic (spec-v1 5v5 battles, random-init QMIX)",
-               "config": {"workload": f"qmix_5v5_{a.plan}_{B}envs_ep{a.episode_limit}", "envs_per_gpu": B,
-                          "episode_limit": a.episode_limit, "learner_batch": 32, "rnn_hidden_dim": 64,
-                          "buffer_size": 5000, "parallelism": f"league{world}"},
+               "config": {"workload": workload, "mode": mode, "envs_per_gpu": B, "episode_limit": a.episode_limit,
+                          "learner_batch": 32, "rnn_hidden_dim": 64, "buffer_size": 5000,
+                          "parallelism": parallelism, **({"match_len": a.match_len} if inst else {})},
                "env_steps": env_steps, "mean_episode_len": env_steps / max(1, a.steps * B * world),
                "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12,
                             "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic,
-                            "kernel": "rollout_v2_kernel<64>", "avg_kernel_ms": avg_kernel_s * 1e3,
-                            "flops_per_launch": fl * forwards,
-                            "issued_tflops": issued / 1e12, "issued_frac": issued / FP32_MFMA_PEAK,
-                            "issued_rows_per_launch": rows_per_launch},
+                            "kernel": kernel, "avg_kernel_ms": avg_kernel_s * 1e3,
+                            "flops_per_launch": fl * forwards},
                "cpu_baseline": cpu}
+        if issued is not None:
+            out["roofline"].update({"issued_tflops": issued / 1e12, "issued_frac": issued / FP32_MFMA_PEAK,
+                                    "issued_rows_per_launch": rows_per_launch})
+        if inst is not None:
+            out["league"] = {"opponents_rank0": [h[1] for h in inst.history],
+                             "historical_snapshots": len(inst.league.historical_meta)}
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

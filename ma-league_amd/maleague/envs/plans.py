@@ -35,3 +35,13 @@ def builtin_plan(name: str, self_play: bool = False):
 
 def available() -> list:
     return sorted(_COMPOSITIONS)
+
+
+def mirror_plan(plan, ai: bool, config_dir=None):
+    """LeagueExperimentInstance._configure_experiment (league_experiment_process.py:57-62) with no away team:
+    team 0 = the home (policy) team, team 1 = its mirror, scripted iff ``ai``."""
+    from .teams_env import load_match_build_plan
+    teams = load_match_build_plan(plan, config_dir)
+    home = next((t for t in teams if not t.get("is_scripted", False)), teams[0])
+    return [{"is_scripted": False, "units": list(home["units"])},
+            {"is_scripted": bool(ai), "units": list(home["units"])}]

@@ -3,13 +3,19 @@
 Replaces the reference's process topology (src/league/processes/*: AgentPool queues, a shared-memory payoff
 tensor incremented racily from every process, Barrier.wait -- SURVEY §2.1 table) with three collectives per
 league iteration:
-  * all_gather of each rank's flat agent parameters  (AgentParamsUpdate/AgentPoolGet, agent_pool_instance.py:115-128)
+  * all_gather of each rank's flat agent parameters + [trained_steps, checkpoint flag]
+    (AgentParamsUpdate/AgentPoolGet/AgentCheckpointAdd, agent_pool_instance.py:84-128)
   * all_reduce(SUM) of each rank's local payoff delta (payoff_entry.py:50-51, central_worker.py:63)
   * barrier                                           (league_experiment_process.py:83)
-They run once per league iteration (play_time_mins), never on the per-step data path.
+They run once per league iteration (play_time_mins), never on the per-step data path. The payoff table and
+the agent pool (current parameters of every player + historical snapshots) are replicated on every rank, so
+matchmaking is local and needs no coordinator process.
 """
 from __future__ import annotations
 
+from typing import List
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -17,19 +23,25 @@ from .payoff import PayoffEntry, PayoffWrapper, PFSPSampling
 
 
 class DistributedLeague:
-    def __init__(self, n_players: int, device, reference_compat: bool = False, seed: int = 0):
+    def __init__(self, n_players: int, device, reference_compat: bool = False, seed: int = 0,
+                 max_historical: int = 0):
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.n = n_players
+        self.capacity = n_players + max_historical  # payoff rows/cols: players, then historical snapshots
         self.device = torch.device(device)
-        self.payoff = PayoffWrapper(torch.zeros(n_players, n_players, 5, device=self.device), reference_compat)
+        self.payoff = PayoffWrapper(torch.zeros(self.capacity, self.capacity, 5, device=self.device), reference_compat)
         self._delta = torch.zeros_like(self.payoff.tensor)
-        import numpy as np
         self.sampling = PFSPSampling(np.random.RandomState(seed + self.rank))
+        # agent pool (replicated): current parameters of every player, historical snapshots
+        self.current = None            # [n_players, n_params]
+        self.historical = None         # [max_historical, n_params]
+        self.historical_meta: List[tuple] = []  # (pid, parent pid, trained_steps)
 
     def player(self) -> int:
         return self.rank % self.n
 
+    # ---- payoff ------------------------------------------------------------------------------------------
     def record(self, home: int, away: int, result: PayoffEntry, n: int = 1):
         """Local, race-free accumulation; published by sync_payoff()."""
         d = PayoffWrapper(self._delta, self.payoff.reference_compat)
@@ -38,6 +50,18 @@ class DistributedLeague:
     def record_match(self, home: int, away: int):
         self._delta[home, away, PayoffEntry.MATCHES] += 1
 
+    def record_runs(self, home: int, away: int, won: torch.Tensor, draw: torch.Tensor):
+        """Episode results of one batched run, on the device (no host sync): _extract_result +
+        _update_payoff (league_experiment_process.py:85-105) for every env. won [B, 2] (policy team first),
+        draw [B]; DRAW if the env says so or if both / no team won, else WIN / LOSS by won[:, 0]."""
+        w0, w1 = won[:, 0] != 0, won[:, 1] != 0
+        d = (draw != 0) | (w0 == w1)
+        win = ~d & w0
+        counts = torch.stack([win.sum(), (~d & ~w0).sum(), d.sum()]).to(self._delta.dtype)
+        self._delta[home, away, PayoffEntry.WIN:PayoffEntry.DRAW + 1] += counts
+        if not self.payoff.reference_compat:
+            self._delta[home, away, PayoffEntry.GAMES] += won.shape[0]
+
     def sync_payoff(self):
         if self.world > 1:
             dist.all_reduce(self._delta, op=dist.ReduceOp.SUM)
@@ -45,6 +69,7 @@ class DistributedLeague:
         self._delta.zero_()
         return self.payoff.tensor
 
+    # ---- agent pool --------------------------------------------------------------------------------------
     def share_params(self, flat: torch.Tensor):
         """Every rank's flat parameter vector (index = rank)."""
         flat = flat.detach().contiguous()
@@ -53,6 +78,38 @@ class DistributedLeague:
         out = [torch.empty_like(flat) for _ in range(self.world)]
         dist.all_gather(out, flat)
         return out
+
+    def exchange(self, flat: torch.Tensor, trained_steps: int, checkpoint: bool):
+        """all_gather [params | trained_steps | checkpoint flag] of every player; refresh the replicated pool and
+        append a historical snapshot for every player that asked for a checkpoint (in player order, so every
+        rank assigns the same historical pids). Returns the list of new historical pids."""
+        n_p = flat.numel()
+        msg = torch.cat([flat.detach().reshape(-1).to(torch.float32),
+                         torch.tensor([float(trained_steps), 1.0 if checkpoint else 0.0], device=flat.device)])
+        gathered = self.share_params(msg)
+        allm = torch.stack(gathered)[: self.n]
+        if self.current is None:
+            self.current = torch.empty(self.n, n_p, dtype=torch.float32, device=flat.device)
+            cap = self.capacity - self.n
+            self.historical = torch.empty(max(cap, 0), n_p, dtype=torch.float32, device=flat.device)
+        self.current.copy_(allm[:, :n_p])
+        meta = allm[:, n_p:].detach().cpu().numpy()
+        new = []
+        for pid in range(self.n):
+            if meta[pid, 1] > 0.5:
+                k = len(self.historical_meta)
+                if self.n + k >= self.capacity:
+                    continue  # pool full: keep the existing snapshots
+                self.historical[k].copy_(self.current[pid])
+                hp = self.n + k
+                self.historical_meta.append((hp, pid, int(meta[pid, 0])))
+                new.append(hp)
+        return new
+
+    def params_of(self, pid: int) -> torch.Tensor:
+        if pid < self.n:
+            return self.current[pid]
+        return self.historical[pid - self.n]
 
     def pfsp_opponent(self, weighting: str = "squared", exclude_self: bool = False) -> int:
         """PFSPMatchmaking.get_match / SimplePlayer.get_match (matchmaker.py:64-72, simple_player.py:24-37)."""

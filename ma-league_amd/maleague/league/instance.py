@@ -1,0 +1,144 @@
+"""One league player per rank: the training loop of a league instance.
+
+Restates the per-process loop of src/league/processes/training/matchmaking_league_instance.py:19-71 and
+role_based_league_instance.py:21-53 (with LeagueExperimentInstance, league_experiment_process.py:57-105):
+  1. (optional) pre-train the home policy against the mirrored scripted AI     (:21-25)
+  2. share the home agent's parameters with the league                          (:26)
+  3. per league iteration: get a match (matchmaker or league role), load the adversary's parameters, play
+     ``iterations_per_match`` self-play training iterations recording every episode's result, share.
+Processes, queues and the coordinator are replaced by one rank per GPU and DistributedLeague collectives.
+The self-play experiment is built once per instance and its adversary swapped between matches (the
+reference rebuilds LeagueExperiment -- replay buffer, optimizer state -- for every match).
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..envs.plans import mirror_plan
+from ..runs import LeagueExperiment, MultiAgentExperiment
+from ..runs.sp_ma_experiment import agent_vector, load_agent_vector
+from .distributed import DistributedLeague
+from .matchmaking import REGISTRY as matchmaking_REGISTRY
+from .roles import ROLES, Historical, LeagueView, alphastar_roles
+
+
+class LeagueInstance:
+    """``mode``: "matchmaking" (args.matchmaking in pfsp/uniform/random/fsp/adversaries, every player a
+    learner) or "rolebased" (``role`` in simple/main/main_exploiter/league_exploiter)."""
+
+    def __init__(self, args, logger, league: DistributedLeague, mode="matchmaking", role=None, seed=0,
+                 experiment=None):
+        self.args, self.logger, self.league = args, logger, league
+        self.pid = league.player()
+        self.mode = mode
+        rng = np.random.RandomState(seed * 1000 + self.pid)
+        if mode == "rolebased":
+            roles = role if isinstance(role, (list, tuple)) else [role or "simple"] * league.n
+            kw = dict(checkpoint_min_steps=float(getattr(args, "league_checkpoint_min_steps", 2e9)),
+                      checkpoint_max_steps=float(getattr(args, "league_checkpoint_max_steps", 4e9)))
+            # every rank holds the full player table (roles are needed by the others' matchmaking)
+            self.players = [ROLES[r](pid, np.random.RandomState(seed * 1000 + pid), **kw) for pid, r in enumerate(roles)]
+            self.me = self.players[self.pid]
+            self.matchmaker = None
+        else:
+            self.players = [ROLES["simple"](pid) for pid in range(league.n)]
+            self.me = self.players[self.pid]
+            self.matchmaker = matchmaking_REGISTRY[getattr(args, "matchmaking", "pfsp")](
+                rng, record_match=league.record_match)
+        if experiment is None:
+            sp_args = copy.deepcopy(args)
+            sp_args.env_args = dict(args.env_args)
+            sp_args.env_args["match_build_plan"] = mirror_plan(args.env_args["match_build_plan"], ai=False,
+                                                                config_dir=getattr(args, "config_dir", None))
+            experiment = LeagueExperiment(sp_args, logger)
+            experiment._init_stepper()
+        self.experiment = experiment
+        self.opponent = None
+        self.history = []  # (league iteration, opponent pid, historical?)
+        self.episode = 0
+
+    # ---- phases -------------------------------------------------------------------------------------------
+    def pretrain_vs_ai(self, iterations: int):
+        """matchmaking_league_instance.py:21-25: initial play against the mirrored scripted AI."""
+        if iterations <= 0:
+            return
+        ai_args = copy.deepcopy(self.args)
+        ai_args.env_args = dict(self.args.env_args)
+        ai_args.env_args["match_build_plan"] = mirror_plan(self.args.env_args["match_build_plan"], ai=True,
+                                                            config_dir=getattr(self.args, "config_dir", None))
+        exp = MultiAgentExperiment(ai_args, self.logger)
+        load_agent_vector(exp.home_mac, agent_vector(self.experiment.home_mac))
+        exp.start(max_iterations=iterations)
+        self.experiment.load_home_agent(exp.home_mac.agent.state_dict())
+        del exp
+
+    def view(self) -> LeagueView:
+        hist = [Historical(pid, parent, steps) for pid, parent, steps in self.league.historical_meta]
+        return LeagueView(self.league.payoff, self.players, hist)
+
+    def sync(self):
+        """League iteration boundary: payoff all_reduce, parameter / checkpoint all_gather, barrier, next match.
+        Returns (opponent pid, historical?) or None when the matchmaker ends the league for this player."""
+        home = self.experiment.home_mac
+        self.league.sync_payoff()
+        steps = int(home.agent.trained_steps)
+        self.me.trained_steps = steps
+        ckpt = self.me.ready_to_checkpoint(self.view()) if self.mode == "rolebased" else False
+        self.league.exchange(agent_vector(home), steps, ckpt)
+        if ckpt:
+            self.me.checkpoint()
+        self.league.barrier()
+        view = self.view()
+        if self.matchmaker is not None:
+            opp, hist = self.matchmaker.get_match(self.pid, view), False
+        else:
+            opp, hist = self.me.get_match(view)
+            self.league.record_match(self.pid, opp)
+        # the league ends for everybody once one player has no match left (keeps the collectives aligned)
+        if self._any(opp is None):
+            return None
+        self.opponent = int(opp)
+        self.experiment.load_adversary_vector(self.league.params_of(self.opponent))
+        self.history.append((len(self.history), self.opponent, bool(hist)))
+        return self.opponent, hist
+
+    def _any(self, flag: bool) -> bool:
+        if self.league.world == 1:
+            return bool(flag)
+        t = torch.tensor([1.0 if flag else 0.0], device=self.league.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return bool(t.item() > 0)
+
+    def play(self, iterations: int):
+        """Self-play training iterations against the current opponent, every episode's result recorded into
+        the local payoff delta on the device (league_experiment_process.py:96-105 via on_episode_end)."""
+        exp, st = self.experiment, self.experiment.stepper
+        B = st.batch_size
+        for _ in range(iterations):
+            exp._train_episode(self.episode)
+            info = st._info
+            self.league.record_runs(self.pid, self.opponent, info[B:3 * B].view(B, 2), info[3 * B:4 * B])
+            self.episode += B
+
+    def run(self, league_iterations: int, iterations_per_match: int, pretrain_iterations: int = 0):
+        self.pretrain_vs_ai(pretrain_iterations)
+        for _ in range(league_iterations):
+            if self.sync() is None:
+                break
+            self.play(iterations_per_match)
+        self.league.sync_payoff()
+        return self.history
+
+
+def league_roles_for(world: int, args) -> list:
+    """Config 3 (2 learners): PFSP self-play between simple players; config 4 (>= 4 ranks): AlphaStar roles
+    (half main players, half main exploiters unless league_main_agents / league_main_exploiters say otherwise)."""
+    if world < 4:
+        return ["simple"] * world
+    return alphastar_roles(world, getattr(args, "league_main_agents", None),
+                           getattr(args, "league_main_exploiters", None),
+                           int(getattr(args, "league_league_exploiters", 0)))

@@ -15,6 +15,23 @@ from ..steppers import SELF_REGISTRY as self_steppers_REGISTRY
 from .ma_experiment import MultiAgentExperiment
 
 
+def agent_vector(mac) -> torch.Tensor:
+    """The MAC's agent parameters as one flat vector (named_parameters order)."""
+    return torch.nn.utils.parameters_to_vector(mac.agent.parameters()).detach()
+
+
+@torch.no_grad()
+def load_agent_vector(mac, vec: torch.Tensor):
+    """In-place copy (keeps a learner's flat-parameter views valid; bumps versions -> weights repacked)."""
+    off = 0
+    for p in mac.agent.parameters():
+        k = p.numel()
+        p.copy_(vec[off:off + k].view_as(p))
+        off += k
+    if off != vec.numel():
+        raise ValueError(f"parameter vector of {vec.numel()} floats for an agent of {off}")
+
+
 class SelfPlayMultiAgentExperiment(MultiAgentExperiment):
     def __init__(self, args, logger, on_episode_end=None, log_start_t=0):
         super().__init__(args, logger, on_episode_end=on_episode_end, log_start_t=log_start_t)
@@ -25,6 +42,10 @@ class SelfPlayMultiAgentExperiment(MultiAgentExperiment):
         """Frozen opponent parameters (a DRQN state_dict), sp_ma_experiment.py:27-29."""
         self.away_mac.load_state_dict(agent=agent)
         del agent
+
+    def load_adversary_vector(self, vec: torch.Tensor):
+        """Opponent parameters as a flat vector (the league's agent pool, exchanged over RCCL)."""
+        load_agent_vector(self.away_mac, vec)
 
     def _integrate_env_info(self):
         total_n_agents = int(self.env_info["n_agents"])

@@ -224,3 +224,31 @@ def test_selfplay_experiment_trains_home_only(device):
     assert any(not torch.equal(v, home0[k]) for k, v in exp.home_mac.agent.state_dict().items()), "home trained"
     h, a = exp.evaluate_mean_returns(episode_n=1)
     assert torch.isfinite(h) and torch.isfinite(a)
+
+
+@pytest.mark.parametrize("mode", ["matchmaking", "rolebased"])
+def test_league_instance_single_rank(device, mode):
+    """A league player on one GPU: pre-training vs the scripted AI, then league iterations against its own
+    snapshots (world 1: the collectives degenerate to local copies); results land in the payoff table."""
+    from maleague.custom_logging import MainLogger
+    from maleague.league import DistributedLeague, LeagueInstance, PayoffEntry
+    from maleague.utils.config import build_config, to_args
+    cfg = build_config("qmix", "ma", overrides=["batch_size_run=64", "runner=parallel", "buffer_cpu_only=False",
+                                                "buffer_size=256", "env_args.episode_limit=30", "t_max=1000000",
+                                                "test_interval=100000000", "league_checkpoint_min_steps=1",
+                                                "league_checkpoint_max_steps=2"])
+    args = to_args(cfg)
+    lg = DistributedLeague(n_players=1, device=device, max_historical=4)
+    inst = LeagueInstance(args, MainLogger(), lg, mode=mode, role=["main"] if mode == "rolebased" else None)
+    hist = inst.run(league_iterations=3, iterations_per_match=2, pretrain_iterations=1)
+    torch.cuda.synchronize()
+    assert len(hist) == 3
+    pay = lg.payoff.tensor.cpu()
+    assert pay[0, :, PayoffEntry.GAMES].sum() == 3 * 2 * 64
+    assert pay[0, :, PayoffEntry.WIN:PayoffEntry.DRAW + 1].sum() == 3 * 2 * 64
+    assert pay[0, :, PayoffEntry.MATCHES].sum() == 3
+    if mode == "rolebased":
+        assert len(lg.historical_meta) >= 1  # checkpoints taken (tiny thresholds)
+        # the away MAC holds the chosen opponent's parameters
+        from maleague.runs.sp_ma_experiment import agent_vector
+        assert torch.equal(agent_vector(inst.experiment.away_mac), lg.params_of(inst.opponent))

@@ -73,3 +73,203 @@ def test_distributed_league_gloo_world2():
     pay = np.array(pay0)
     assert pay[0, 1, 0] == 2 and pay[0, 1, 1] == 2 and pay[1, 0, 0] == 2 and pay[1, 0, 2] == 2
     assert pay[0, 1, 4] == 1 and pay[1, 0, 4] == 1
+
+
+# ---- roles, matchmakers, device-side result recording -------------------------------------------------------
+def _view(n_players, roles, payoff_rows, hist=()):
+    from maleague.league import PayoffWrapper, ROLES, LeagueView
+    from maleague.league.roles import Historical
+    cap = n_players + len(hist)
+    p = torch.zeros(cap, cap, 5)
+    for (i, j), (g, w, l, d) in payoff_rows.items():
+        p[i, j, 0], p[i, j, 1], p[i, j, 2], p[i, j, 3] = g, w, l, d
+    players = [ROLES[r](pid, np.random.RandomState(pid), checkpoint_min_steps=10, checkpoint_max_steps=20)
+               for pid, r in enumerate(roles)]
+    return LeagueView(PayoffWrapper(p), players, [Historical(pid, parent) for pid, parent in hist])
+
+
+def test_remove_monotonic_suffix():
+    from maleague.league import remove_monotonic_suffix
+    wr, pl = remove_monotonic_suffix(np.array([0.2, 0.5, 0.4, 0.6, 0.8]), [5, 6, 7, 8, 9])
+    assert list(wr) == [0.2, 0.5, 0.4, 0.6, 0.8] and pl == [5, 6, 7, 8, 9]
+    wr, pl = remove_monotonic_suffix(np.array([0.9, 0.5, 0.4]), [5, 6, 7])
+    assert len(wr) == 0 and pl == []
+    wr, pl = remove_monotonic_suffix(np.array([0.3, 0.5, 0.4]), [5, 6, 7])
+    assert list(wr) == [0.3, 0.5] and pl == [5, 6]
+
+
+def test_alphastar_roles_and_matches():
+    from maleague.league import alphastar_roles
+    roles = alphastar_roles(8)
+    assert roles == ["main"] * 4 + ["main_exploiter"] * 4
+    # no historical players yet: every branch falls back to a current main player
+    v = _view(8, roles, {})
+    for pid in range(8):
+        for _ in range(20):
+            opp, hist = v.players[pid].get_match(v)
+            assert 0 <= opp < 4 and not hist
+    # main exploiter losing badly to main 0 -> PFSP over main 0's checkpoints
+    hist = [(8, 0), (9, 0), (10, 1)]
+    rows = {(4, m): (10, 0, 10, 0) for m in range(4)}
+    v = _view(8, roles, rows, hist)
+    for _ in range(20):
+        opp, is_hist = v.players[4].get_match(v)
+        assert (opp in (8, 9, 10) and is_hist) or (opp in (2, 3) and not is_hist)
+    # main player: historical checkpoints exist -> the PFSP branch picks among them with prob ~0.5
+    picks = [v.players[0].get_match(v) for _ in range(200)]
+    assert any(h for _, h in picks) and any(not h for _, h in picks)
+    assert all((o >= 8) == h for o, h in picks)
+
+
+def test_checkpoint_readiness():
+    from maleague.league import alphastar_roles
+    roles = alphastar_roles(4)
+    v = _view(4, roles, {(0, 4): (10, 9, 1, 0)}, hist=[(4, 2)])
+    me = v.players[0]
+    me.trained_steps = 5
+    assert not me.ready_to_checkpoint(v)        # < min steps
+    me.trained_steps = 15
+    assert me.ready_to_checkpoint(v)            # beats every checkpoint (0.9 > 0.7)
+    me.checkpoint()
+    v.payoff.tensor[0, 4, 1:3] = torch.tensor([5.0, 5.0])  # win rate 0.5 now
+    me.trained_steps = 30
+    assert not me.ready_to_checkpoint(v)        # 15 since the checkpoint, win rate 0.5 <= 0.7
+    me.trained_steps = 40
+    assert me.ready_to_checkpoint(v)            # > max steps since the last checkpoint
+
+
+def test_matchmakers():
+    from maleague.league import MATCHMAKING_REGISTRY, PayoffEntry
+    v = _view(3, ["simple"] * 3, {})
+    v.payoff.tensor[0, 0, PayoffEntry.MATCHES] = 2
+    v.payoff.tensor[0, 1, PayoffEntry.MATCHES] = 1
+    recorded = []
+    mm = MATCHMAKING_REGISTRY["uniform"](np.random.RandomState(0), record_match=lambda i, j: recorded.append((i, j)))
+    assert mm.get_match(0, v) == 2 and recorded == [(0, 2)]
+    adv = MATCHMAKING_REGISTRY["adversaries"](np.random.RandomState(0))
+    assert adv.get_match(0, v) == 2
+    v.payoff.tensor[0, 2, PayoffEntry.MATCHES] = 1
+    assert adv.get_match(0, v) is None
+    for k in ("pfsp", "fsp", "random"):
+        assert MATCHMAKING_REGISTRY[k](np.random.RandomState(1)).get_match(1, v) in (0, 1, 2)
+
+
+def test_record_runs_matches_episode_result():
+    from maleague.league import DistributedLeague, PayoffEntry, episode_result
+    rng = np.random.RandomState(3)
+    won = torch.from_numpy(rng.randint(0, 2, size=(500, 2)).astype(np.int32))
+    draw = torch.from_numpy(rng.randint(0, 2, size=500).astype(np.int32))
+    lg = DistributedLeague(n_players=2, device="cpu", max_historical=2)
+    lg.record_runs(0, 3, won, draw)
+    pay = lg.sync_payoff()
+    exp = np.zeros(5)
+    for w, d in zip(won.tolist(), draw.tolist()):
+        exp[episode_result({"battle_won": [bool(w[0]), bool(w[1])], "draw": bool(d)})] += 1
+    exp[PayoffEntry.GAMES] = 500
+    np.testing.assert_array_equal(pay[0, 3].numpy(), exp)
+
+
+class _FakeAgent(torch.nn.Module):
+    def __init__(self, rank):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.full((6,), float(rank)))
+        self.trained_steps = 0
+
+
+class _FakeMAC:
+    def __init__(self, rank):
+        self.agent = _FakeAgent(rank)
+
+
+class _FakeStepper:
+    def __init__(self, B):
+        self.batch_size = B
+        self._info = torch.zeros(6 * B, dtype=torch.int32)
+
+
+class _FakeExperiment:
+    """Stands in for LeagueExperiment on CPU: random battle outcomes, trained_steps counting."""
+
+    def __init__(self, rank, B=16):
+        self.home_mac, self.away_mac = _FakeMAC(rank), _FakeMAC(-1)
+        self.stepper = _FakeStepper(B)
+        self.rng = np.random.RandomState(rank)
+        self.adversaries = []
+
+    def load_adversary_vector(self, vec):
+        with torch.no_grad():
+            self.away_mac.agent.w.copy_(vec)
+        self.adversaries.append(vec.clone())
+
+    def _train_episode(self, episode):
+        B = self.stepper.batch_size
+        self.stepper._info[B:3 * B] = torch.from_numpy(self.rng.randint(0, 2, 2 * B).astype(np.int32))
+        self.stepper._info[3 * B:4 * B] = torch.from_numpy(self.rng.randint(0, 2, B).astype(np.int32))
+        self.home_mac.agent.trained_steps += B * 10
+        with torch.no_grad():
+            self.home_mac.agent.w.add_(1.0)
+
+
+def _league_worker(rank, world, port, mode, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from types import SimpleNamespace
+    from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
+    args = SimpleNamespace(matchmaking="pfsp", league_checkpoint_min_steps=300, league_checkpoint_max_steps=600,
+                           env_args={})
+    lg = DistributedLeague(n_players=world, device="cpu", seed=0, max_historical=4 * world)
+    exp = _FakeExperiment(rank)
+    roles = league_roles_for(world, args) if mode == "rolebased" else None
+    inst = LeagueInstance(args, None, lg, mode=mode, role=roles, seed=0, experiment=exp)
+    hist = inst.run(league_iterations=6, iterations_per_match=2)
+    out.put((rank, lg.payoff.tensor.numpy().tolist(), list(lg.historical_meta), hist,
+             [a.tolist() for a in exp.adversaries]))
+    dist.destroy_process_group()
+
+
+def _run_league(world, mode):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_league_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_league_instances_gloo_world2_pfsp():
+    """Config 3 shape: 2 learners, PFSP matchmaking; payoff and agent pool replicated identically."""
+    res = _run_league(2, "matchmaking")
+    pay0 = np.array(res[0][1])
+    for rank, pay, hmeta, hist, advs in res:
+        np.testing.assert_array_equal(np.array(pay), pay0)
+        assert len(hist) == 6
+        for (_, opp, is_hist), adv in zip(hist, advs):
+            assert opp in (0, 1) and not is_hist
+    # every episode of every rank is in the table exactly once: GAMES = ranks x iterations x matches x B
+    assert pay0[:, :, 0].sum() == 2 * 6 * 2 * 16
+    assert pay0[:, :, 4].sum() == 2 * 6
+
+
+def test_league_instances_gloo_world4_alphastar():
+    """Config 4 shape (scaled to 4 ranks): 2 main players + 2 main exploiters, checkpoints into the replicated
+    historical pool, identical on every rank; matches against historical snapshots use their stored params."""
+    res = _run_league(4, "rolebased")
+    pay0, meta0 = np.array(res[0][1]), res[0][2]
+    assert len(meta0) > 0, "checkpoints were taken"
+    assert all(parent in range(4) for _, parent, _ in meta0)
+    for rank, pay, meta, hist, advs in res:
+        np.testing.assert_array_equal(np.array(pay), pay0)
+        assert meta == meta0
+        for (_, opp, is_hist), adv in zip(hist, advs):
+            assert (opp >= 4) == is_hist
+            if rank >= 2:  # exploiters only ever face main players or main players' checkpoints
+                assert opp in (0, 1) or any(h[0] == opp and h[1] in (0, 1) for h in meta0)
