@@ -159,7 +159,7 @@ def main():
     achieved = fl * forwards / avg_kernel_s
     issued = fl / (sides * N) * rows_per_launch / avg_kernel_s if mode == "ai" else None
     traffic = None
-    kernel = "rollout_v2_kernel<64>" if mode == "ai" else "rollout_kernel<64,2,false> (self-play sides)"
+    kernel = "rollout_v2_kernel<64>" if mode == "ai" else "rollout_sp_kernel<64>"
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
             traffic = json.load(f).get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")

@@ -1449,6 +1449,8 @@ __global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel
 // ------------------------------------------------------------------------------------------------
 // Standalone env kernels (one thread per env) -- the EnvWorker command set for host-side TeamsEnv use
 // and for kernel-level parity tests.
+#include "rollout_sp.inc"
+
 __global__ void env_reset_kernel(MlgEnvSpec spec, MlgEnvState st) {
     __shared__ SpecShared SS;
     load_spec_tables(spec, SS);
@@ -1830,5 +1832,19 @@ extern "C" int mlg_rollout_selfplay(const MlgEnvSpec* spec, MlgEnvState* st, con
     sd.eps[1] = test_mode ? 0.f : eps_away;
     sd.ns = 2;
     sd.nh = nh;
+    // self-play kernel (v2 structure, two policies) when the shape allows it, else the generic v1 kernel
+    const char* k = getenv("MLG_ROLLOUT_KERNEL");
+    const RolloutLdsSP lsp = make_rollout_lds_sp(L, spec->U, spec->n_agents);
+    if (!(k && k[0] == 'v' && k[1] == '1') && (L.H == 64 || L.H == 32) && spec->U <= 32 &&
+        lsp.total * 4 <= LDS_LIMIT_BYTES) {
+        const size_t bytes = (size_t)lsp.total * 4;
+        auto kern = L.H == 64 ? rollout_sp_kernel<64> : rollout_sp_kernel<32>;
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return mlg::fail("rollout_selfplay: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
+        hipLaunchKernelGGL(kern, dim3((st->B + RS - 1) / RS), dim3(512), bytes, (hipStream_t)stream, *spec, *st, L,
+                           home_packed, away_packed, *home, *away, *info, sd.eps[0], sd.eps[1], test_mode, lsp);
+        return mlg::check_launch("rollout_sp_kernel");
+    }
     return dispatch_rollout_v1((hipStream_t)stream, *spec, *st, L, sd, *info, test_mode);
 }

@@ -252,3 +252,29 @@ def test_league_instance_single_rank(device, mode):
         # the away MAC holds the chosen opponent's parameters
         from maleague.runs.sp_ma_experiment import agent_vector
         assert torch.equal(agent_vector(inst.experiment.away_mac), lg.params_of(inst.opponent))
+
+
+@pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium"])
+def test_selfplay_kernel_equals_v1(device, plan, monkeypatch):
+    """The compacted two-policy kernel (rollout_sp_kernel) and the generic per-tile kernel (v1) compute in the
+    same arithmetic order: both batches and the run summary must be bit-identical (train mode, epsilon on)."""
+    from maleague.envs.teams_env import VecEnvState
+    stepper, home, away, args = _build(device, plan=plan, B=100, episode_limit=60, seed=3)
+    out = {}
+    for kern in ("v1", "sp"):
+        if kern == "v1":
+            monkeypatch.setenv("MLG_ROLLOUT_KERNEL", "v1")
+        else:
+            monkeypatch.delenv("MLG_ROLLOUT_KERNEL", raising=False)
+        stepper.envs = VecEnvState(stepper.spec, 100, device)
+        stepper.t_env = 30000
+        hb, ab, _ = stepper.run(test_mode=False)
+        last = stepper.last_run
+        out[kern] = ({k: v.clone() for k, v in hb.data.transition_data.items()},
+                     {k: v.clone() for k, v in ab.data.transition_data.items()},
+                     last["ep_len"].clone(), last["returns"].clone(), last["away_returns"].clone())
+    for side in (0, 1):
+        for k in out["v1"][side]:
+            assert torch.equal(out["v1"][side][k], out["sp"][side][k]), (side, k)
+    for i in (2, 3, 4):
+        assert torch.equal(out["v1"][i], out["sp"][i])
