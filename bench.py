@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="auto", choices=["auto", "ai", "league"])
     ap.add_argument("--match-len", type=int, default=5, help="league: training iterations per league iteration")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
+    ap.add_argument("--device", type=int, default=None, help="GPU index for every rank (rehearsal on one GPU)")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--episode-limit", type=int, default=100)
     ap.add_argument("--plan", default="medium_1h_4t")
@@ -57,12 +59,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.device is not None:
+        local_rank = a.device
     mode = a.mode if a.mode != "auto" else ("ai" if world == 1 else "league")
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        else:
+            dist.init_process_group(a.backend)
     dev = torch.device(f"cuda:{local_rank}")
     torch.cuda.set_device(dev)
 
@@ -137,10 +144,11 @@ def main():
     local_env_steps = env_steps
     rows_per_launch = (int(stepper.agent_rows.item()) - rows0) / a.steps
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if a.backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        s = torch.tensor([env_steps], dtype=torch.float64, device=dev)
+        s = torch.tensor([env_steps], dtype=torch.float64, device=rdev)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         env_steps = int(s.item())
     ev_ms = [st.elapsed_time(en) for st, en in stepper.timing]

@@ -62,9 +62,18 @@ class DistributedLeague:
         if not self.payoff.reference_compat:
             self._delta[home, away, PayoffEntry.GAMES] += won.shape[0]
 
+    def _host_staged(self) -> bool:
+        """gloo (CPU tests, single-GPU rehearsals) reduces host tensors; RCCL reduces device tensors in place."""
+        return self.device.type == "cuda" and dist.get_backend() == "gloo"
+
     def sync_payoff(self):
         if self.world > 1:
-            dist.all_reduce(self._delta, op=dist.ReduceOp.SUM)
+            if self._host_staged():
+                d = self._delta.cpu()
+                dist.all_reduce(d, op=dist.ReduceOp.SUM)
+                self._delta.copy_(d)
+            else:
+                dist.all_reduce(self._delta, op=dist.ReduceOp.SUM)
         self.payoff.tensor.add_(self._delta)
         self._delta.zero_()
         return self.payoff.tensor
@@ -75,6 +84,11 @@ class DistributedLeague:
         flat = flat.detach().contiguous()
         if self.world == 1:
             return [flat.clone()]
+        if self._host_staged():
+            host = flat.cpu()
+            out = [torch.empty_like(host) for _ in range(self.world)]
+            dist.all_gather(out, host)
+            return [o.to(flat.device) for o in out]
         out = [torch.empty_like(flat) for _ in range(self.world)]
         dist.all_gather(out, flat)
         return out

@@ -109,7 +109,8 @@ class LeagueInstance:
     def _any(self, flag: bool) -> bool:
         if self.league.world == 1:
             return bool(flag)
-        t = torch.tensor([1.0 if flag else 0.0], device=self.league.device)
+        t = torch.tensor([1.0 if flag else 0.0],
+                         device="cpu" if dist.get_backend() == "gloo" else self.league.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return bool(t.item() > 0)
 
