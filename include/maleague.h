@@ -23,6 +23,7 @@
  *   mlg_select_actions EpsilonGreedyActionSelector.select src/marl/components/action_selectors.py:44-62
  *   mlg_pack_agent     (layout step feeding the above; no reference counterpart)
  *   mlg_qmix_forward   QMixer.forward               src/marl/modules/mixers/qmix.py:41-59
+ *   mlg_refil_*        REFIL (config 5): see the REFIL section below
  *   mlg_qlearner_*     QLearner.train               src/marl/learners/q_learner.py:34-131
  *                      + clip_grad_norm_ + RMSprop.step (q_learner.py:104-105, learner.py:25-31)
  */
@@ -194,6 +195,54 @@ typedef struct {
 int64_t mlg_qlearner_param_counts(const MlgLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);
 int64_t mlg_qlearner_workspace_floats(const MlgLearnerCfg *c);
 int mlg_qlearner_train(const MlgLearnerCfg *c, const MlgLearnerBufs *b, void *stream);
+
+
+/* ---- REFIL (config 5): entity scheme, EntityAttentionRNNAgent, FlexQMixer, REFILLearner ----------------- */
+/* Entity env variant: base.U = 2S units, policy team 0 = units 0..S-1 (= the agents = entities
+ * 0..S-1), scripted team 1 = S..2S-1; per episode k ~ U{min_agents..max_agents} active slots per team. */
+typedef struct {
+    MlgEnvSpec base;
+    int32_t min_agents, max_agents;
+} MlgEntityEnvSpec;
+
+/* Entity-scheme EpisodeBatch, all [B][T1][...] row-major (REFIL scheme: no state / obs). */
+typedef struct {
+    float *entities;       /* [B][T1][NE][ED] */
+    uint8_t *obs_mask;     /* [B][T1][NE][NE]  1 = entity not observable by the row entity */
+    uint8_t *entity_mask;  /* [B][T1][NE]      1 = entity absent (padding) or dead */
+    int64_t *actions;      /* [B][T1][NA][1] */
+    int32_t *avail;        /* [B][T1][NA][A] */
+    float *reward;         /* [B][T1][1] */
+    uint8_t *terminated;   /* [B][T1][1] */
+    float *actions_onehot; /* [B][T1][NA][A] */
+    int64_t *filled;       /* [B][T1][1] */
+    int32_t B, T1, ring_slot0, ring_size, full_write; /* as MlgBatch */
+    const int32_t *rows;   /* sampled view (learner): episode b lives in slot rows[b]; nullptr = identity */
+} MlgEntityBatch;
+
+typedef struct {
+    int32_t n_agents, n_entities, entity_shape, n_actions, entity_last_action;
+    int32_t attn_embed_dim, attn_n_heads, rnn_hidden_dim;
+} MlgRefilDims;
+
+/* Packed EntityAttentionRNNAgent weights from the flat named_parameters() vector: fc1.weight [64][D0], fc1.bias,
+ * attn.in_trans.weight [192][64], attn.out_trans.weight [64][64], attn.out_trans.bias, fc2.weight, fc2.bias,
+ * rnn.weight_ih [192][64], rnn.weight_hh, rnn.bias_ih [192], rnn.bias_hh, fc3.weight [A][64], fc3.bias
+ * (D0 = entity_shape + n_actions with entity_last_action). */
+int64_t mlg_refil_packed_agent_size(const MlgRefilDims *d);
+int mlg_refil_pack_agent(const MlgRefilDims *d, const float *flat, float *packed, void *stream);
+
+/* One EntityAttentionRNNAgent.forward step (ts = 1) over R items: entities [R][NE][D0] (last-action one-hot
+ * included), obs_mask [R][NE][NE], entity_mask [R][NE], h_in [R][NA][64] -> q [R][NA][A], h_out [R][NA][64]. */
+int mlg_refil_agent_forward(const MlgRefilDims *d, const float *packed, const float *entities, const uint8_t *obs_mask,
+                            const uint8_t *entity_mask, const float *h_in, float *q, float *h_out, int32_t R,
+                            void *stream);
+
+/* One ParallelStepper.run over the entity env with EntityMAC acting (entity_controller.py:11-30 with
+ * t -> slice(t, t + 1); entity_rnn_agent.py:32-65; action_selectors.py:44-62). Same run semantics, ring /
+ * full-write modes and run info as mlg_rollout. */
+int mlg_refil_rollout(const MlgEntityEnvSpec *spec, MlgEnvState *st, const MlgRefilDims *d, const float *packed,
+                      MlgEntityBatch *batch, MlgRunInfo *info, float epsilon, int32_t test_mode, void *stream);
 
 /* Diagnostic builds only (-DMLG_STAMPS): device buffer [grid][8 waves][16] u64 of per-phase cycle counts
  * of mlg_rollout. Returns nonzero in normal builds. */

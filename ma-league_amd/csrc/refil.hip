@@ -1,0 +1,564 @@
+// refil.hip -- REFIL (config 5) on gfx950: the entity-scheme rollout and the EntityAttentionRNNAgent forward.
+//
+//   mlg_refil_pack_agent    canonical flat parameters -> kernel layout (refil_device.h RAgent)
+//   mlg_refil_rollout       ParallelStepper.run over the entity env variant with EntityMAC acting
+//                           (src/steppers/parallel_stepper.py:106-216 semantics, EntityMAC._build_inputs
+//                           src/marl/controllers/entity_controller.py:11-30 with t -> slice(t, t + 1),
+//                           EntityAttentionRNNAgent.forward src/marl/modules/agents/entity_rnn_agent.py:32-65,
+//                           EpsilonGreedyActionSelector.select src/marl/components/action_selectors.py:44-62)
+//   mlg_refil_agent_forward one EntityAttentionRNNAgent.forward step (ts = 1) over R items
+//
+// Rollout structure: one wave per workgroup owns two envs for the whole episode. Env lanes 0..31 (lane per unit,
+// half-wave per env) step the env with the unit state in LDS; the agent phase runs per env: entity inputs ->
+// fc1 (MFMA, 16 entity rows) -> in_trans -> attention (lane per head x query), then both envs' 2 x 8 agent rows
+// form one 16-row tile for out_trans -> fc2 -> GRUCell -> fc3 with the hidden state in VGPRs.
+#include "mlg_host.h"
+#include "refil_device.h"
+
+using namespace refil;
+
+namespace {
+
+// ---- packing -----------------------------------------------------------------------------------------
+struct CopyJob {
+    int64_t src, src2, dst;
+    int rows_dst, cols_dst, rows_src, cols_src;
+};
+struct CopyJobs {
+    CopyJob j[16];
+    int n;
+    int64_t total;  // floats of the packed block (everything not covered by a job is zeroed)
+};
+
+__global__ void copy_jobs_kernel(CopyJobs J, const float* __restrict__ src, float* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J.total) return;
+    float v = 0.f;
+    for (int q = 0; q < J.n; ++q) {
+        const CopyJob& c = J.j[q];
+        const int64_t n = (int64_t)c.rows_dst * c.cols_dst;
+        if (i >= c.dst && i < c.dst + n) {
+            const int64_t l = i - c.dst;
+            const int r = (int)(l / c.cols_dst), col = (int)(l % c.cols_dst);
+            if (r < c.rows_src && col < c.cols_src) {
+                v = src[c.src + (int64_t)r * c.cols_src + col];
+                if (c.src2 >= 0) v += src[c.src2 + (int64_t)r * c.cols_src + col];
+            }
+            break;
+        }
+    }
+    dst[i] = v;
+}
+
+CopyJob cj(int64_t src, int64_t dst, int rd, int cd, int rs, int cs, int64_t src2 = -1) {
+    return CopyJob{src, src2, dst, rd, cd, rs, cs};
+}
+
+CopyJobs agent_pack_jobs(const RAgent& L) {
+    CopyJobs J;
+    J.n = 0;
+    J.j[J.n++] = cj(L.c_w1, L.w1, EMB, L.K1, EMB, L.D0);
+    J.j[J.n++] = cj(L.c_b1, L.b1, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_win, L.win, 3 * EMB, EMB, 3 * EMB, EMB);
+    J.j[J.n++] = cj(L.c_wout, L.wout, EMB, EMB, EMB, EMB);
+    J.j[J.n++] = cj(L.c_bout, L.bout, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_w2, L.w2, EMB, EMB, EMB, EMB);
+    J.j[J.n++] = cj(L.c_b2, L.b2, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_wih, L.wih, 3 * EMB, EMB, 3 * EMB, EMB);
+    J.j[J.n++] = cj(L.c_whh, L.whh, 3 * EMB, EMB, 3 * EMB, EMB);
+    J.j[J.n++] = cj(L.c_bih, L.bih, 1, 3 * EMB, 1, 3 * EMB);
+    J.j[J.n++] = cj(L.c_bhh, L.bhh, 1, 3 * EMB, 1, 3 * EMB);
+    J.j[J.n++] = cj(L.c_bih, L.brz, 1, 2 * EMB, 1, 2 * EMB, L.c_bhh);
+    J.j[J.n++] = cj(L.c_w3, L.w3, L.Ap, EMB, L.A, EMB);
+    J.j[J.n++] = cj(L.c_b3, L.b3, 1, L.Ap, 1, L.A);
+    J.total = L.total;
+    return J;
+}
+
+int launch_copy(const CopyJobs& J, const float* src, float* dst, hipStream_t s) {
+    hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((J.total + 255) / 256)), dim3(256), 0, s, J, src, dst);
+    return mlg::check_launch("refil pack");
+}
+
+int check_dims(const MlgRefilDims* d) {
+    MLG_REQUIRE(d != nullptr, "null refil dims");
+    MLG_REQUIRE(d->n_agents >= 1 && d->n_agents <= NAS, "refil: n_agents=%d unsupported (1..8)", d->n_agents);
+    MLG_REQUIRE(d->n_entities >= d->n_agents && d->n_entities <= NE, "refil: n_entities=%d unsupported (n_agents..16)",
+                d->n_entities);
+    MLG_REQUIRE(d->attn_embed_dim == EMB && d->rnn_hidden_dim == EMB && d->attn_n_heads == NH,
+                "refil: attn_embed_dim=%d rnn_hidden_dim=%d attn_n_heads=%d unsupported (64, 64, 4)", d->attn_embed_dim,
+                d->rnn_hidden_dim, d->attn_n_heads);
+    const int D0 = d->entity_shape + (d->entity_last_action ? d->n_actions : 0);
+    MLG_REQUIRE(d->entity_shape >= 1 && D0 <= KMAX, "refil: entity input width %d unsupported (<= %d)", D0, KMAX);
+    MLG_REQUIRE(d->n_actions >= 1 && d->n_actions <= 32, "refil: n_actions=%d unsupported (<= 32)", d->n_actions);
+    return 0;
+}
+
+__host__ inline RAgent agent_layout(const MlgRefilDims* d) {
+    return make_ragent(d->entity_shape + (d->entity_last_action ? d->n_actions : 0), d->n_actions);
+}
+
+// ---- the agent tile (two items x 8 agent rows) ----------------------------------------------------------
+// Entity block of one item: ein (LDS [16][LDI]) -> x1 = relu(fc1) -> qkv = in_trans(x1) -> attention with the
+// item's pre-mask rows -> o rows [obase, obase + nq). The caller syncs before reusing ein/x1/qkv.
+__device__ inline void entity_block(const float* __restrict__ P, const RAgent& L, const float* ein, float* x1, float* qkv,
+                                    const uint32_t* mrow, int nq, int ne, float* o, int lane) {
+    dense_lds<true>(P + L.w1, L.K1, P + L.b1, EMB / 16, ein, LDI, L.K1 / 16, x1, LDX, lane);
+    wave_sync();
+    dense_lds<false>(P + L.win, EMB, nullptr, 3 * EMB / 16, x1, LDX, EMB / 16, qkv, LDQ, lane);
+    wave_sync();
+    attn_fwd(qkv, mrow, nq, ne, o, LDX, nullptr, lane);
+    wave_sync();
+}
+
+// out_trans (+ post mask) -> fc2 -> ReLU -> GRUCell on the 16-row tile; h in/out (D layout).
+// dead: bit r set = tile row r is a masked agent (post_mask, attention.py:75-76).
+__device__ inline void agent_tile_post(const float* __restrict__ P, const RAgent& L, const float* o, uint32_t dead,
+                                       floatx4 (&h)[4], int lane) {
+    const int col = lane & 15;
+    floatx4 x2[4], x3[4];
+    bias_init<4>(x2, P + L.bout, 0, lane);
+    mm_lds<4>(x2, P + L.wout, EMB, 0, o, LDX, EMB / 16, lane);
+    if ((dead >> col) & 1u) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x2[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    bias_init<4>(x3, P + L.b2, 0, lane);
+    mm_reg<4, 4>(x3, P + L.w2, EMB, 0, x2, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x3[i] = relu4(x3[i]);
+    gru_tile(P + L.wih, P + L.whh, P + L.bih, P + L.bhh, P + L.brz, x3, h, lane);
+}
+
+// fc3 action tile `at` of the tile rows (q masked to 0 for dead rows, entity_rnn_agent.py:61)
+__device__ __forceinline__ floatx4 agent_q(const float* __restrict__ P, const RAgent& L, const floatx4 (&h)[4], int at,
+                                           uint32_t dead, int lane) {
+    floatx4 q[1];
+    bias_init<1>(q, P + L.b3, at, lane);
+    mm_reg<1, 4>(q, P + L.w3, EMB, at, h, lane);
+    if ((dead >> (lane & 15)) & 1u) q[0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    return q[0];
+}
+
+// ---- rollout ------------------------------------------------------------------------------------------------
+struct RoLds {
+    float ein[NE * LDI];
+    float x1[NE * LDX];
+    float qkv[NE * LDQ];
+    float o[16 * LDX];
+    float feat[2][NE][8];
+    uint32_t om[2][NE];
+    uint32_t em[2];
+    uint32_t av[2][NAS];
+    int x[2][NE], y[2][NE], hp[2][NE], act[2][NE], nhp[2][NE];
+    int pact[2][NAS];
+    int team[NE], role[NE], melee[NE], agent[NE];
+    int status[2], len[2], slot[2], stepped[2];
+    uint32_t ep[2];
+    float ret[2];
+};
+
+struct RoArgs {
+    int U, NA, A, ED, S, kmin, kmax, B;
+    float inv_p;
+};
+
+__device__ __forceinline__ int64_t ro_slot(const MlgEntityBatch& bt, int b) {
+    return bt.ring_size > 0 ? (int64_t)((bt.ring_slot0 + b) % bt.ring_size) : (int64_t)b;
+}
+
+// pre-transition data of step t for env e (lanes (e, u)); writes batch rows and the LDS copies
+__device__ inline void ro_observe(RoLds& S, const EnvTables& T, const RoArgs& a, const MlgEntityBatch& bt, int e, int u,
+                                  bool active, int t) {
+    const bool me = active && u < a.U;
+    if (me) {
+        const int* x = S.x[e];
+        const int* y = S.y[e];
+        const int* hp = S.hp[e];
+        const int64_t row = (S.slot[e] * (int64_t)bt.T1 + t);
+        float f[8];
+        entity_feat(T, x[u], y[u], hp[u], u, a.inv_p, f);
+        float* eg = bt.entities + (row * a.U + u) * a.ED;
+        for (int k = 0; k < 8; ++k) {
+            S.feat[e][u][k] = f[k];
+            if (k < a.ED) eg[k] = f[k];
+        }
+        uint32_t bits = 0;
+        uint8_t* omg = bt.obs_mask + (row * a.U + u) * a.U;
+        for (int j = 0; j < a.U; ++j) {
+            const int m = hp[u] <= 0 || hp[j] <= 0 || env_dist2(x, y, u, j) > MLG_SIGHT2;
+            bits |= (uint32_t)m << j;
+            omg[j] = (uint8_t)m;
+        }
+        S.om[e][u] = bits;
+        bt.entity_mask[row * a.U + u] = (uint8_t)(hp[u] <= 0);
+        if (u < a.NA) {
+            uint32_t av = 0;
+            int32_t* ag = bt.avail + (row * a.NA + u) * a.A;
+            for (int k = 0; k < a.A; ++k) {
+                const int v = env_avail_one(T, x, y, hp, u, k);
+                av |= (uint32_t)v << k;
+                ag[k] = v;
+            }
+            S.av[e][u] = av;
+        }
+        if (u == 0) bt.filled[row] = 1;
+    }
+    const uint64_t bal = __ballot(me && S.hp[e][u] <= 0);
+    if (active && u == 0) S.em[e] = (uint32_t)((bal >> (16 * e)) & 0xFFFFu);
+}
+
+// zero slots [t0, T1) of every key for env e (full-write ring mode), all 64 lanes
+__device__ inline void ro_zero_tail(const MlgEntityBatch& bt, const RoArgs& a, int64_t slot, int t0, int lane) {
+    if (t0 >= bt.T1) return;
+    const int64_t r0 = slot * bt.T1 + t0, r1 = (slot + 1) * (int64_t)bt.T1;
+    auto zf = [&](float* p, int64_t inner) {
+        for (int64_t i = r0 * inner + lane; i < r1 * inner; i += 64) p[i] = 0.f;
+    };
+    zf(bt.entities, (int64_t)a.U * a.ED);
+    zf(bt.actions_onehot, (int64_t)a.NA * a.A);
+    zf(bt.reward, 1);
+    for (int64_t i = r0 * a.U * a.U + lane; i < r1 * a.U * a.U; i += 64) bt.obs_mask[i] = 0;
+    for (int64_t i = r0 * a.U + lane; i < r1 * a.U; i += 64) bt.entity_mask[i] = 0;
+    for (int64_t i = r0 * a.NA + lane; i < r1 * a.NA; i += 64) bt.actions[i] = 0;
+    for (int64_t i = r0 * a.NA * a.A + lane; i < r1 * a.NA * a.A; i += 64) bt.avail[i] = 0;
+    for (int64_t i = r0 + lane; i < r1; i += 64) {
+        bt.terminated[i] = 0;
+        bt.filled[i] = 0;
+    }
+}
+
+__global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec, MlgEnvState st, RAgent L,
+                                                           const float* __restrict__ P, MlgEntityBatch bt,
+                                                           MlgRunInfo info, RoArgs a, float eps, int test_mode) {
+    __shared__ RoLds S;
+    const int lane = threadIdx.x;
+    const int e = (lane >> 4) & 1, u = lane & 15;
+    const bool env_lane = lane < 32;
+    const int b0 = blockIdx.x * 2;
+    const MlgEnvSpec& sp = spec.base;
+    if (lane < a.U) {
+        S.team[lane] = sp.team[lane];
+        S.role[lane] = sp.role[lane];
+        S.melee[lane] = sp.melee[lane];
+        S.agent[lane] = lane < a.NA ? lane + 1 : 0;
+    }
+    for (int i = lane; i < 16 * LDX; i += 64) S.o[i] = 0.f;
+    for (int i = lane; i < NE * LDI; i += 64) S.ein[i] = 0.f;
+    if (lane < 2) {
+        const int b = b0 + lane;
+        S.status[lane] = b < a.B ? 0 : 2;
+        S.len[lane] = 0;
+        S.ret[lane] = 0.f;
+        S.stepped[lane] = 0;
+        S.slot[lane] = b < a.B ? (int)ro_slot(bt, b) : 0;
+        S.ep[lane] = b < a.B ? st.episode[b] : 0u;
+    }
+    if (lane < 16) S.pact[lane >> 3][lane & 7] = 0;
+    wave_sync();
+    EnvTables T;
+    T.team = S.team;
+    T.role = S.role;
+    T.melee = S.melee;
+    T.agent = S.agent;
+    T.U = a.U;
+    T.grid = sp.grid;
+    T.episode_limit = sp.episode_limit;
+    T.stochastic = sp.stochastic;
+    // ---- reset (EnvWorker "reset", env_worker_process.py:54-60) ----
+    const int b = b0 + e;
+    const bool live = env_lane && b < a.B;
+    if (live && u < a.U) {
+        const uint64_t key = mlg_env_key(sp.seed, b);
+        const uint32_t ep = S.ep[e];
+        const int k = entity_team_k(key, ep, a.kmin, a.kmax);
+        const int tf = S.team[u] ? a.S : 0;
+        int xx, yy, hh;
+        env_spawn_xyh(T, key, ep, u, tf, a.S, xx, yy, hh);
+        if (u - tf >= k) hh = 0;
+        S.x[e][u] = xx;
+        S.y[e][u] = yy;
+        S.hp[e][u] = hh;
+    }
+    wave_sync();
+    ro_observe(S, T, a, bt, e, u, live, 0);
+    wave_sync();
+    floatx4 h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    uint64_t rows = 0;
+    const int col = lane & 15, g = lane >> 4;
+    for (int t = 0;; ++t) {
+        const int st0 = S.status[0], st1 = S.status[1];
+        if (st0 == 2 && st1 == 2) break;
+        // ---- agent phase: EntityMAC.forward(t) + epsilon-greedy for both envs ----
+        for (int ee = 0; ee < 2; ++ee) {
+            if (S.status[ee] == 2) continue;
+            const int D0 = a.ED + a.A;
+            for (int i = lane; i < NE * L.K1; i += 64) {
+                const int j = i / L.K1, c = i % L.K1;
+                float v = 0.f;
+                if (j < a.U) {
+                    if (c < a.ED) v = S.feat[ee][j][c];
+                    else if (c < D0 && j < a.NA && t > 0 && S.pact[ee][j] == c - a.ED) v = 1.f;
+                }
+                S.ein[j * LDI + c] = v;
+            }
+            wave_sync();
+            entity_block(P, L, S.ein, S.x1, S.qkv, S.om[ee], a.NA, a.U, S.o + ee * NAS * LDX, lane);
+            rows += (uint64_t)a.NA;
+        }
+        // tile row r = env (r >> 3), agent (r & 7); dead = agent entity masked
+        uint32_t dead = 0;
+        for (int ee = 0; ee < 2; ++ee) {
+            uint32_t m = S.em[ee] & ((1u << a.NA) - 1u);
+            m |= ~((1u << a.NA) - 1u) & 0xFFu;  // padding rows >= n_agents
+            dead |= (m & 0xFFu) << (8 * ee);
+        }
+        agent_tile_post(P, L, S.o, dead, h, lane);
+        // fc3 + masked argmax + epsilon-greedy
+        const int re = col >> 3, rn = col & 7;
+        const uint32_t avm = (rn < a.NA) ? S.av[re][rn] : 1u;
+        ArgmaxState as{-INFINITY, 1 << 30};
+        for (int at = 0; at < L.Ap / 16; ++at) {
+            const floatx4 q = agent_q(P, L, h, at, dead, lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ac = at * 16 + 4 * g + r;
+                if (ac >= a.A) continue;
+                const float v = ((avm >> ac) & 1u) ? q[r] : -INFINITY;
+                if (amax_better(v, ac, as.bv, as.bi)) { as.bv = v; as.bi = ac; }
+            }
+        }
+        int act = argmax_reduce(as);
+        const int bb = b0 + re;
+        if (g == 0 && rn < a.NA && S.status[re] != 2) {
+            if (!test_mode && eps > 0.f) {
+                const uint64_t key = mlg_env_key(sp.seed, bb);
+                const uint64_t r1 = mlg_rng(key, mlg_ctr(S.ep[re], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)rn));
+                if (mlg_u01(r1) < eps) {
+                    const uint64_t r2 = mlg_rng(key, mlg_ctr(S.ep[re], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)rn));
+                    const int na = __popc(avm);
+                    if (na == 0) {
+                        act = 0;
+                    } else {
+                        const int k = (int)(((r2 >> 40) * (uint64_t)na) >> 24);
+                        uint32_t m = avm;
+                        for (int i = 0; i < k; ++i) m &= m - 1;
+                        act = __ffs((int)m) - 1;
+                    }
+                }
+            }
+            S.pact[re][rn] = act;
+            const int64_t off = ((int64_t)S.slot[re] * bt.T1 + t) * a.NA + rn;
+            bt.actions[off] = act;
+            float* oh = bt.actions_onehot + off * a.A;
+            if (bt.full_write) {
+                for (int k = 0; k < a.A; ++k) oh[k] = k == act ? 1.f : 0.f;
+            } else {
+                oh[act] = 1.f;
+            }
+        }
+        wave_sync();
+        // ---- env phase (EnvWorker "step", env_worker_process.py:32-53) ----
+        const bool stepping = env_lane && S.status[e] == 0;
+        if (stepping && u < a.U) {
+            const int ag = S.agent[u];
+            S.act[e][u] = env_exec_action(T, S.x[e], S.y[e], S.hp[e], u, ag ? (int64_t)S.pact[e][ag - 1] : 0);
+        }
+        wave_sync();
+        if (stepping && u < a.U) S.nhp[e][u] = env_resolve_hp(T, S.act[e], S.hp[e], u);
+        wave_sync();
+        if (stepping && u < a.U && S.hp[e][u] > 0) env_apply_move(S.act[e][u], &S.x[e][u], &S.y[e][u]);
+        if (env_lane && u == 0) {
+            const int stt = S.status[e];
+            S.stepped[e] = 0;
+            const int64_t sl = (int64_t)S.slot[e] * bt.T1 + t;
+            if (stt == 1) {  // final action recorded (parallel_stepper.py:153); env done
+                S.status[e] = 2;
+                if (bt.full_write) {
+                    bt.reward[sl] = 0.f;
+                    bt.terminated[sl] = 0;
+                }
+            } else if (stt == 0) {
+                int alive[2] = {0, 0}, lost[2] = {0, 0}, kills[2] = {0, 0};
+                for (int j = 0; j < a.U; ++j) {
+                    const int tm = S.team[j];
+                    const int h0 = S.hp[e][j], h1 = S.nhp[e][j];
+                    if (h0 > 0) {
+                        lost[tm] += h0 - h1 > 0 ? h0 - h1 : 0;
+                        if (h1 == 0) kills[1 - tm] += 1;
+                    }
+                    if (h1 > 0) alive[tm] += 1;
+                }
+                const int done = alive[0] == 0 || alive[1] == 0 || t + 1 >= sp.episode_limit;
+                const int w0 = alive[1] == 0 && alive[0] > 0, w1 = alive[0] == 0 && alive[1] > 0;
+                const float r = (float)(lost[1] + 10 * kills[0] + 200 * w0) * 0.0625f;  // policy team 0
+                bt.reward[sl] = r;
+                bt.terminated[sl] = (uint8_t)done;
+                S.ret[e] += r;
+                S.stepped[e] = 1;
+                if (done) {
+                    S.status[e] = 1;
+                    S.len[e] = t + 1;
+                    const int bb2 = b0 + e;
+                    info.won[2 * bb2] = w0;
+                    info.won[2 * bb2 + 1] = w1;
+                    info.draw[bb2] = !w0 && !w1;
+                }
+            }
+        }
+        wave_sync();
+        const bool stepped = env_lane && S.stepped[e];
+        if (stepped && u < a.U) S.hp[e][u] = S.nhp[e][u];
+        wave_sync();
+        ro_observe(S, T, a, bt, e, u, stepped, t + 1);
+        wave_sync();
+    }
+    // ---- finish: run summary, env state, full-write tails ----
+    if (live && u == 0) {
+        info.ep_len[b] = S.len[e];
+        info.ret[b] = S.ret[e];
+        st.t[b] = S.len[e];
+        st.episode[b] = S.ep[e] + 1u;
+    }
+    if (live && u < a.U) {
+        st.x[(int64_t)b * a.U + u] = S.x[e][u];
+        st.y[(int64_t)b * a.U + u] = S.y[e][u];
+        st.hp[(int64_t)b * a.U + u] = S.hp[e][u];
+    }
+    if (bt.full_write) {
+        for (int ee = 0; ee < 2; ++ee)
+            if (b0 + ee < a.B) ro_zero_tail(bt, a, S.slot[ee], S.len[ee] + 1, lane);
+    }
+    if (info.agent_rows && lane == 0) atomicAdd((unsigned long long*)info.agent_rows, (unsigned long long)rows);
+}
+
+// ---- one EntityAttentionRNNAgent step over R items (two items per wave) -------------------------------
+__global__ void __launch_bounds__(64) refil_agent_step_kernel(RAgent L, const float* __restrict__ P, int R, int NA,
+                                                              int NEa, int D0, int A, const float* __restrict__ ent,
+                                                              const uint8_t* __restrict__ om,
+                                                              const uint8_t* __restrict__ em,
+                                                              const float* __restrict__ h_in, float* __restrict__ q_out,
+                                                              float* __restrict__ h_out) {
+    __shared__ float ein[NE * LDI];
+    __shared__ float x1[NE * LDX];
+    __shared__ float qkv[NE * LDQ];
+    __shared__ float o[16 * LDX];
+    __shared__ uint32_t mrow[2][NE];
+    __shared__ uint32_t emb[2];
+    const int lane = threadIdx.x;
+    const int i0 = blockIdx.x * 2;
+    for (int i = lane; i < 16 * LDX; i += 64) o[i] = 0.f;
+    if (lane < 32) {
+        const int e = lane >> 4, q = lane & 15;
+        const int it = i0 + e;
+        uint32_t bits = 0xFFFFFFFFu;
+        if (it < R && q < NEa) {
+            bits = 0;
+            for (int j = 0; j < NEa; ++j) bits |= (uint32_t)(om[((int64_t)it * NEa + q) * NEa + j] != 0) << j;
+        }
+        mrow[e][q] = bits;
+        if (q == 0) {
+            uint32_t m = 0xFFFFFFFFu;
+            if (it < R) {
+                m = 0;
+                for (int j = 0; j < NEa; ++j) m |= (uint32_t)(em[(int64_t)it * NEa + j] != 0) << j;
+                m |= ~((1u << NEa) - 1u);
+            }
+            emb[e] = m;
+        }
+    }
+    wave_sync();
+    for (int e = 0; e < 2; ++e) {
+        const int it = i0 + e;
+        for (int i = lane; i < NE * L.K1; i += 64) {
+            const int j = i / L.K1, c = i % L.K1;
+            ein[j * LDI + c] = (it < R && j < NEa && c < D0) ? ent[((int64_t)it * NEa + j) * D0 + c] : 0.f;
+        }
+        wave_sync();
+        entity_block(P, L, ein, x1, qkv, mrow[e], NA, NEa, o + e * NAS * LDX, lane);
+    }
+    const int col = lane & 15, g = lane >> 4;
+    const int e = col >> 3, n = col & 7, it = i0 + e;
+    const bool valid = it < R && n < NA;
+    uint32_t dead = 0;
+    for (int ee = 0; ee < 2; ++ee) dead |= ((emb[ee] | ~((1u << NA) - 1u)) & 0xFFu) << (8 * ee);
+    floatx4 h[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+        h[mt] = valid ? ld4(h_in + ((int64_t)it * NA + n) * EMB + mt * 16 + 4 * g) : floatx4{0.f, 0.f, 0.f, 0.f};
+    agent_tile_post(P, L, o, dead, h, lane);
+    if (valid) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) *reinterpret_cast<floatx4*>(h_out + ((int64_t)it * NA + n) * EMB + mt * 16 + 4 * g) = h[mt];
+    }
+    for (int at = 0; at < L.Ap / 16; ++at) {
+        const floatx4 q = agent_q(P, L, h, at, dead, lane);
+        if (valid) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ac = at * 16 + 4 * g + r;
+                if (ac < A) q_out[((int64_t)it * NA + n) * A + ac] = q[r];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int64_t mlg_refil_packed_agent_size(const MlgRefilDims* d) {
+    if (check_dims(d)) return -1;
+    return agent_layout(d).total;
+}
+
+extern "C" int mlg_refil_pack_agent(const MlgRefilDims* d, const float* flat, float* packed, void* stream) {
+    if (check_dims(d)) return 1;
+    MLG_REQUIRE(flat && packed, "refil_pack_agent: null pointer");
+    return launch_copy(agent_pack_jobs(agent_layout(d)), flat, packed, (hipStream_t)stream);
+}
+
+extern "C" int mlg_refil_agent_forward(const MlgRefilDims* d, const float* packed, const float* entities,
+                                       const uint8_t* obs_mask, const uint8_t* entity_mask, const float* h_in, float* q,
+                                       float* h_out, int32_t R, void* stream) {
+    if (check_dims(d)) return 1;
+    MLG_REQUIRE(packed && entities && obs_mask && entity_mask && h_in && q && h_out, "refil_agent_forward: null pointer");
+    MLG_REQUIRE(R >= 0, "refil_agent_forward: R=%d", R);
+    if (R == 0) return 0;
+    const RAgent L = agent_layout(d);
+    hipLaunchKernelGGL(refil_agent_step_kernel, dim3((unsigned)((R + 1) / 2)), dim3(64), 0, (hipStream_t)stream, L, packed,
+                       R, d->n_agents, d->n_entities, L.D0, d->n_actions, entities, obs_mask, entity_mask, h_in, q, h_out);
+    return mlg::check_launch("refil_agent_forward");
+}
+
+extern "C" int mlg_refil_rollout(const MlgEntityEnvSpec* spec, MlgEnvState* st, const MlgRefilDims* d,
+                                 const float* packed, MlgEntityBatch* batch, MlgRunInfo* info, float epsilon,
+                                 int32_t test_mode, void* stream) {
+    if (check_dims(d)) return 1;
+    MLG_REQUIRE(spec && st && packed && batch && info, "refil_rollout: null argument");
+    const MlgEnvSpec& sp = spec->base;
+    const int S = sp.U / 2;
+    MLG_REQUIRE(sp.U % 2 == 0 && sp.U <= NE && S <= NAS, "refil_rollout: U=%d unsupported (even, <= 16)", sp.U);
+    MLG_REQUIRE(sp.n_agents == S && d->n_agents == S && d->n_entities == sp.U && d->entity_shape == 8 &&
+                    d->n_actions == MLG_ACT_BASE + sp.U && d->entity_last_action,
+                "refil_rollout: dims (n_agents=%d n_entities=%d entity_shape=%d n_actions=%d) do not match the env "
+                "(S=%d, U=%d)", d->n_agents, d->n_entities, d->entity_shape, d->n_actions, S, sp.U);
+    MLG_REQUIRE(spec->min_agents >= 1 && spec->min_agents <= spec->max_agents && spec->max_agents <= S,
+                "refil_rollout: min_agents=%d max_agents=%d (slots %d)", spec->min_agents, spec->max_agents, S);
+    MLG_REQUIRE(sp.policy_team == 0 && sp.scripted[0] == 0 && sp.scripted[1] == 1,
+                "refil_rollout: the entity env has policy team 0 and scripted team 1");
+    const MlgEntityBatch& bt = *batch;
+    MLG_REQUIRE(bt.entities && bt.obs_mask && bt.entity_mask && bt.actions && bt.avail && bt.reward && bt.terminated &&
+                    bt.actions_onehot && bt.filled, "refil_rollout: batch has null tensors");
+    MLG_REQUIRE(st->B == bt.B && bt.T1 >= sp.episode_limit + 1, "refil_rollout: B=%d/%d T1=%d (episode_limit %d)", st->B,
+                bt.B, bt.T1, sp.episode_limit);
+    MLG_REQUIRE(info->ep_len && info->ret && info->won && info->draw, "refil_rollout: run info has null buffers");
+    if (bt.B == 0) return 0;
+    int p = 1;
+    while (p < sp.grid) p <<= 1;
+    RoArgs a{sp.U, S, d->n_actions, d->entity_shape, S, spec->min_agents, spec->max_agents, bt.B, 1.0f / (float)p};
+    const RAgent L = agent_layout(d);
+    hipLaunchKernelGGL(refil_rollout_kernel, dim3((unsigned)((bt.B + 1) / 2)), dim3(64), 0, (hipStream_t)stream, *spec, *st,
+                       L, packed, bt, *info, a, test_mode ? 0.f : epsilon, test_mode);
+    return mlg::check_launch("refil_rollout");
+}

@@ -1,0 +1,425 @@
+// refil_device.h -- REFIL (config 5) building blocks for gfx950, shared by the rollout and the learner:
+//
+//   * wave-level f32 MFMA (16x16x4) GEMMs over one 16-row tile: rows = entities (fc1, in_trans) or
+//     agent rows of two items (out_trans, fc2, GRU, fc3); weights [M][K] row-major from HBM/L2, activations
+//     from LDS (row-major) or from registers (the D layout of the previous GEMM, see mlg_device.h)
+//   * EntityAttentionLayer forward / backward for one item (src/marl/modules/layers/attention.py:24-79):
+//     lane = (head, query), 4 heads x 16 query slots, keys in LDS; -inf pre-mask, softmax, NaN rows -> 0
+//   * the entity env variant (oracle/env_ref.c envref_reset_entity / envref_entities)
+//
+// Sizes fixed by the kernels (host-checked): n_entities <= 16 (one MFMA tile), n_agents <= 8 (two items per
+// agent-row tile), attn_embed_dim = rnn_hidden_dim = hypernet_embed = 64, attn_n_heads = 4 (head_dim 16),
+// mixing_embed_dim = 32, entity input dim ED + A <= 48.
+#pragma once
+#include "agent_device.h"
+
+namespace refil {
+
+constexpr int NE = 16;            // entity slots per item
+constexpr int NAS = 8;            // agent-row slots per item
+constexpr int EMB = 64;           // attention / hidden width
+constexpr int NH = 4, HD = 16;    // heads, head dim
+constexpr int EM = 32;            // mixing_embed_dim
+constexpr int LDX = EMB + 4;      // LDS row stride of 64-wide activations (conflict-free 16-row reads)
+constexpr int LDQ = 3 * EMB + 4;  // qkv rows
+constexpr int KMAX = 48;          // entity input width, padded
+constexpr int LDI = KMAX + 4;
+
+// wave-local barrier: orders the LDS writes of some lanes before the reads of others (single wave)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- packed weight blocks ---------------------------------------------------------------------------
+// Agent (EntityAttentionRNNAgent, entity_rnn_agent.py:9-26): K1 = entity input width padded to 16.
+//   w1 [64][K1], b1 [64], win [192][64], wout [64][64], bout [64], w2 [64][64], b2 [64],
+//   wih [192][64], whh [192][64], bih [192], bhh [192], brz [128] (= b_ih + b_hh of r, z), w3 [Ap][64], b3 [Ap]
+// Canonical flat order (named_parameters): fc1.w [64][D0], fc1.b, attn.in_trans.w [192][64], attn.out_trans.w,
+//   attn.out_trans.b, fc2.w, fc2.b, rnn.weight_ih, rnn.weight_hh, rnn.bias_ih, rnn.bias_hh, fc3.w [A][64], fc3.b [A]
+struct RAgent {
+    int D0, K1, A, Ap;
+    int64_t w1, b1, win, wout, bout, w2, b2, wih, whh, bih, bhh, brz, w3, b3, total;
+    // canonical offsets
+    int64_t c_w1, c_b1, c_win, c_wout, c_bout, c_w2, c_b2, c_wih, c_whh, c_bih, c_bhh, c_w3, c_b3, c_total;
+};
+
+__host__ __device__ inline RAgent make_ragent(int D0, int A) {
+    RAgent L;
+    L.D0 = D0;
+    L.K1 = (D0 + 15) / 16 * 16;
+    L.A = A;
+    L.Ap = (A + 15) / 16 * 16;
+    int64_t o = 0;
+    auto take = [&](int64_t n) { int64_t r = o; o += mlg_align4(n); return r; };
+    L.w1 = take((int64_t)EMB * L.K1);
+    L.b1 = take(EMB);
+    L.win = take(3 * EMB * EMB);
+    L.wout = take(EMB * EMB);
+    L.bout = take(EMB);
+    L.w2 = take(EMB * EMB);
+    L.b2 = take(EMB);
+    L.wih = take(3 * EMB * EMB);
+    L.whh = take(3 * EMB * EMB);
+    L.bih = take(3 * EMB);
+    L.bhh = take(3 * EMB);
+    L.brz = take(2 * EMB);
+    L.w3 = take((int64_t)L.Ap * EMB);
+    L.b3 = take(L.Ap);
+    L.total = o;
+    int64_t c = 0;
+    L.c_w1 = c; c += (int64_t)EMB * D0;
+    L.c_b1 = c; c += EMB;
+    L.c_win = c; c += 3 * EMB * EMB;
+    L.c_wout = c; c += EMB * EMB;
+    L.c_bout = c; c += EMB;
+    L.c_w2 = c; c += EMB * EMB;
+    L.c_b2 = c; c += EMB;
+    L.c_wih = c; c += 3 * EMB * EMB;
+    L.c_whh = c; c += 3 * EMB * EMB;
+    L.c_bih = c; c += 3 * EMB;
+    L.c_bhh = c; c += 3 * EMB;
+    L.c_w3 = c; c += (int64_t)A * EMB;
+    L.c_b3 = c; c += A;
+    L.c_total = c;
+    return L;
+}
+
+// Attention hypernet (AttentionHyperNet, flex_qmix.py:5-53) with mixing_embed_dim outputs:
+//   w1 [64][K1], b1 [64], win [192][64], wout [64][64], bout [64], w2 [32][64], b2 [32]
+// canonical (named_parameters): fc1.w [64][D0], fc1.b, attn.in_trans.w, attn.out_trans.w, attn.out_trans.b,
+//   fc2.w [32][64], fc2.b [32].  FlexQMixer = hyper_w_1, hyper_w_final, hyper_b_1, V (flex_qmix.py:61-66).
+struct RHyper {
+    int D0, K1;
+    int64_t w1, b1, win, wout, bout, w2, b2, total;
+    int64_t c_w1, c_b1, c_win, c_wout, c_bout, c_w2, c_b2, c_total;
+};
+
+__host__ __device__ inline RHyper make_rhyper(int D0) {
+    RHyper L;
+    L.D0 = D0;
+    L.K1 = (D0 + 15) / 16 * 16;
+    int64_t o = 0;
+    auto take = [&](int64_t n) { int64_t r = o; o += mlg_align4(n); return r; };
+    L.w1 = take((int64_t)EMB * L.K1);
+    L.b1 = take(EMB);
+    L.win = take(3 * EMB * EMB);
+    L.wout = take(EMB * EMB);
+    L.bout = take(EMB);
+    L.w2 = take(EM * EMB);
+    L.b2 = take(EM);
+    L.total = o;
+    int64_t c = 0;
+    L.c_w1 = c; c += (int64_t)EMB * D0;
+    L.c_b1 = c; c += EMB;
+    L.c_win = c; c += 3 * EMB * EMB;
+    L.c_wout = c; c += EMB * EMB;
+    L.c_bout = c; c += EMB;
+    L.c_w2 = c; c += EM * EMB;
+    L.c_b2 = c; c += EM;
+    L.c_total = c;
+    return L;
+}
+
+// ---- wave GEMM helpers ---------------------------------------------------------------------------------
+// acc[i] (D layout: lane (col, g), reg r = output feature (mt0 + i) * 16 + 4g + r of tile row col)
+//   += W[(mt0 + i) * 16 + col][k] * X[col][k]   over k < 16 * kchunks
+template <int MT>
+__device__ __forceinline__ void bias_init(floatx4 (&acc)[MT], const float* bias, int mt0, int lane) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[i] = bias ? ld4(bias + (mt0 + i) * 16 + 4 * g) : floatx4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <int MT>
+__device__ __forceinline__ void mm_lds(floatx4 (&acc)[MT], const float* __restrict__ W, int ldw, int mt0, const float* X,
+                                       int ldx, int kchunks, int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    const float* xr = X + col * ldx + 4 * g;
+    const float* wr = W + (int64_t)(mt0 * 16 + col) * ldw + 4 * g;
+    for (int kc = 0; kc < kchunks; ++kc) {
+        const floatx4 xv = ld4(xr + kc * 16);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i] = mfma_chunk(ld4(wr + (int64_t)i * 16 * ldw + kc * 16), xv, acc[i]);
+    }
+}
+
+template <int MT, int KC>
+__device__ __forceinline__ void mm_reg(floatx4 (&acc)[MT], const float* __restrict__ W, int ldw, int mt0,
+                                       const floatx4 (&x)[KC], int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    const float* wr = W + (int64_t)(mt0 * 16 + col) * ldw + 4 * g;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i] = mfma_chunk(ld4(wr + (int64_t)i * 16 * ldw + kc * 16), x[kc], acc[i]);
+}
+
+__device__ __forceinline__ void st_row(float* Y, int ldy, int mt, const floatx4 v, int lane) {
+    *reinterpret_cast<floatx4*>(Y + (lane & 15) * ldy + mt * 16 + 4 * (lane >> 4)) = v;
+}
+
+__device__ __forceinline__ floatx4 relu4(floatx4 v) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    return v;
+}
+
+// Y[16][64 * G] rows of LDS = act(bias + W X) for 4*G output tiles (G groups of 4 tiles)
+template <bool RELU>
+__device__ __forceinline__ void dense_lds(const float* __restrict__ W, int ldw, const float* bias, int mtiles,
+                                          const float* X, int ldx, int kchunks, float* Y, int ldy, int lane) {
+    for (int m0 = 0; m0 < mtiles; m0 += 4) {
+        floatx4 acc[4];
+        bias_init<4>(acc, bias, m0, lane);
+        mm_lds<4>(acc, W, ldw, m0, X, ldx, kchunks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st_row(Y, ldy, m0 + i, RELU ? relu4(acc[i]) : acc[i], lane);
+    }
+}
+
+// ---- EntityAttentionLayer core for one item ---------------------------------------------------------
+// qkv: LDS [NE][LDQ] (query cols 0..63, key 64..127, value 128..191; chunk(3) of in_trans, attention.py:33);
+// mrow[q]: pre-mask bits of query row q (bit j = entity j masked); nq <= 16 queries; keys k >= ne are masked.
+// Lane (h = lane >> 4, q = lane & 15). Output o row q (cols h*16..) in LDS; P[h][q][k] saved when non-null
+// (global or LDS, row stride 16). Rows with every key masked: softmax NaN -> 0 (attention.py:59).
+__device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, int ne, float* o, int ldo, float* P,
+                                int lane) {
+    const int h = lane >> 4, q = lane & 15;
+    if (q >= nq) return;
+    float qv[HD];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const floatx4 v = ld4(qkv + q * LDQ + h * HD + 4 * c);
+        qv[4 * c] = v[0]; qv[4 * c + 1] = v[1]; qv[4 * c + 2] = v[2]; qv[4 * c + 3] = v[3];
+    }
+    const uint32_t m = mrow[q] | (ne < 32 ? (~0u << ne) : 0u);
+    float s[NE];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const float* kr = qkv + k * LDQ + EMB + h * HD;
+        float d = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const floatx4 kv = ld4(kr + 4 * c);
+            d = fmaf(qv[4 * c], kv[0], d);
+            d = fmaf(qv[4 * c + 1], kv[1], d);
+            d = fmaf(qv[4 * c + 2], kv[2], d);
+            d = fmaf(qv[4 * c + 3], kv[3], d);
+        }
+        s[k] = ((m >> k) & 1u) ? -INFINITY : d * 0.25f;  // / sqrt(head_dim) = / 4 (exact)
+        mx = fmaxf(mx, s[k]);
+    }
+    float ov[HD];
+#pragma unroll
+    for (int d = 0; d < HD; ++d) ov[d] = 0.f;
+    if (mx != -INFINITY) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            s[k] = ((m >> k) & 1u) ? 0.f : expf(s[k] - mx);
+            sum += s[k];
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) s[k] = s[k] / sum;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            const float* vr = qkv + k * LDQ + 2 * EMB + h * HD;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const floatx4 vv = ld4(vr + 4 * c);
+                ov[4 * c] = fmaf(s[k], vv[0], ov[4 * c]);
+                ov[4 * c + 1] = fmaf(s[k], vv[1], ov[4 * c + 1]);
+                ov[4 * c + 2] = fmaf(s[k], vv[2], ov[4 * c + 2]);
+                ov[4 * c + 3] = fmaf(s[k], vv[3], ov[4 * c + 3]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NE; ++k) s[k] = 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        *reinterpret_cast<floatx4*>(o + q * ldo + h * HD + 4 * c) = floatx4{ov[4 * c], ov[4 * c + 1], ov[4 * c + 2], ov[4 * c + 3]};
+    if (P) {
+        float* pr = P + (h * 16 + q) * NE;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            *reinterpret_cast<floatx4*>(pr + 4 * c) = floatx4{s[4 * c], s[4 * c + 1], s[4 * c + 2], s[4 * c + 3]};
+    }
+}
+
+// Backward of attn_fwd for one item. P: [NH][16][16] saved weights; dO: rows q < nq (cols h*16..);
+// DS: LDS scratch [NH][16][16]; dqkv: LDS [NE][LDQ], written (ACC = false) or accumulated (ACC = true):
+// dQ rows < nq (rows >= nq get 0 when writing), dK / dV all 16 rows.
+//   dP = dO V^T, dS = P (dP - sum_k P dP) / 4, dQ = dS K, dK = dS^T Q, dV = P^T dO
+// (masked keys and fully masked rows have P = 0 -> dS = 0, matching the masked_fill backward)
+template <bool ACC>
+__device__ inline void attn_bwd(const float* qkv, const float* P, int nq, const float* dO, int ldo, float* DS, float* dqkv,
+                                int lane) {
+    const int h = lane >> 4, q = lane & 15;
+    {
+        float dq[HD];
+#pragma unroll
+        for (int d = 0; d < HD; ++d) dq[d] = 0.f;
+        float ds[NE];
+        if (q < nq) {
+            float dov[HD];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const floatx4 v = ld4(dO + q * ldo + h * HD + 4 * c);
+                dov[4 * c] = v[0]; dov[4 * c + 1] = v[1]; dov[4 * c + 2] = v[2]; dov[4 * c + 3] = v[3];
+            }
+            const float* pr = P + (h * 16 + q) * NE;
+            float sdp = 0.f;
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                const float* vr = qkv + k * LDQ + 2 * EMB + h * HD;
+                float d = 0.f;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const floatx4 vv = ld4(vr + 4 * c);
+                    d = fmaf(dov[4 * c], vv[0], d);
+                    d = fmaf(dov[4 * c + 1], vv[1], d);
+                    d = fmaf(dov[4 * c + 2], vv[2], d);
+                    d = fmaf(dov[4 * c + 3], vv[3], d);
+                }
+                ds[k] = d;
+                sdp = fmaf(pr[k], d, sdp);
+            }
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                const float p = pr[k];
+                ds[k] = p * (ds[k] - sdp) * 0.25f;
+                const float* kr = qkv + k * LDQ + EMB + h * HD;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const floatx4 kv = ld4(kr + 4 * c);
+                    dq[4 * c] = fmaf(ds[k], kv[0], dq[4 * c]);
+                    dq[4 * c + 1] = fmaf(ds[k], kv[1], dq[4 * c + 1]);
+                    dq[4 * c + 2] = fmaf(ds[k], kv[2], dq[4 * c + 2]);
+                    dq[4 * c + 3] = fmaf(ds[k], kv[3], dq[4 * c + 3]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NE; ++k) ds[k] = 0.f;
+        }
+        float* dsr = DS + (h * 16 + q) * NE;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            *reinterpret_cast<floatx4*>(dsr + 4 * c) = floatx4{ds[4 * c], ds[4 * c + 1], ds[4 * c + 2], ds[4 * c + 3]};
+        float* dqr = dqkv + q * LDQ + h * HD;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            floatx4 v{dq[4 * c], dq[4 * c + 1], dq[4 * c + 2], dq[4 * c + 3]};
+            if (ACC) v += ld4(dqr + 4 * c);
+            *reinterpret_cast<floatx4*>(dqr + 4 * c) = v;
+        }
+    }
+    wave_sync();
+    {
+        const int k = q;  // lane (h, key k)
+        float dk[HD], dv[HD];
+#pragma unroll
+        for (int d = 0; d < HD; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+        for (int qq = 0; qq < nq; ++qq) {
+            const float dsv = DS[(h * 16 + qq) * NE + k];
+            const float pv = P[(h * 16 + qq) * NE + k];
+            const float* qr = qkv + qq * LDQ + h * HD;
+            const float* dor = dO + qq * ldo + h * HD;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const floatx4 qv = ld4(qr + 4 * c);
+                const floatx4 ov = ld4(dor + 4 * c);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    dk[4 * c + r] = fmaf(dsv, qv[r], dk[4 * c + r]);
+                    dv[4 * c + r] = fmaf(pv, ov[r], dv[4 * c + r]);
+                }
+            }
+        }
+        float* kr = dqkv + k * LDQ + EMB + h * HD;
+        float* vr = dqkv + k * LDQ + 2 * EMB + h * HD;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            floatx4 a{dk[4 * c], dk[4 * c + 1], dk[4 * c + 2], dk[4 * c + 3]};
+            floatx4 b{dv[4 * c], dv[4 * c + 1], dv[4 * c + 2], dv[4 * c + 3]};
+            if (ACC) {
+                a += ld4(kr + 4 * c);
+                b += ld4(vr + 4 * c);
+            }
+            *reinterpret_cast<floatx4*>(kr + 4 * c) = a;
+            *reinterpret_cast<floatx4*>(vr + 4 * c) = b;
+        }
+    }
+}
+
+// ---- GRUCell on one 16-row tile, x and h in registers (D layout), PyTorch gate order r, z, n ------------
+// brz = b_ih + b_hh for r, z (pre-summed). h updated in place; optional gate outputs for the backward.
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+__device__ inline void gru_tile(const float* __restrict__ wih, const float* __restrict__ whh, const float* __restrict__ bih,
+                                const float* __restrict__ bhh, const float* __restrict__ brz, const floatx4 (&x)[4],
+                                floatx4 (&h)[4], int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    floatx4 hn[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        floatx4 ar = ld4(brz + mt * 16 + 4 * g);
+        floatx4 az = ld4(brz + EMB + mt * 16 + 4 * g);
+        floatx4 ain = ld4(bih + 2 * EMB + mt * 16 + 4 * g);
+        floatx4 ahn = ld4(bhh + 2 * EMB + mt * 16 + 4 * g);
+        const float* wi = wih + (int64_t)(mt * 16 + col) * EMB + 4 * g;
+        const float* wh = whh + (int64_t)(mt * 16 + col) * EMB + 4 * g;
+        constexpr int64_t GATE = (int64_t)EMB * EMB;
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            ar = mfma_chunk(ld4(wi + kc * 16), x[kc], ar);
+            az = mfma_chunk(ld4(wi + GATE + kc * 16), x[kc], az);
+            ain = mfma_chunk(ld4(wi + 2 * GATE + kc * 16), x[kc], ain);
+            ar = mfma_chunk(ld4(wh + kc * 16), h[kc], ar);
+            az = mfma_chunk(ld4(wh + GATE + kc * 16), h[kc], az);
+            ahn = mfma_chunk(ld4(wh + 2 * GATE + kc * 16), h[kc], ahn);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float rg = sigm(ar[r]);
+            const float zg = sigm(az[r]);
+            const float ng = tanhf(ain[r] + rg * ahn[r]);
+            hn[mt][r] = ng + zg * (h[mt][r] - ng);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) h[mt] = hn[mt];
+}
+
+// ---- entity env variant (oracle/env_ref.c envref_reset_entity / envref_entities) ------------------------
+enum { MLG_PURPOSE_TEAM = 4 };
+
+__device__ __forceinline__ int entity_team_k(uint64_t key, uint32_t episode, int kmin, int kmax) {
+    const uint64_t r = mlg_rng(key, mlg_ctr(episode, 0, MLG_PURPOSE_TEAM, 0));
+    return kmin + (int)(r % (uint64_t)(kmax - kmin + 1));
+}
+
+// entity features of unit j: [1, x/P, y/P, hp/max_hp, team, role/2, melee, power/8] if alive, else zeros
+__device__ __forceinline__ void entity_feat(const EnvTables& T, int x, int y, int hp, int j, float inv_p, float* o) {
+    if (hp <= 0) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) o[f] = 0.f;
+        return;
+    }
+    o[0] = 1.f;
+    o[1] = (float)x * inv_p;
+    o[2] = (float)y * inv_p;
+    o[3] = (float)hp * inv_maxhp(T.role[j]);
+    o[4] = (float)T.team[j];
+    o[5] = (float)T.role[j] * 0.5f;
+    o[6] = (float)T.melee[j];
+    o[7] = (float)role_power(T.role[j]) * 0.125f;
+}
+
+}  // namespace refil

@@ -74,6 +74,23 @@ class MlgLearnerBufs(ctypes.Structure):
                                                                       "target_params", "workspace", "stats"]]
 
 
+class MlgEntityEnvSpec(ctypes.Structure):
+    _fields_ = [("base", MlgEnvSpec), ("min_agents", ctypes.c_int32), ("max_agents", ctypes.c_int32)]
+
+
+class MlgEntityBatch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ["entities", "obs_mask", "entity_mask", "actions", "avail", "reward",
+                                              "terminated", "actions_onehot", "filled"]] + \
+               [(n, ctypes.c_int32) for n in ["B", "T1", "ring_slot0", "ring_size", "full_write"]] + \
+               [("rows", ctypes.c_void_p)]
+
+
+class MlgRefilDims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ["n_agents", "n_entities", "entity_shape", "n_actions",
+                                              "entity_last_action", "attn_embed_dim", "attn_n_heads",
+                                              "rnn_hidden_dim"]]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
 # name -> (restype, argtypes); mirrors include/maleague.h one for one.
@@ -93,6 +110,10 @@ SIGNATURES = {
     "mlg_qlearner_workspace_floats": (ctypes.c_int64, [_P]),
     "mlg_qlearner_train": (ctypes.c_int, [_P, _P, _P]),
     "mlg_zero_slots_bytes": (ctypes.c_int, [_P, _P, _I, _I, _I, _P]),
+    "mlg_refil_packed_agent_size": (ctypes.c_int64, [_P]),
+    "mlg_refil_pack_agent": (ctypes.c_int, [_P, _P, _P, _P]),
+    "mlg_refil_agent_forward": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "mlg_refil_rollout": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P]),
     "mlg_debug_set_stamps": (ctypes.c_int, [_P]),
     "mlg_last_error": (ctypes.c_char_p, []),
     "mlg_version": (ctypes.c_char_p, []),

@@ -58,3 +58,41 @@ def mlg_batch(batch, required=KEYS):
     mb = _native.MlgBatch(p("state"), p("obs"), p("actions"), p("avail_actions"), p("reward"), p("terminated"),
                           p("actions_onehot"), p("filled"), B, T1, 0, 0, 0, None if rows is None else rows.data_ptr())
     return mb, list(tensors.values()) + [rows]
+
+
+ENTITY_KEYS = ("entities", "obs_mask", "entity_mask", "actions", "avail_actions", "reward", "terminated",
+               "actions_onehot", "filled")
+ENTITY_DTYPES = {"entities": torch.float32, "obs_mask": torch.uint8, "entity_mask": torch.uint8,
+                 "actions": torch.int64, "avail_actions": torch.int32, "reward": torch.float32,
+                 "terminated": torch.uint8, "actions_onehot": torch.float32, "filled": torch.int64}
+
+
+def mlg_entity_batch(batch):
+    """Entity-scheme EpisodeBatch (REFIL, config 5) -> MlgEntityBatch. Returns (MlgEntityBatch, keepalive)."""
+    rows = None
+    if getattr(batch, "rows", None) is not None and getattr(batch, "_data", None) is None:
+        rows = batch.rows
+        data = batch.ring.data.transition_data
+    else:
+        data = batch.data.transition_data
+    B = batch.batch_size
+    ref = data["entities"]
+    T1 = ref.stride(0) // max(1, ref.stride(1)) if ref.dim() > 1 and ref.stride(1) > 0 else ref.shape[1]
+    tensors = {}
+    for k in ENTITY_KEYS:
+        if k not in data:
+            raise KeyError(f"entity EpisodeBatch lacks {k!r} needed by the kernel")
+        t = data[k]
+        if t.dtype != ENTITY_DTYPES[k]:
+            raise TypeError(f"EpisodeBatch[{k!r}] has dtype {t.dtype}, kernel expects {ENTITY_DTYPES[k]}")
+        if not t.is_cuda:
+            raise _native.NativeError(f"EpisodeBatch[{k!r}] is on {t.device}; kernels need device tensors")
+        tensors[k] = t
+    if not all(_time_stride_ok(t, T1) for t in tensors.values()):
+        tensors = {k: t.contiguous() for k, t in tensors.items()}
+        T1 = batch.max_seq_length
+    p = lambda k: tensors[k].data_ptr()  # noqa: E731
+    mb = _native.MlgEntityBatch(p("entities"), p("obs_mask"), p("entity_mask"), p("actions"), p("avail_actions"),
+                                p("reward"), p("terminated"), p("actions_onehot"), p("filled"), B, T1, 0, 0, 0,
+                                None if rows is None else rows.data_ptr())
+    return mb, list(tensors.values()) + [rows]

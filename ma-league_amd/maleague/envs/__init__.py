@@ -1,4 +1,5 @@
 """Env registry (reference: src/envs/__init__.py:9 -- REGISTRY["ma"])."""
+from .entity_env import EntityEnvSpec
 from .teams_env import TeamsEnv, TeamsEnvSpec, VecEnvState, load_match_build_plan
 
 
@@ -8,4 +9,4 @@ def ma_env(**kwargs) -> TeamsEnv:
 
 REGISTRY = {"ma": ma_env}
 
-__all__ = ["REGISTRY", "TeamsEnv", "TeamsEnvSpec", "VecEnvState", "load_match_build_plan"]
+__all__ = ["EntityEnvSpec", "REGISTRY", "TeamsEnv", "TeamsEnvSpec", "VecEnvState", "load_match_build_plan"]

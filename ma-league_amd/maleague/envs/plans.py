@@ -18,6 +18,8 @@ _COMPOSITIONS = {
     "medium_1h_2t_2a": "TR TR HR AR AR",
     "medium_1h_2t_2a_melee": "TM TM HM AM AM",
     "large": " ".join(["TR"] * 25),
+    # entity env (REFIL, config 5): 8 slots per team, the first k in play; every k >= 3 fields a healer
+    "refil_8": "TR AR HR AR TM AR HR AM",
 }
 
 
@@ -45,3 +47,8 @@ def mirror_plan(plan, ai: bool, config_dir=None):
     home = next((t for t in teams if not t.get("is_scripted", False)), teams[0])
     return [{"is_scripted": False, "units": list(home["units"])},
             {"is_scripted": bool(ai), "units": list(home["units"])}]
+
+
+def builtin_composition(name: str):
+    """[(ROLE, ATTACK), ...] unit slots of a built-in composition."""
+    return [(_ROLE[c[0]], _ATK[c[1]]) for c in _COMPOSITIONS[name].split()]

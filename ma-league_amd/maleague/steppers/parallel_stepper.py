@@ -88,7 +88,7 @@ class ParallelStepper(EnvStepper):
         self.device = torch.device(args.device)
         env_args = dict(args.env_args)
         env_args.setdefault("seed", getattr(args, "seed", 0))
-        self.spec = TeamsEnvSpec.from_env_args(env_args, getattr(args, "config_dir", None))
+        self.spec = self._build_spec(env_args, getattr(args, "config_dir", None))
         self.policy_team_id = self.spec.policy_team
         self.env_info = self.spec.env_info()
         self.episode_limit = self.env_info["episode_limit"]
@@ -114,6 +114,21 @@ class ParallelStepper(EnvStepper):
         self.away_mac = None  # self-play only (SelfPlayParallelStepper)
         self.timing = None  # list -> (start, end) HIP events around every rollout launch (bench.py)
         self._ring = None   # ReplayBuffer written in place (zero-copy insert), see attach_replay()
+
+    _batch_keys = ("state", "obs", "actions", "avail_actions", "reward", "terminated", "actions_onehot", "filled")
+
+    def _build_spec(self, env_args, config_dir):
+        return TeamsEnvSpec.from_env_args(env_args, config_dir)
+
+    def _to_mlg(self, batch):
+        return mlg_batch(batch)
+
+    def _rollout(self, mb, run_info, epsilon, test_mode):
+        agent = self.home_mac.agent
+        st = self.envs.to_c()
+        _native.call("mlg_rollout", _native.byref(self._cspec), _native.byref(st), _native.byref(agent.dims()),
+                     _native.ptr(agent.packed()), _native.byref(mb), _native.byref(run_info), float(epsilon),
+                     int(bool(test_mode)), _native.stream_ptr(self.device))
 
     def initialize(self, scheme, groups, preprocess, home_mac, away_mac=None):
         if away_mac is not None:
@@ -213,9 +228,7 @@ class ParallelStepper(EnvStepper):
         insert_episode_batch then only advances its indices). Returns False when the layouts differ."""
         ok = (_same_device(buffer.device, self.device) and buffer.max_seq_length == self.episode_limit + 1
               and buffer.buffer_size >= self.batch_size
-              and all(k in buffer.data.transition_data for k in ("state", "obs", "actions", "avail_actions",
-                                                                  "reward", "terminated", "actions_onehot",
-                                                                  "filled")))
+              and all(k in buffer.data.transition_data for k in self._batch_keys))
         self._ring = buffer if ok else None
         return ok
 
@@ -231,7 +244,7 @@ class ParallelStepper(EnvStepper):
         self.env_steps_this_run = 0
 
     def _launch(self, batch: EpisodeBatch, epsilon: float, test_mode: bool):
-        mb, keep = mlg_batch(batch)
+        mb, keep = self._to_mlg(batch)
         self._launch_mb(mb, epsilon, test_mode)
         del keep
 
@@ -244,17 +257,11 @@ class ParallelStepper(EnvStepper):
 
     def _launch_mb(self, mb, epsilon: float, test_mode: bool):
         run_info = self._run_info()
-        agent = self.home_mac.agent
-        d = agent.dims()
-        st = self.envs.to_c()
-        packed = agent.packed()
         ev = None
         if self.timing is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        _native.call("mlg_rollout", _native.byref(self._cspec), _native.byref(st), _native.byref(d),
-                     _native.ptr(packed), _native.byref(mb), _native.byref(run_info), float(epsilon),
-                     int(bool(test_mode)), _native.stream_ptr(self.device))
+        self._rollout(mb, run_info, epsilon, test_mode)
         if ev is not None:
             ev[1].record()
             self.timing.append(ev)
@@ -273,7 +280,7 @@ class ParallelStepper(EnvStepper):
         ring = self._ring if not test_mode else None
         if ring is not None:
             slot0 = ring.buffer_index
-            mb, keep = mlg_batch(ring)
+            mb, keep = self._to_mlg(ring)
             # full-write mode: the kernel writes every byte of the B ring slots (zeros past each episode's end,
             # by the idle lanes of finished envs), so nothing is zero-initialised or copied
             mb.B, mb.ring_slot0, mb.ring_size, mb.full_write = self.batch_size, slot0, ring.buffer_size, 1

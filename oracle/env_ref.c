@@ -280,3 +280,50 @@ void envref_avail(const envref_spec *s, const int *x, const int *y, const int *h
 
 int envref_maxu(void) { return MAXU; }
 int envref_sizeof_spec(void) { return (int)sizeof(envref_spec); }
+
+/*
+ * Entity variant ("refil" env, config 5). U = 2S units, S slots per team: policy team = units
+ * 0..S-1 (they are the agents, entity index = unit index, so entities[:n_agents] are the agents as
+ * EntityAttentionRNNAgent assumes, src/marl/modules/agents/entity_rnn_agent.py:38), scripted team = S..2S-1.
+ * Per episode k active slots per team, k = kmin + r % (kmax - kmin + 1), r = rng(key, ctr(episode, 0, TEAM=4, 0));
+ * absent units have hp 0 for the whole episode (never spawn, never act, never targetable). Everything else is
+ * spec v1.
+ */
+int envref_reset_entity(const envref_spec *s, uint64_t key, uint32_t episode, int kmin, int kmax, int *x, int *y,
+                        int *hp) {
+    envref_reset(s, key, episode, x, y, hp);
+    uint64_t r = envref_rng(key, envref_ctr(episode, 0, 4, 0));
+    int k = kmin + (int)(r % (uint64_t)(kmax - kmin + 1));
+    for (int u = 0; u < s->U; ++u)
+        if (u - s->team_first[s->team[u]] >= k) hp[u] = 0;
+    return k;
+}
+
+/*
+ * Entity observation (the REFIL entity scheme: entities [U][8], obs_mask [U][U], entity_mask [U]; 1 = masked).
+ *   entity j (alive): [1, x/P, y/P, hp/max_hp, team, role/2, melee, power/8]; dead or absent: zeros.
+ *   entity_mask[j] = hp_j <= 0.   obs_mask[i][j] = hp_i <= 0 || hp_j <= 0 || dist2(i, j) > sight^2.
+ */
+void envref_entities(const envref_spec *s, const int *x, const int *y, const int *hp, float *ent, uint8_t *obs_mask,
+                     uint8_t *entity_mask) {
+    int U = s->U;
+    float inv_p = 1.0f / (float)pow2_at_least(s->grid);
+    for (int j = 0; j < U; ++j) {
+        float *o = ent + j * 8;
+        entity_mask[j] = hp[j] <= 0;
+        if (hp[j] <= 0) {
+            for (int f = 0; f < 8; ++f) o[f] = 0.0f;
+        } else {
+            o[0] = 1.0f;
+            o[1] = (float)x[j] * inv_p;
+            o[2] = (float)y[j] * inv_p;
+            o[3] = (float)hp[j] * (1.0f / (float)ROLE_MAXHP[s->role[j]]);
+            o[4] = (float)s->team[j];
+            o[5] = (float)s->role[j] * 0.5f;
+            o[6] = (float)s->melee[j];
+            o[7] = (float)ROLE_POWER[s->role[j]] * 0.125f;
+        }
+        for (int i = 0; i < U; ++i)
+            obs_mask[i * U + j] = hp[i] <= 0 || hp[j] <= 0 || dist2(x, y, i, j) > SIGHT2;
+    }
+}

@@ -155,3 +155,38 @@ class RefEnv:
         a = np.zeros((self.N, self.A), np.int32)
         lib().envref_avail(ctypes.byref(self.spec), self._p(self.x), self._p(self.y), self._p(self.hp), self._p(a))
         return a
+
+
+class RefEntityEnv(RefEnv):
+    """The entity ("refil") variant of the spec (env_ref.c envref_reset_entity / envref_entities): S slots per
+    team, policy team = units 0..S-1 (the agents), scripted team = S..2S-1, k ~ U{kmin..kmax} active per team
+    per episode."""
+
+    def __init__(self, roles, melees, kmin, kmax, grid=20, episode_limit=100, stochastic=True, seed=0, env_index=0):
+        S = len(roles)
+        super().__init__([0] * S + [1] * S, list(roles) * 2, list(melees) * 2, [False, True], grid=grid,
+                         episode_limit=episode_limit, stochastic=stochastic, seed=seed, env_index=env_index)
+        self.kmin, self.kmax = int(kmin), int(kmax)
+        self.k = None
+
+    def reset(self):
+        L = lib()
+        L.envref_reset_entity.restype = ctypes.c_int
+        L.envref_reset_entity.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        self.k = L.envref_reset_entity(ctypes.byref(self.spec), self.key, self.episode, self.kmin, self.kmax,
+                                       self._p(self.x), self._p(self.y), self._p(self.hp))
+        self.cur_episode = self.episode
+        self.episode += 1
+        self.t = 0
+
+    def entities(self):
+        U = self.U
+        ent = np.zeros((U, 8), np.float32)
+        om = np.zeros((U, U), np.uint8)
+        em = np.zeros(U, np.uint8)
+        L = lib()
+        L.envref_entities.argtypes = [ctypes.c_void_p] * 7
+        L.envref_entities(ctypes.byref(self.spec), self._p(self.x), self._p(self.y), self._p(self.hp), self._p(ent),
+                          self._p(om), self._p(em))
+        return ent, om, em

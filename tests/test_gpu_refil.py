@@ -1,0 +1,152 @@
+"""GPU parity of the REFIL path (config 5): entity env + EntityMAC rollout kernel and the
+EntityAttentionRNNAgent forward against the CPU oracle (oracle/env_ref.c entity variant, oracle/refil_ref.py)
+and the reference's golden vectors (tests/golden/refil_layers.npz, made by tests/golden/make_refil_golden.py).
+
+Tolerances: env arithmetic, masks, bookkeeping and epsilon draws bit-exact; Q / hidden fp32 within 1e-4 abs.
+"""
+import numpy as np
+import pytest
+import torch
+
+import envref
+import refil_ref as RR
+from helpers import entity_scheme_for, np_batch, ref_entity_envs_for, refil_args
+
+pytestmark = pytest.mark.gpu
+
+Q_TOL = 1e-4
+
+
+def _agent(device, params=None, seed=0, **kw):
+    from maleague.modules.agents import REGISTRY
+    a = refil_args(**kw)
+    torch.manual_seed(seed)
+    ag = REGISTRY["imagine_entity_attend_rnn"](a.entity_shape + a.n_actions, a).to(device)
+    if params is not None:
+        ag.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in params.items()})
+    return ag, a
+
+
+def _params(d, prefix):
+    return {k[len(prefix):]: d[k] for k in d.files if k.startswith(prefix)}
+
+
+def test_agent_forward_matches_golden(device, golden):
+    d = golden("refil_layers.npz")
+    ag, a = _agent(device, _params(d, "agent.p."))
+    ent, om, em = (torch.from_numpy(d[k]).to(device) for k in ("agent.ent", "agent.om", "agent.em"))
+    h0 = torch.from_numpy(d["agent.h0"]).to(device)
+    q, hs = ag((ent, om, em), h0)
+    np.testing.assert_allclose(q.cpu().numpy(), d["agent.q"], atol=Q_TOL, rtol=0)
+    np.testing.assert_allclose(hs.cpu().numpy(), d["agent.hs"], atol=Q_TOL, rtol=0)
+    # imagination: 3 copies (plain, within, interact) with the recorded group draw
+    qi, hi, (Wm, Im) = ag((ent, om, em), h0, imagine=True, groupA=torch.from_numpy(d["imagine.groupA"]).to(device))
+    np.testing.assert_allclose(qi.cpu().numpy(), d["imagine.q"], atol=Q_TOL, rtol=0)
+    np.testing.assert_array_equal(Wm.cpu().numpy(), d["imagine.Wmask"])
+    np.testing.assert_array_equal(Im.cpu().numpy(), d["imagine.Imask"])
+
+
+def _rollout(device, B=12, T=40, seed=5, eps=0.0, test_mode=True, ring=None, agent_seed=1, st=None, kmin=3, kmax=8):
+    from maleague import _native
+    from maleague.components.episode_batch import EpisodeBatch
+    from maleague.components.batch_view import mlg_entity_batch
+    from maleague.envs.entity_env import EntityEnvSpec
+    from maleague.envs.teams_env import VecEnvState
+    spec = EntityEnvSpec.from_env_args({"match_build_plan": "refil_8", "episode_limit": T, "seed": seed,
+                                        "min_agents": kmin, "max_agents": kmax})
+    ag, a = _agent(device, seed=agent_seed)
+    info = spec.env_info()
+    scheme, groups, pre = entity_scheme_for(info, torch)
+    if st is None:
+        st = VecEnvState(spec, B, device)
+    batch = EpisodeBatch(scheme, groups, B, T + 1, preprocess=pre, device=device)
+    if ring is not None:
+        for v in batch.data.transition_data.values():
+            v.fill_(7)
+    mb, keep = mlg_entity_batch(batch)
+    if ring is not None:
+        mb.full_write = 1
+    run = torch.zeros(6 * B, dtype=torch.int32, device=device)
+    ri = _native.MlgRunInfo(run[0:B].data_ptr(), run[4 * B:5 * B].data_ptr(), run[B:3 * B].data_ptr(),
+                            run[3 * B:4 * B].data_ptr(), None, None)
+    _native.call("mlg_refil_rollout", _native.byref(spec.to_c()), _native.byref(st.to_c()), _native.byref(ag.dims()),
+                 _native.ptr(ag.packed()), _native.byref(mb), _native.byref(ri), float(eps), int(test_mode),
+                 _native.stream_ptr())
+    torch.cuda.synchronize()
+    r = run.cpu().numpy()
+    summary = {"len": r[0:B], "won": r[B:3 * B].reshape(B, 2), "draw": r[3 * B:4 * B],
+               "ret": r[4 * B:5 * B].view(np.float32)}
+    return spec, ag, a, np_batch(batch), summary, st
+
+
+@pytest.mark.parametrize("eps,test_mode", [(0.0, True), (0.3, False)])
+def test_rollout_teacher_forced_vs_oracle(device, eps, test_mode):
+    B, T, seed = 12, 40, 5
+    spec, ag, a, nb, summ, _ = _rollout(device, B, T, seed, eps, test_mode)
+    refs = ref_entity_envs_for(spec, B, seed=seed)
+    NA, A = spec.n_agents, spec.n_actions
+    p = {k: v.detach().cpu() for k, v in ag.state_dict().items()}
+    qref, _ = RR.mac_forward(p, {k: torch.from_numpy(v) for k, v in nb.items()}, a)
+    qref = qref.numpy()
+    n_rand = n_greedy = 0
+    for b, r in enumerate(refs):
+        r.reset()
+        L = int(summ["len"][b])
+        assert 1 <= L <= T
+        ret = np.float32(0)
+        for t in range(L + 1):
+            ent, om, em = r.entities()
+            np.testing.assert_array_equal(nb["entities"][b, t], ent, err_msg=f"entities b={b} t={t}")
+            np.testing.assert_array_equal(nb["obs_mask"][b, t], om, err_msg=f"obs_mask b={b} t={t}")
+            np.testing.assert_array_equal(nb["entity_mask"][b, t], em)
+            av = r.avail()
+            np.testing.assert_array_equal(nb["avail_actions"][b, t], av)
+            assert nb["filled"][b, t, 0] == 1
+            acts = nb["actions"][b, t, :, 0]
+            for n in range(NA):
+                key = envref.env_key(seed, b)
+                coin = not test_mode and eps > 0 and envref.u01(envref.rng(key, envref.ctr(r.cur_episode, t, 2, n))) < eps
+                if coin:
+                    want = envref.random_available(av[n], envref.rng(key, envref.ctr(r.cur_episode, t, 3, n)))
+                    assert acts[n] == want
+                    n_rand += 1
+                else:
+                    qm = np.where(av[n] != 0, qref[b, t, n], -np.inf)
+                    assert av[n, acts[n]] != 0 and qm[acts[n]] >= qm.max() - Q_TOL, (b, t, n)
+                    n_greedy += 1
+            oh = np.zeros((NA, A), np.float32)
+            oh[np.arange(NA), acts] = 1
+            np.testing.assert_array_equal(nb["actions_onehot"][b, t], oh)
+            if t < L:
+                rew, done, info = r.step(acts)
+                assert nb["reward"][b, t, 0] == np.float32(rew[0])
+                assert nb["terminated"][b, t, 0] == int(done)
+                assert done == (t == L - 1)
+                ret += np.float32(rew[0])
+        assert summ["won"][b, 0] == int(info["battle_won"][0]) and summ["won"][b, 1] == int(info["battle_won"][1])
+        assert summ["draw"][b] == int(info["draw"])
+        assert abs(summ["ret"][b] - ret) <= 1e-3
+        assert nb["filled"][b, L + 1:].sum() == 0 and nb["reward"][b, L:].sum() == 0
+    assert n_greedy > 0 and (test_mode or n_rand > 0)
+
+
+def test_rollout_ring_full_write_equals_zeroed(device):
+    """full-write mode writes every byte of the slots (garbage-filled here): identical to the zeroed batch."""
+    *_, nb0, s0, st = _rollout(device, B=10, T=30, seed=9, eps=0.2, test_mode=False)
+    # same env state as the first run started from: a fresh state advanced by nothing
+    *_, nb1, s1, _ = _rollout(device, B=10, T=30, seed=9, eps=0.2, test_mode=False, ring=True)
+    for k in nb0:
+        np.testing.assert_array_equal(nb0[k], nb1[k], err_msg=k)
+    np.testing.assert_array_equal(s0["len"], s1["len"])
+
+
+def test_rollout_fixed_team_sizes(device):
+    """k = 8 (full teams) and k = 3 (smallest): absent slots masked, padded agents only no-op."""
+    for k in (3, 8):
+        spec, ag, a, nb, summ, _ = _rollout(device, B=6, T=25, seed=2, kmin=k, kmax=k)
+        em = nb["entity_mask"][:, 0]
+        assert (em[:, :k] == 0).all() and (em[:, k:8] == 1).all() and (em[:, 8:8 + k] == 0).all()
+        if k < 8:
+            av = nb["avail_actions"][:, 0, k:]
+            assert (av[..., 0] == 1).all() and (av[..., 1:] == 0).all()
+            assert (nb["actions"][:, 0, k:, 0] == 0).all()
