@@ -244,6 +244,35 @@ int mlg_refil_agent_forward(const MlgRefilDims *d, const float *packed, const fl
 int mlg_refil_rollout(const MlgEntityEnvSpec *spec, MlgEnvState *st, const MlgRefilDims *d, const float *packed,
                       MlgEntityBatch *batch, MlgRunInfo *info, float epsilon, int32_t test_mode, void *stream);
 
+/* REFILLearner.train (src/marl/learners/refil_learner.py:102-218) as one device pipeline: EntityMAC unrolls of the
+ * plain / within / interact copies + target, FlexQMixer (flex_qmix.py:55-117) plain + imagined mixing, double-Q
+ * targets, the lambda-mixed TD loss, all gradients, clip_grad_norm_ and RMSprop.
+ * Flat parameters = [agent | mixer]; agent in named_parameters order (see mlg_refil_pack_agent); mixer =
+ * hyper_w_1, hyper_w_final, hyper_b_1, V, each: fc1.weight [64][D0], fc1.bias, attn.in_trans.weight [192][64],
+ * attn.out_trans.weight [64][64], attn.out_trans.bias, fc2.weight [32][64], fc2.bias [32]. */
+typedef struct {
+    int32_t B, T, n_agents, n_entities, entity_shape, n_actions, entity_last_action;
+    int32_t attn_embed_dim, attn_n_heads, rnn_hidden_dim, hypernet_embed, mixing_embed_dim;
+    int32_t double_q, softmax_mixing_weights, imagine;
+    float gamma, lmbda, lr, optim_alpha, optim_eps, grad_norm_clip;
+} MlgRefilLearnerCfg;
+
+typedef struct {
+    MlgEntityBatch batch;        /* B episodes, T timesteps used (batch.T1 = stride) */
+    const uint8_t *groupA;       /* [B][NE] the imagine group draw per episode (entity_rnn_agent.py:95-97) */
+    float *params;               /* [n_agent + n_mixer] updated in place (RMSprop) */
+    float *grads;                /* [n_agent + n_mixer] out: clipped gradients */
+    float *square_avg;           /* RMSprop state */
+    const float *target_params;  /* target networks, same layout */
+    float *workspace;            /* mlg_refil_workspace_floats() floats */
+    float *stats;                /* [8] out: loss, im_loss, grad_norm, td_error_abs, q_taken_mean, target_mean,
+                                    mask_sum, 0 */
+} MlgRefilLearnerBufs;
+
+int64_t mlg_refil_param_counts(const MlgRefilLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);
+int64_t mlg_refil_workspace_floats(const MlgRefilLearnerCfg *c);
+int mlg_refil_train(const MlgRefilLearnerCfg *c, const MlgRefilLearnerBufs *b, void *stream);
+
 /* Diagnostic builds only (-DMLG_STAMPS): device buffer [grid][8 waves][16] u64 of per-phase cycle counts
  * of mlg_rollout. Returns nonzero in normal builds. */
 int mlg_debug_set_stamps(void *ptr);

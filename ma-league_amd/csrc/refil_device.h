@@ -156,6 +156,20 @@ __device__ __forceinline__ void mm_reg(floatx4 (&acc)[MT], const float* __restri
         for (int i = 0; i < MT; ++i) acc[i] = mfma_chunk(ld4(wr + (int64_t)i * 16 * ldw + kc * 16), x[kc], acc[i]);
 }
 
+// same with a per-lane row pointer (rows scattered in HBM): lane (col, g) passes the base of its tile row col
+template <int MT>
+__device__ __forceinline__ void mm_ptr(floatx4 (&acc)[MT], const float* __restrict__ W, int ldw, int mt0, const float* xrow,
+                                       int kchunks, int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    const float* xr = xrow + 4 * g;
+    const float* wr = W + (int64_t)(mt0 * 16 + col) * ldw + 4 * g;
+    for (int kc = 0; kc < kchunks; ++kc) {
+        const floatx4 xv = ld4(xr + kc * 16);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i] = mfma_chunk(ld4(wr + (int64_t)i * 16 * ldw + kc * 16), xv, acc[i]);
+    }
+}
+
 __device__ __forceinline__ void st_row(float* Y, int ldy, int mt, const floatx4 v, int lane) {
     *reinterpret_cast<floatx4*>(Y + (lane & 15) * ldy + mt * 16 + 4 * (lane >> 4)) = v;
 }

@@ -1,0 +1,1305 @@
+// refil_learner.hip -- REFILLearner.train (src/marl/learners/refil_learner.py:102-218) as one device pipeline.
+//
+//   pack        online/target agent + 4 hypernets -> kernel layouts; transposes for the backward
+//   mask_sum    mask = filled[:, :-1] * (1 - terminated shifted) and its sum              (:106-108, :197-201)
+//   ein         entity inputs [entities | last-action one-hot of agent entities] per (b, t)  (_build_inputs,
+//               entity_controller.py:11-30, _get_mixer_ins :81-100)
+//   ent_fwd     per item pair: fc1 -> in_trans -> attention for the three agent copies (plain, within,
+//               interact; entity_rnn_agent.py:88-126) -> out_trans -> fc2 -> W_ih x; target net: plain copy only
+//   rec         GRU recurrence over t for all online (3 copies) and target rows, gates saved
+//   q           fc3 for every (t, row), masked agents -> 0 (entity_rnn_agent.py:58-61)
+//   hyper_fwd   per (item, hypernet, net): AttentionHyperNet forward (flex_qmix.py:20-53); hyper_w_1 online with
+//               the plain / W / I attention masks (imagine groups)
+//   mix_td      per item: chosen Q gather, double-Q target (refil_learner.py:147-164), FlexQMixer mixing of the
+//               plain and the imagined Q (:166-190, flex_qmix.py:73-117), targets, TD, the lambda-mixed loss
+//               (:193-208), and the mixing backward -> dX of every hypernet output and dQ of every agent copy
+//   hyper_bwd   per (item, hypernet): fc2 / out_trans / attention / in_trans / fc1 backward (deltas for wgrad)
+//   rec_bwd     reverse-time GRU backward of the online rows
+//   ent_bwd     per item pair: W_ih^T, fc2, out_trans, attention (3 copies, accumulated), in_trans, fc1 backward
+//   wgrad       23 weight-gradient jobs (wgrad_device.h), deterministic
+//   finish      clip_grad_norm_ (10), RMSprop, stats (:211-231)
+// Agent rows: r = (c * B + b) * NA + n for copy c (0 plain, 1 within, 2 interact); target rows r = b * NA + n.
+// Items i = b * T + t. Mixer items use t < T - 1 (the other kernels write zeros for t = T - 1).
+#include "mlg_host.h"
+#include "refil_device.h"
+#include "wgrad_device.h"
+
+using namespace refil;
+
+namespace {
+
+constexpr int MJ = 24;
+using RJobs = mlg::WJobsT<MJ>;
+
+struct RCfg {
+    int B, T, T1, NA, NE, ED, D0, K1, A, Ap, I, Ron, Rtg;
+    int double_q, softmax;
+    float gamma, lmbda;
+};
+
+struct WsR {
+    int64_t pa_on, pa_tg, ph_on[4], ph_tg[4];
+    int64_t a_winT, a_woutT, a_w2T, a_wihT, h_winT[4], h_woutT[4], h_w2T[4];
+    int64_t ein, x1, qkv, P, o, x2, x3, gi_on, gi_tg, hs_on, hs_tg, gr, gz, gn, ghn, mac, tmac;
+    int64_t x1m[4], qkvm[4], Pm[4], om[4], x2m[4], X[4], Xtg[4], dX[4], doutm[4], dqkvm[4], dfc1m[4];
+    int64_t dq, d2, part, msum, dgi, dgh, dfc2, dout, dqkv, dfc1;
+    int64_t slab, nrm, total;
+};
+
+struct Plan {
+    RCfg c;
+    RAgent La;
+    RHyper Lh;
+    WsR w;
+    int64_t n_agent, n_mixer;
+};
+
+__host__ __device__ inline int nvar(int k) { return k == 0 ? 3 : 1; }
+
+int check_cfg(const MlgRefilLearnerCfg* c) {
+    MLG_REQUIRE(c != nullptr, "null refil learner cfg");
+    MLG_REQUIRE(c->B >= 1 && c->T >= 2, "refil learner: B=%d T=%d", c->B, c->T);
+    MLG_REQUIRE(c->n_agents >= 1 && c->n_agents <= NAS && c->n_entities >= c->n_agents && c->n_entities <= NE,
+                "refil learner: n_agents=%d n_entities=%d unsupported (<= 8, <= 16)", c->n_agents, c->n_entities);
+    MLG_REQUIRE(c->attn_embed_dim == EMB && c->rnn_hidden_dim == EMB && c->hypernet_embed == EMB && c->attn_n_heads == NH &&
+                    c->mixing_embed_dim == EM,
+                "refil learner: attn_embed_dim/rnn_hidden_dim/hypernet_embed 64, 4 heads, mixing_embed_dim 32 supported");
+    const int D0 = c->entity_shape + (c->entity_last_action ? c->n_actions : 0);
+    MLG_REQUIRE(D0 <= KMAX && c->n_actions >= 1 && c->n_actions <= 32, "refil learner: entity input %d / actions %d",
+                D0, c->n_actions);
+    MLG_REQUIRE(c->imagine == 1, "refil learner: the imagine agent (REFIL) is the built path");
+    return 0;
+}
+
+Plan make_plan(const MlgRefilLearnerCfg* cfg, int T1) {
+    Plan p;
+    RCfg& c = p.c;
+    c.B = cfg->B;
+    c.T = cfg->T;
+    c.T1 = T1;
+    c.NA = cfg->n_agents;
+    c.NE = cfg->n_entities;
+    c.ED = cfg->entity_shape;
+    c.A = cfg->n_actions;
+    c.D0 = cfg->entity_shape + (cfg->entity_last_action ? cfg->n_actions : 0);
+    c.K1 = (c.D0 + 15) / 16 * 16;
+    c.Ap = (c.A + 15) / 16 * 16;
+    c.I = c.B * c.T;
+    c.Ron = 3 * c.B * c.NA;
+    c.Rtg = c.B * c.NA;
+    c.double_q = cfg->double_q;
+    c.softmax = cfg->softmax_mixing_weights;
+    c.gamma = cfg->gamma;
+    c.lmbda = cfg->lmbda;
+    p.La = make_ragent(c.D0, c.A);
+    p.Lh = make_rhyper(c.D0);
+    p.n_agent = p.La.c_total;
+    p.n_mixer = 4 * p.Lh.c_total;
+    WsR& w = p.w;
+    int64_t o = 0;
+    auto take = [&](int64_t n) { int64_t r = o; o += mlg_align4(n); return r; };
+    const int64_t I = c.I, T = c.T, Ron = c.Ron, Rtg = c.Rtg;
+    w.pa_on = take(p.La.total);
+    w.pa_tg = take(p.La.total);
+    for (int k = 0; k < 4; ++k) w.ph_on[k] = take(p.Lh.total);
+    for (int k = 0; k < 4; ++k) w.ph_tg[k] = take(p.Lh.total);
+    w.a_winT = take(EMB * 3 * EMB);
+    w.a_woutT = take(EMB * EMB);
+    w.a_w2T = take(EMB * EMB);
+    w.a_wihT = take(EMB * 3 * EMB);
+    for (int k = 0; k < 4; ++k) {
+        w.h_winT[k] = take(EMB * 3 * EMB);
+        w.h_woutT[k] = take(EMB * EMB);
+        w.h_w2T[k] = take(EMB * EM);
+    }
+    w.ein = take(I * NE * c.K1);
+    w.x1 = take(I * NE * EMB);
+    w.qkv = take(I * NE * 3 * EMB);
+    w.P = take(3 * I * 1024);
+    w.o = take(T * Ron * EMB);
+    w.x2 = take(T * Ron * EMB);
+    w.x3 = take(T * Ron * EMB);
+    w.gi_on = take(T * Ron * 3 * EMB);
+    w.gi_tg = take(T * Rtg * 3 * EMB);
+    w.hs_on = take((T + 1) * Ron * EMB);
+    w.hs_tg = take((T + 1) * Rtg * EMB);
+    w.gr = take(T * Ron * EMB);
+    w.gz = take(T * Ron * EMB);
+    w.gn = take(T * Ron * EMB);
+    w.ghn = take(T * Ron * EMB);
+    w.mac = take(T * Ron * c.A);
+    w.tmac = take(T * Rtg * c.A);
+    for (int k = 0; k < 4; ++k) {
+        const int V = nvar(k);
+        w.x1m[k] = take(I * NE * EMB);
+        w.qkvm[k] = take(I * NE * 3 * EMB);
+        w.Pm[k] = take((int64_t)V * I * 1024);
+        w.om[k] = take((int64_t)V * I * NAS * EMB);
+        w.x2m[k] = take((int64_t)V * I * NAS * EMB);
+        w.X[k] = take((int64_t)V * I * NAS * EM);
+        w.Xtg[k] = take(I * NAS * EM);
+        w.dX[k] = take((int64_t)V * I * NAS * EM);
+        w.doutm[k] = take((int64_t)V * I * NAS * EMB);
+        w.dqkvm[k] = take(I * NE * 3 * EMB);
+        w.dfc1m[k] = take(I * NE * EMB);
+    }
+    w.dq = take(T * Ron);
+    w.d2 = take(T * Ron * c.A);
+    w.part = take(I * 8);
+    w.msum = take(4);
+    w.dgi = take(T * Ron * 3 * EMB);
+    w.dgh = take(T * Ron * 3 * EMB);
+    w.dfc2 = take(T * Ron * EMB);
+    w.dout = take(T * Ron * EMB);
+    w.dqkv = take(I * NE * 3 * EMB);
+    w.dfc1 = take(I * NE * EMB);
+    w.slab = o;
+    w.nrm = 0;
+    w.total = o;
+    return p;
+}
+
+// ---- small kernels ---------------------------------------------------------------------------------------
+struct CopyJob {
+    int64_t src, src2, dst;
+    int rows_dst, cols_dst, rows_src, cols_src;
+};
+struct CopyJobs {
+    CopyJob j[16];
+    int n;
+    int64_t total;
+};
+
+__global__ void copy_jobs_kernel(CopyJobs J, const float* __restrict__ src, float* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J.total) return;
+    float v = 0.f;
+    for (int q = 0; q < J.n; ++q) {
+        const CopyJob& c = J.j[q];
+        const int64_t n = (int64_t)c.rows_dst * c.cols_dst;
+        if (i >= c.dst && i < c.dst + n) {
+            const int64_t l = i - c.dst;
+            const int r = (int)(l / c.cols_dst), col = (int)(l % c.cols_dst);
+            if (r < c.rows_src && col < c.cols_src) {
+                v = src[c.src + (int64_t)r * c.cols_src + col];
+                if (c.src2 >= 0) v += src[c.src2 + (int64_t)r * c.cols_src + col];
+            }
+            break;
+        }
+    }
+    dst[i] = v;
+}
+
+CopyJob cj(int64_t src, int64_t dst, int rd, int cd, int rs, int cs, int64_t src2 = -1) {
+    return CopyJob{src, src2, dst, rd, cd, rs, cs};
+}
+
+CopyJobs agent_jobs(const RAgent& L) {
+    CopyJobs J;
+    J.n = 0;
+    J.j[J.n++] = cj(L.c_w1, L.w1, EMB, L.K1, EMB, L.D0);
+    J.j[J.n++] = cj(L.c_b1, L.b1, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_win, L.win, 3 * EMB, EMB, 3 * EMB, EMB);
+    J.j[J.n++] = cj(L.c_wout, L.wout, EMB, EMB, EMB, EMB);
+    J.j[J.n++] = cj(L.c_bout, L.bout, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_w2, L.w2, EMB, EMB, EMB, EMB);
+    J.j[J.n++] = cj(L.c_b2, L.b2, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_wih, L.wih, 3 * EMB, EMB, 3 * EMB, EMB);
+    J.j[J.n++] = cj(L.c_whh, L.whh, 3 * EMB, EMB, 3 * EMB, EMB);
+    J.j[J.n++] = cj(L.c_bih, L.bih, 1, 3 * EMB, 1, 3 * EMB);
+    J.j[J.n++] = cj(L.c_bhh, L.bhh, 1, 3 * EMB, 1, 3 * EMB);
+    J.j[J.n++] = cj(L.c_bih, L.brz, 1, 2 * EMB, 1, 2 * EMB, L.c_bhh);
+    J.j[J.n++] = cj(L.c_w3, L.w3, L.Ap, EMB, L.A, EMB);
+    J.j[J.n++] = cj(L.c_b3, L.b3, 1, L.Ap, 1, L.A);
+    J.total = L.total;
+    return J;
+}
+
+CopyJobs hyper_jobs(const RHyper& L) {
+    CopyJobs J;
+    J.n = 0;
+    J.j[J.n++] = cj(L.c_w1, L.w1, EMB, L.K1, EMB, L.D0);
+    J.j[J.n++] = cj(L.c_b1, L.b1, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_win, L.win, 3 * EMB, EMB, 3 * EMB, EMB);
+    J.j[J.n++] = cj(L.c_wout, L.wout, EMB, EMB, EMB, EMB);
+    J.j[J.n++] = cj(L.c_bout, L.bout, 1, EMB, 1, EMB);
+    J.j[J.n++] = cj(L.c_w2, L.w2, EM, EMB, EM, EMB);
+    J.j[J.n++] = cj(L.c_b2, L.b2, 1, EM, 1, EM);
+    J.total = L.total;
+    return J;
+}
+
+__global__ void transpose_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)rows * cols) return;
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    dst[(int64_t)c * rows + r] = src[i];
+}
+
+__device__ __forceinline__ int64_t eslot(const MlgEntityBatch& bt, int b) {
+    return bt.rows ? (int64_t)bt.rows[b] : (int64_t)b;
+}
+
+__device__ __forceinline__ float emask_at(const MlgEntityBatch& bt, int b, int t) {
+    const int64_t base = eslot(bt, b) * bt.T1;
+    float m = (float)bt.filled[base + t];
+    if (t > 0) m *= 1.f - (float)bt.terminated[base + t - 1];
+    return m;
+}
+
+__global__ void mask_sum_kernel(MlgEntityBatch bt, int B, int T, float* __restrict__ msum) {
+    __shared__ float red[1024];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < B * (T - 1); i += blockDim.x) s += emask_at(bt, i / (T - 1), i % (T - 1));
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) msum[0] = red[0];
+}
+
+// entity inputs ein[i][j][c] (K1 columns, zero padded)
+__global__ void ein_kernel(RCfg c, MlgEntityBatch bt, float* __restrict__ ein) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)c.I * NE * c.K1) return;
+    const int col = (int)(idx % c.K1);
+    const int j = (int)((idx / c.K1) % NE);
+    const int i = (int)(idx / ((int64_t)c.K1 * NE));
+    const int b = i / c.T, t = i % c.T;
+    const int64_t row = eslot(bt, b) * bt.T1 + t;
+    float v = 0.f;
+    if (j < c.NE) {
+        if (col < c.ED) v = bt.entities[(row * c.NE + j) * c.ED + col];
+        else if (col < c.D0 && j < c.NA && t > 0) v = bt.actions_onehot[((row - 1) * c.NA + j) * c.A + (col - c.ED)];
+    }
+    ein[idx] = v;
+}
+
+// ---- masks -----------------------------------------------------------------------------------------------
+// entity mask bits of (b, t); bits >= NE set (absent)
+__device__ __forceinline__ uint32_t em_bits(const RCfg& c, const MlgEntityBatch& bt, int b, int t) {
+    const uint8_t* em = bt.entity_mask + (eslot(bt, b) * bt.T1 + t) * c.NE;
+    uint32_t m = ~((1u << c.NE) - 1u) & 0xFFFFu;
+    for (int j = 0; j < c.NE; ++j) m |= (uint32_t)(em[j] != 0) << j;
+    return m;
+}
+__device__ __forceinline__ uint32_t om_row(const RCfg& c, const MlgEntityBatch& bt, int b, int t, int q) {
+    if (q >= c.NE) return 0xFFFFu;
+    const uint8_t* om = bt.obs_mask + ((eslot(bt, b) * bt.T1 + t) * c.NE + q) * c.NE;
+    uint32_t m = ~((1u << c.NE) - 1u) & 0xFFFFu;
+    for (int j = 0; j < c.NE; ++j) m |= (uint32_t)(om[j] != 0) << j;
+    return m;
+}
+// imagine group bits of episode b: gA = groupA | em0, gB = !groupA | em0 (entity_rnn_agent.py:97-101)
+__device__ __forceinline__ void group_bits(const RCfg& c, const MlgEntityBatch& bt, const uint8_t* groupA, int b,
+                                           uint32_t& gA, uint32_t& gB, uint32_t& em0) {
+    em0 = em_bits(c, bt, b, 0);
+    uint32_t ga = 0;
+    for (int j = 0; j < c.NE; ++j) ga |= (uint32_t)(groupA[(int64_t)b * c.NE + j] != 0) << j;
+    gA = (ga | em0) & 0xFFFFu;
+    gB = ((~ga) | em0) & 0xFFFFu;
+}
+// interact row q: pairs in the same group are masked (entity_rnn_agent.py:107-110); within = !interact
+__device__ __forceinline__ uint32_t interact_row(uint32_t gA, uint32_t gB, int q) {
+    const uint32_t a = ((gA >> q) & 1u) ? 0u : (~gA & 0xFFFFu);
+    const uint32_t bb = ((gB >> q) & 1u) ? 0u : (~gB & 0xFFFFu);
+    return a | bb;
+}
+__device__ __forceinline__ uint32_t active_row(uint32_t em0, int q) { return ((em0 >> q) & 1u) ? 0xFFFFu : em0; }
+// dead agent rows of an item (bits < 8): entity-masked agents and padding slots >= NA
+__device__ __forceinline__ uint32_t dead_bits(const RCfg& c, uint32_t em) {
+    return ((em & ((1u << c.NA) - 1u)) | (~((1u << c.NA) - 1u))) & 0xFFu;
+}
+
+// ---- agent entity block forward (online: 3 copies; target: plain) ---------------------------------------
+struct AgentPtrs {
+    const float* P;
+    float *x1, *qkv, *Pw, *o, *x2, *x3, *gi;
+};
+
+__global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
+                                                     RAgent L, const float* __restrict__ ein, AgentPtrs on,
+                                                     AgentPtrs tg) {
+    __shared__ float s_ein[NE * LDI];
+    __shared__ float s_x1[NE * LDX];
+    __shared__ float s_qkv[NE * LDQ];
+    __shared__ float s_o[3][16 * LDX];
+    __shared__ uint32_t s_m[3][2][16];
+    __shared__ uint32_t s_dead[2];
+    const int lane = threadIdx.x;
+    const bool online = blockIdx.y == 0;
+    const AgentPtrs& A = online ? on : tg;
+    const int ncopy = online ? 3 : 1;
+    const int R = online ? c.Ron : c.Rtg;
+    const int i0 = blockIdx.x * 2;
+    for (int k = lane; k < 3 * 16 * LDX; k += 64) (&s_o[0][0])[k] = 0.f;
+    if (lane < 32) {
+        const int e = lane >> 4, q = lane & 15, i = i0 + e;
+        if (i < c.I) {
+            const int b = i / c.T, t = i % c.T;
+            const uint32_t om = om_row(c, bt, b, t, q);
+            s_m[0][e][q] = om;
+            if (online) {
+                uint32_t gA, gB, em0;
+                group_bits(c, bt, groupA, b, gA, gB, em0);
+                const uint32_t it = interact_row(gA, gB, q);
+                s_m[1][e][q] = ((~it) & 0xFFFFu) | om;
+                s_m[2][e][q] = it | om;
+            }
+            if (q == 0) s_dead[e] = dead_bits(c, em_bits(c, bt, b, t));
+        } else {
+            for (int cc = 0; cc < 3; ++cc) s_m[cc][e][q] = 0xFFFFu;
+            if (q == 0) s_dead[e] = 0xFFu;
+        }
+    }
+    wave_sync();
+    for (int e = 0; e < 2; ++e) {
+        const int i = i0 + e;
+        if (i >= c.I) continue;
+        for (int k = lane; k < NE * c.K1; k += 64) s_ein[(k / c.K1) * LDI + k % c.K1] = ein[(int64_t)i * NE * c.K1 + k];
+        wave_sync();
+        dense_lds<true>(A.P + L.w1, L.K1, A.P + L.b1, EMB / 16, s_ein, LDI, L.K1 / 16, s_x1, LDX, lane);
+        wave_sync();
+        dense_lds<false>(A.P + L.win, EMB, nullptr, 3 * EMB / 16, s_x1, LDX, EMB / 16, s_qkv, LDQ, lane);
+        wave_sync();
+        if (online) {
+            for (int k = lane; k < NE * EMB; k += 64) A.x1[(int64_t)i * NE * EMB + k] = s_x1[(k / EMB) * LDX + k % EMB];
+            for (int k = lane; k < NE * 3 * EMB; k += 64)
+                A.qkv[(int64_t)i * NE * 3 * EMB + k] = s_qkv[(k / (3 * EMB)) * LDQ + k % (3 * EMB)];
+        }
+        for (int cc = 0; cc < ncopy; ++cc)
+            attn_fwd(s_qkv, s_m[cc][e], c.NA, c.NE, s_o[cc] + e * NAS * LDX, LDX,
+                     online ? A.Pw + ((int64_t)cc * c.I + i) * 1024 : nullptr, lane);
+        wave_sync();
+    }
+    const int col = lane & 15, g = lane >> 4;
+    const int e = col >> 3, n = col & 7, i = i0 + e;
+    const bool valid = i < c.I && n < c.NA;
+    const int b = valid ? i / c.T : 0, t = valid ? i % c.T : 0;
+    const uint32_t dead = s_dead[0] | (s_dead[1] << 8);
+    const bool rdead = (dead >> col) & 1u;
+    for (int cc = 0; cc < ncopy; ++cc) {
+        const int64_t r = ((int64_t)cc * c.B + b) * c.NA + n;
+        const int64_t ro = ((int64_t)t * R + r);
+        floatx4 x2[4], x3[4];
+        bias_init<4>(x2, A.P + L.bout, 0, lane);
+        mm_lds<4>(x2, A.P + L.wout, EMB, 0, s_o[cc], LDX, EMB / 16, lane);
+        if (rdead) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x2[k] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        bias_init<4>(x3, A.P + L.b2, 0, lane);
+        mm_reg<4, 4>(x3, A.P + L.w2, EMB, 0, x2, lane);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x3[k] = relu4(x3[k]);
+        if (valid && online) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                *reinterpret_cast<floatx4*>(A.o + ro * EMB + k * 16 + 4 * g) = ld4(s_o[cc] + col * LDX + k * 16 + 4 * g);
+                *reinterpret_cast<floatx4*>(A.x2 + ro * EMB + k * 16 + 4 * g) = x2[k];
+                *reinterpret_cast<floatx4*>(A.x3 + ro * EMB + k * 16 + 4 * g) = x3[k];
+            }
+        }
+        // GI = [b_ir + b_hr + W_ir x | b_iz + b_hz + W_iz x | b_in + W_in x]
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            floatx4 acc[4];
+            bias_init<4>(acc, q < 2 ? A.P + L.brz + q * EMB : A.P + L.bih + 2 * EMB, 0, lane);
+            mm_reg<4, 4>(acc, A.P + L.wih + (int64_t)q * EMB * EMB, EMB, 0, x3, lane);
+            if (valid) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *reinterpret_cast<floatx4*>(A.gi + ro * 3 * EMB + q * EMB + k * 16 + 4 * g) = acc[k];
+            }
+        }
+    }
+}
+
+// ---- GRU recurrence (online rows then target rows) ------------------------------------------------------
+// grid (ntiles_on + ntiles_tg), 4 waves: wave w owns hidden chunk w, its W_hh rows in VGPRs.
+__global__ void __launch_bounds__(256) rec_kernel(RCfg c, RAgent L, const float* __restrict__ Pon,
+                                                  const float* __restrict__ Ptg, const float* __restrict__ gi_on,
+                                                  const float* __restrict__ gi_tg, float* __restrict__ hs_on,
+                                                  float* __restrict__ hs_tg, float* __restrict__ ws_gr,
+                                                  float* __restrict__ ws_gz, float* __restrict__ ws_gn,
+                                                  float* __restrict__ ws_ghn) {
+    constexpr int H = EMB, HC = 4;
+    __shared__ __attribute__((aligned(16))) float hs[2][16 * LDX];
+    const int nt_on = (c.Ron + 15) / 16;
+    const bool online = (int)blockIdx.x < nt_on;
+    const int tile = online ? blockIdx.x : blockIdx.x - nt_on;
+    const int R = online ? c.Ron : c.Rtg;
+    const float* P = online ? Pon : Ptg;
+    const float* gi = online ? gi_on : gi_tg;
+    float* hsg = online ? hs_on : hs_tg;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int r = tile * 16 + col;
+    const bool valid = r < R;
+    const int f0 = w * 16 + 4 * g;
+    floatx4 wr[3][HC];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int kc = 0; kc < HC; ++kc) wr[q][kc] = ld4(P + L.whh + (int64_t)(q * H + w * 16 + col) * H + kc * 16 + 4 * g);
+    const floatx4 bhn = ld4(P + L.bhh + 2 * H + f0);
+    for (int i = tid; i < 16 * LDX; i += blockDim.x) hs[0][i] = 0.f;
+    if (valid) *reinterpret_cast<floatx4*>(hsg + (int64_t)r * H + f0) = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int rr = valid ? r : 0;
+    auto gi_at = [&](int t, int q) { return ld4(gi + ((int64_t)t * R + rr) * 3 * H + q * H + f0); };
+    floatx4 nr = gi_at(0, 0), nz = gi_at(0, 1), nn = gi_at(0, 2);
+    __syncthreads();
+    int cur = 0;
+    for (int t = 0; t < c.T; ++t) {
+        floatx4 ar = nr, az = nz;
+        const floatx4 gin = nn;
+        if (t + 1 < c.T) {
+            nr = gi_at(t + 1, 0);
+            nz = gi_at(t + 1, 1);
+            nn = gi_at(t + 1, 2);
+        }
+        floatx4 ahn = bhn;
+        const float* hrow = hs[cur] + col * LDX + 4 * g;
+#pragma unroll
+        for (int kc = 0; kc < HC; ++kc) {
+            const floatx4 hin = ld4(hrow + kc * 16);
+            ar = mfma_chunk(wr[0][kc], hin, ar);
+            az = mfma_chunk(wr[1][kc], hin, az);
+            ahn = mfma_chunk(wr[2][kc], hin, ahn);
+        }
+        const floatx4 hp = ld4(hs[cur] + col * LDX + f0);
+        floatx4 rg, zg, ng, hn;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            rg[q] = sigm(ar[q]);
+            zg[q] = sigm(az[q]);
+            ng[q] = tanhf(gin[q] + rg[q] * ahn[q]);
+            hn[q] = ng[q] + zg[q] * (hp[q] - ng[q]);
+        }
+        *reinterpret_cast<floatx4*>(hs[cur ^ 1] + col * LDX + f0) = hn;
+        if (valid) {
+            const int64_t o = ((int64_t)t * R + r) * H + f0;
+            *reinterpret_cast<floatx4*>(hsg + o + (int64_t)R * H) = hn;
+            if (online) {
+                *reinterpret_cast<floatx4*>(ws_gr + o) = rg;
+                *reinterpret_cast<floatx4*>(ws_gz + o) = zg;
+                *reinterpret_cast<floatx4*>(ws_gn + o) = ng;
+                *reinterpret_cast<floatx4*>(ws_ghn + o) = ahn;
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+}
+
+// agent row r of a net -> (b, n); copy = r / (B * NA)
+__device__ __forceinline__ void row_bn(const RCfg& c, int r, int& b, int& n) {
+    n = r % c.NA;
+    b = (r / c.NA) % c.B;
+}
+
+// fc3 for every (t, row): grid (ntiles_max, T, 2), Ap/16 waves (wave = action tile); masked agents -> 0
+__global__ void __launch_bounds__(128) q_kernel(RCfg c, MlgEntityBatch bt, RAgent L, const float* __restrict__ Pon,
+                                                const float* __restrict__ Ptg, const float* __restrict__ hs_on,
+                                                const float* __restrict__ hs_tg, float* __restrict__ mac,
+                                                float* __restrict__ tmac) {
+    const bool online = blockIdx.z == 0;
+    const int R = online ? c.Ron : c.Rtg;
+    const int tile = blockIdx.x, t = blockIdx.y;
+    if (tile * 16 >= R) return;
+    const float* P = online ? Pon : Ptg;
+    const float* hsg = (online ? hs_on : hs_tg) + (int64_t)(t + 1) * R * EMB;
+    float* qout = online ? mac : tmac;
+    const int lane = threadIdx.x & 63, at = threadIdx.x >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int r = tile * 16 + col;
+    const bool valid = r < R;
+    int b = 0, n = 0;
+    if (valid) row_bn(c, r, b, n);
+    const bool dead = valid && bt.entity_mask[(eslot(bt, b) * bt.T1 + t) * c.NE + n] != 0;
+    floatx4 q[1];
+    bias_init<1>(q, P + L.b3, at, lane);
+    mm_ptr<1>(q, P + L.w3, EMB, at, hsg + (int64_t)(valid ? r : 0) * EMB, EMB / 16, lane);
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int a = at * 16 + 4 * g + k;
+            if (a < c.A) qout[((int64_t)t * R + r) * c.A + a] = dead ? 0.f : q[0][k];
+        }
+    }
+}
+
+// ---- hypernet forward: grid (I, 8): y = k + 4 * net -------------------------------------------------------
+struct HypPtrs {
+    const float* Pon[4];
+    const float* Ptg[4];
+    float* x1m[4];
+    float* qkvm[4];
+    float* Pm[4];
+    float* om[4];
+    float* x2m[4];
+    float* X[4];
+    float* Xtg[4];
+};
+
+__global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
+                                                       RHyper L, const float* __restrict__ ein, HypPtrs hp) {
+    __shared__ float s_ein[NE * LDI];
+    __shared__ float s_x1[NE * LDX];
+    __shared__ float s_qkv[NE * LDQ];
+    __shared__ float s_o[32 * LDX];
+    __shared__ uint32_t s_m[3][16];
+    __shared__ uint32_t s_dead;
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x, k = blockIdx.y & 3, net = blockIdx.y >> 2;
+    const int b = i / c.T, t = i % c.T;
+    if (t == c.T - 1) {  // no mixer item: zero the wgrad inputs of the online item (never NaN garbage)
+        if (!net) {
+            for (int q = lane; q < NE * EMB; q += 64) hp.x1m[k][(int64_t)i * NE * EMB + q] = 0.f;
+            for (int v = 0; v < nvar(k); ++v)
+                for (int q = lane; q < NAS * EMB; q += 64) {
+                    hp.om[k][((int64_t)v * c.I + i) * NAS * EMB + q] = 0.f;
+                    hp.x2m[k][((int64_t)v * c.I + i) * NAS * EMB + q] = 0.f;
+                }
+        }
+        return;
+    }
+    const int ts = net ? t + 1 : t;
+    const int ie = b * c.T + ts;
+    const float* P = net ? hp.Ptg[k] : hp.Pon[k];
+    const int V = net ? 1 : nvar(k);
+    for (int q = lane; q < 32 * LDX; q += 64) s_o[q] = 0.f;
+    if (lane < 16) {
+        const int q = lane;
+        const uint32_t em = em_bits(c, bt, b, ts);
+        const uint32_t dead = dead_bits(c, em);
+        // default AttentionHyperNet mask: agent q masked or entity j masked (flex_qmix.py:41-45)
+        s_m[0][q] = (q < NAS && ((dead >> q) & 1u)) ? 0xFFFFu : (em & 0xFFFFu);
+        if (V == 3) {
+            uint32_t gA, gB, em0;
+            group_bits(c, bt, groupA, b, gA, gB, em0);
+            const uint32_t it = interact_row(gA, gB, q), ac = active_row(em0, q);
+            s_m[1][q] = (((~it) & 0xFFFFu) | ac) & 0xFFFFu;  // W mask: within | active
+            s_m[2][q] = (it | ac) & 0xFFFFu;                 // I mask: interact | active
+        }
+        if (q == 0) s_dead = dead;
+    }
+    for (int q = lane; q < NE * c.K1; q += 64) s_ein[(q / c.K1) * LDI + q % c.K1] = ein[(int64_t)ie * NE * c.K1 + q];
+    wave_sync();
+    dense_lds<true>(P + L.w1, L.K1, P + L.b1, EMB / 16, s_ein, LDI, L.K1 / 16, s_x1, LDX, lane);
+    wave_sync();
+    dense_lds<false>(P + L.win, EMB, nullptr, 3 * EMB / 16, s_x1, LDX, EMB / 16, s_qkv, LDQ, lane);
+    wave_sync();
+    if (!net) {
+        for (int q = lane; q < NE * EMB; q += 64) hp.x1m[k][(int64_t)i * NE * EMB + q] = s_x1[(q / EMB) * LDX + q % EMB];
+        for (int q = lane; q < NE * 3 * EMB; q += 64)
+            hp.qkvm[k][(int64_t)i * NE * 3 * EMB + q] = s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)];
+    }
+    for (int v = 0; v < V; ++v)
+        attn_fwd(s_qkv, s_m[v], c.NA, c.NE, s_o + v * NAS * LDX, LDX,
+                 net ? nullptr : hp.Pm[k] + ((int64_t)v * c.I + i) * 1024, lane);
+    wave_sync();
+    const int col = lane & 15, g = lane >> 4;
+    const uint32_t dead = s_dead;
+    for (int tile = 0; tile * 16 < V * NAS; ++tile) {
+        const int row = tile * 16 + col, v = row >> 3, n = row & 7;
+        const bool rdead = (dead >> n) & 1u;
+        floatx4 x2[4];
+        bias_init<4>(x2, P + L.bout, 0, lane);
+        mm_lds<4>(x2, P + L.wout, EMB, 0, s_o + tile * 16 * LDX, LDX, EMB / 16, lane);
+        if (rdead) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x2[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        floatx4 X[2];
+        bias_init<2>(X, P + L.b2, 0, lane);
+        mm_reg<2, 4>(X, P + L.w2, EMB, 0, x2, lane);
+        if (rdead) X[0] = X[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (v >= V) continue;  // rows n >= NA are written too (zeros): they are wgrad rows
+        const int64_t ro = ((int64_t)v * c.I + i) * NAS + n;
+        if (!net) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                *reinterpret_cast<floatx4*>(hp.om[k] + ro * EMB + q * 16 + 4 * g) = ld4(s_o + row * LDX + q * 16 + 4 * g);
+                *reinterpret_cast<floatx4*>(hp.x2m[k] + ro * EMB + q * 16 + 4 * g) = x2[q];
+            }
+        }
+        float* Xo = net ? hp.Xtg[k] + ((int64_t)i * NAS + n) * EM : hp.X[k] + ro * EM;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) *reinterpret_cast<floatx4*>(Xo + q * 16 + 4 * g) = X[q];
+    }
+}
+
+// ---- mixing, TD and the mixing backward: one wave per item ------------------------------------------------
+struct MixIO {
+    const float* X[4];
+    const float* Xtg[4];
+    float* dX[4];
+    const float *mac, *tmac, *msum;
+    float *dq, *d2, *part;
+};
+
+__device__ __forceinline__ float sum32(float v) {  // sum over lanes 0..31 (every lane of the half gets it)
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) v += __shfl_xor(v, m);
+    return v;
+}
+__device__ __forceinline__ float max32(float v) {
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) v = fmaxf(v, __shfl_xor(v, m));
+    return v;
+}
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+__device__ __forceinline__ float elu_d(float x) { return x > 0.f ? 1.f : expf(x); }
+
+// mixing weight transform over the embed dim (lane = e): |x| or softmax (flex_qmix.py:96-99,103-106)
+__device__ __forceinline__ float mw(float x, int softmax) {
+    if (!softmax) return fabsf(x);
+    const float m = max32(x);
+    const float ex = expf(x - m);
+    return ex / sum32(ex);
+}
+// backward of mw given the forward output y and input x
+__device__ __forceinline__ float mw_bwd(float dy, float y, float x, int softmax) {
+    if (!softmax) return dy * sgnf(x);
+    return y * (dy - sum32(y * dy));
+}
+
+__global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, MixIO io) {
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x;
+    const int b = i / c.T, t = i % c.T;
+    const int e = lane & 31;
+    const int NA = c.NA;
+    float* part = io.part + (int64_t)i * 8;
+    if (t == c.T - 1) {
+        if (lane < 8) part[lane] = 0.f;
+        for (int k = 0; k < 4; ++k)
+            for (int v = 0; v < nvar(k); ++v)
+                for (int q = lane; q < NAS * EM; q += 64) io.dX[k][((int64_t)v * c.I + i) * NAS * EM + q] = 0.f;
+        return;
+    }
+    const int64_t srow = eslot(bt, b) * bt.T1;
+    const uint32_t dead = dead_bits(c, em_bits(c, bt, b, t));
+    // ---- chosen Q of the three copies, target max (double Q) ----
+    float caq[3][NAS], tmax[NAS];
+    int act[NAS];
+    for (int n = 0; n < NAS; ++n) {
+        act[n] = 0;
+        tmax[n] = 0.f;
+        for (int cc = 0; cc < 3; ++cc) caq[cc][n] = 0.f;
+        if (n >= NA) continue;
+        const int a = (int)bt.actions[(srow + t) * NA + n];
+        act[n] = a;
+        for (int cc = 0; cc < 3; ++cc)
+            caq[cc][n] = io.mac[((int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * NA + n) * c.A + a];
+        const int32_t* av = bt.avail + ((srow + t + 1) * NA + n) * c.A;
+        const float* tq = io.tmac + ((int64_t)(t + 1) * c.Rtg + (int64_t)b * NA + n) * c.A;
+        if (c.double_q) {
+            const float* mq = io.mac + ((int64_t)(t + 1) * c.Ron + (int64_t)b * NA + n) * c.A;
+            float bv = 0.f;
+            int bi = -1;
+            for (int a2 = 0; a2 < c.A; ++a2) {
+                const float v = av[a2] == 0 ? -9999999.f : mq[a2];
+                if (bi < 0 || amax_better(v, a2, bv, bi)) { bv = v; bi = a2; }
+            }
+            tmax[n] = av[bi] == 0 ? -9999999.f : tq[bi];
+        } else {
+            float bv = 0.f;
+            for (int a2 = 0; a2 < c.A; ++a2) {
+                const float v = av[a2] == 0 ? -9999999.f : tq[a2];
+                bv = a2 == 0 ? v : fmaxf(bv, v);
+            }
+            tmax[n] = bv;
+        }
+    }
+    const float invN = 1.f / (float)NA, invNE = 1.f / ((float)NA * (float)EM);
+    // column e of each hypernet output over the agent rows
+    auto col_sum = [&](const float* X) {
+        float s = 0.f;
+        for (int n = 0; n < NA; ++n) s += X[n * EM + e];
+        return s;
+    };
+    // ---- target mixer (flex_qmix on the t + 1 entities, target weights) ----
+    float y_tg;
+    {
+        const float* Xw1 = io.Xtg[0] + (int64_t)i * NAS * EM;
+        float pre = col_sum(io.Xtg[2] + (int64_t)i * NAS * EM) * invN;  // b1
+        for (int n = 0; n < NA; ++n) pre += tmax[n] * mw(Xw1[n * EM + e], c.softmax);
+        const float hid = elu_f(pre);
+        const float wf = mw(col_sum(io.Xtg[1] + (int64_t)i * NAS * EM) * invN, c.softmax);
+        const float vsum = sum32(col_sum(io.Xtg[3] + (int64_t)i * NAS * EM));
+        y_tg = sum32(hid * wf) + vsum * invNE;
+    }
+    // ---- online mixer: plain and imagined ----
+    const float* XP = io.X[0] + ((int64_t)0 * c.I + i) * NAS * EM;
+    const float* XW = io.X[0] + ((int64_t)1 * c.I + i) * NAS * EM;
+    const float* XI = io.X[0] + ((int64_t)2 * c.I + i) * NAS * EM;
+    const float* Xwf = io.X[1] + (int64_t)i * NAS * EM;
+    const float* Xb1 = io.X[2] + (int64_t)i * NAS * EM;
+    const float* XV = io.X[3] + (int64_t)i * NAS * EM;
+    const float b1 = col_sum(Xb1) * invN;
+    const float wfpre = col_sum(Xwf) * invN;
+    const float wf = mw(wfpre, c.softmax);
+    const float vv = sum32(col_sum(XV)) * invNE;
+    float w1P[NAS], w1W[NAS], w1I[NAS];
+    float preP = b1, preI = b1;
+    for (int n = 0; n < NAS; ++n) {
+        w1P[n] = w1W[n] = w1I[n] = 0.f;
+        if (n >= NA) continue;
+        w1P[n] = mw(XP[n * EM + e], c.softmax);
+        w1W[n] = mw(XW[n * EM + e], c.softmax);
+        w1I[n] = mw(XI[n * EM + e], c.softmax);
+        preP += caq[0][n] * w1P[n];
+    }
+    for (int n = 0; n < NA; ++n) preI += caq[1][n] * w1W[n];
+    for (int n = 0; n < NA; ++n) preI += caq[2][n] * w1I[n];
+    const float hidP = elu_f(preP), hidI = elu_f(preI);
+    const float yP = sum32(hidP * wf) + vv;
+    const float yI = sum32(hidI * wf) + vv;
+    const float r = bt.reward[srow + t];
+    const float term = (float)bt.terminated[srow + t];
+    const float m = emask_at(bt, b, t);
+    const float target = r + c.gamma * (1.f - term) * y_tg;
+    const float tdP = (yP - target) * m, tdI = (yI - target) * m;
+    if (lane == 0) {
+        part[0] = tdP * tdP;
+        part[1] = tdI * tdI;
+        part[2] = fabsf(tdP);
+        part[3] = yP * m;
+        part[4] = target * m;
+        part[5] = m;
+        part[6] = 0.f;
+        part[7] = 0.f;
+    }
+    // ---- backward ----
+    const float msum = io.msum[0];
+    const float gP = 2.f * (1.f - c.lmbda) * tdP * m / msum;
+    const float gI = 2.f * c.lmbda * tdI * m / msum;
+    const float dwf = gP * hidP + gI * hidI;
+    const float dv = gP + gI;
+    const float dpP = gP * wf * elu_d(preP);
+    const float dpI = gI * wf * elu_d(preI);
+    const float db1 = dpP + dpI;
+    const float dwfpre = mw_bwd(dwf, wf, wfpre, c.softmax);
+    float* dXP = io.dX[0] + ((int64_t)0 * c.I + i) * NAS * EM;
+    float* dXW = io.dX[0] + ((int64_t)1 * c.I + i) * NAS * EM;
+    float* dXI = io.dX[0] + ((int64_t)2 * c.I + i) * NAS * EM;
+    float* dXwf = io.dX[1] + (int64_t)i * NAS * EM;
+    float* dXb1 = io.dX[2] + (int64_t)i * NAS * EM;
+    float* dXV = io.dX[3] + (int64_t)i * NAS * EM;
+    float dqP[NAS], dqW[NAS], dqI[NAS];
+    for (int n = 0; n < NAS; ++n) {
+        const bool live = n < NA && !((dead >> n) & 1u);
+        float vP = 0.f, vW = 0.f, vI = 0.f, vwf = 0.f, vb1 = 0.f, vV = 0.f;
+        if (n < NA) {
+            vP = mw_bwd(caq[0][n] * dpP, w1P[n], XP[n * EM + e], c.softmax);
+            vW = mw_bwd(caq[1][n] * dpI, w1W[n], XW[n * EM + e], c.softmax);
+            vI = mw_bwd(caq[2][n] * dpI, w1I[n], XI[n * EM + e], c.softmax);
+            vwf = dwfpre * invN;
+            vb1 = db1 * invN;
+            vV = dv * invNE;
+        }
+        dqP[n] = sum32(w1P[n] * dpP);
+        dqW[n] = sum32(w1W[n] * dpI);
+        dqI[n] = sum32(w1I[n] * dpI);
+        if (lane < 32) {
+            dXP[n * EM + e] = live ? vP : 0.f;
+            dXW[n * EM + e] = live ? vW : 0.f;
+            dXI[n * EM + e] = live ? vI : 0.f;
+            dXwf[n * EM + e] = live ? vwf : 0.f;
+            dXb1[n * EM + e] = live ? vb1 : 0.f;
+            dXV[n * EM + e] = live ? vV : 0.f;
+        }
+    }
+    if (lane < NA) {  // dQ of the chosen actions (masked agents: q was masked_fill'ed -> 0)
+        const int n = lane;
+        const bool live = !((dead >> n) & 1u);
+        const float dd[3] = {dqP[n], dqW[n], dqI[n]};
+        for (int cc = 0; cc < 3; ++cc) {
+            const int64_t row = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * NA + n;
+            const float v = live ? dd[cc] : 0.f;
+            io.dq[row] = v;
+            io.d2[row * c.A + act[n]] = v;
+        }
+    }
+}
+
+// ---- hypernet backward: grid (I, 4), one wave ---------------------------------------------------------------
+struct HypBwd {
+    const float* Pon[4];
+    const float* woutT[4];
+    const float* w2T[4];
+    const float* winT[4];
+    const float* x1m[4];
+    const float* qkvm[4];
+    const float* Pm[4];
+    const float* dX[4];
+    float* doutm[4];
+    float* dqkvm[4];
+    float* dfc1m[4];
+};
+
+__global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c, MlgEntityBatch bt, HypBwd hb) {
+    __shared__ float s_qkv[NE * LDQ];
+    __shared__ float s_dqkv[NE * LDQ];
+    __shared__ float s_do[32 * LDX];
+    __shared__ float s_ds[NH * 16 * NE];
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x, k = blockIdx.y;
+    const int b = i / c.T, t = i % c.T;
+    const int V = nvar(k);
+    const int col = lane & 15, g = lane >> 4;
+    if (t == c.T - 1) {
+        for (int q = lane; q < V * NAS * EMB; q += 64) {
+            const int v = q / (NAS * EMB), rem = q % (NAS * EMB);
+            hb.doutm[k][((int64_t)v * c.I + i) * NAS * EMB + rem] = 0.f;
+        }
+        for (int q = lane; q < NE * 3 * EMB; q += 64) hb.dqkvm[k][(int64_t)i * NE * 3 * EMB + q] = 0.f;
+        for (int q = lane; q < NE * EMB; q += 64) hb.dfc1m[k][(int64_t)i * NE * EMB + q] = 0.f;
+        return;
+    }
+    const uint32_t dead = dead_bits(c, em_bits(c, bt, b, t));
+    for (int q = lane; q < NE * 3 * EMB; q += 64)
+        s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = hb.qkvm[k][(int64_t)i * NE * 3 * EMB + q];
+    for (int q = lane; q < 32 * LDX; q += 64) s_do[q] = 0.f;
+    for (int tile = 0; tile * 16 < V * NAS; ++tile) {
+        const int row = tile * 16 + col, v = row >> 3, n = row & 7;
+        const bool valid = v < V && n < c.NA;
+        const bool rdead = (dead >> n) & 1u;
+        const int64_t ro = ((int64_t)(v < V ? v : 0) * c.I + i) * NAS + n;
+        // dx2 = W2^T dX (dX rows of masked agents are zero already)
+        floatx4 dx2[4];
+        bias_init<4>(dx2, nullptr, 0, lane);
+        mm_ptr<4>(dx2, hb.w2T[k], EM, 0, hb.dX[k] + ro * EM, EM / 16, lane);
+        if (rdead || !valid) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dx2[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (v < V) {  // padding rows (n >= NA) get zeros: they are wgrad rows
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<floatx4*>(hb.doutm[k] + ro * EMB + q * 16 + 4 * g) = dx2[q];
+        }
+        // dO = Wout^T dout
+        floatx4 dO[4];
+        bias_init<4>(dO, nullptr, 0, lane);
+        mm_reg<4, 4>(dO, hb.woutT[k], EMB, 0, dx2, lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st_row(s_do + tile * 16 * LDX, LDX, q, dO[q], lane);
+    }
+    wave_sync();
+    for (int v = 0; v < V; ++v) {
+        const float* Pv = hb.Pm[k] + ((int64_t)v * c.I + i) * 1024;
+        if (v == 0) attn_bwd<false>(s_qkv, Pv, c.NA, s_do + v * NAS * LDX, LDX, s_ds, s_dqkv, lane);
+        else attn_bwd<true>(s_qkv, Pv, c.NA, s_do + v * NAS * LDX, LDX, s_ds, s_dqkv, lane);
+        wave_sync();
+    }
+    for (int q = lane; q < NE * 3 * EMB; q += 64)
+        hb.dqkvm[k][(int64_t)i * NE * 3 * EMB + q] = s_dqkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)];
+    // dx1 = W_in^T dqkv * relu'(x1)
+    floatx4 dx1[4];
+    bias_init<4>(dx1, nullptr, 0, lane);
+    mm_lds<4>(dx1, hb.winT[k], 3 * EMB, 0, s_dqkv, LDQ, 3 * EMB / 16, lane);
+    const float* x1 = hb.x1m[k] + ((int64_t)i * NE + col) * EMB;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const floatx4 xv = ld4(x1 + q * 16 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dx1[q][r] = xv[r] > 0.f ? dx1[q][r] : 0.f;
+        *reinterpret_cast<floatx4*>(hb.dfc1m[k] + ((int64_t)i * NE + col) * EMB + q * 16 + 4 * g) = dx1[q];
+    }
+}
+
+// ---- reverse-time GRU backward of the online rows ------------------------------------------------------------
+__global__ void __launch_bounds__(256) rec_bwd_kernel(RCfg c, MlgEntityBatch bt, RAgent L, const float* __restrict__ P,
+                                                      const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
+                                                      const float* __restrict__ ws_gz, const float* __restrict__ ws_gn,
+                                                      const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
+                                                      float* __restrict__ dgi, float* __restrict__ dgh) {
+    constexpr int H = EMB;
+    constexpr int LDG = 3 * H + 4;
+    constexpr int KC = 3 * H / 16;
+    __shared__ __attribute__((aligned(16))) float sgh[2][16 * LDG];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int r = blockIdx.x * 16 + col;
+    const int R = c.Ron;
+    const bool valid = r < R;
+    int b = 0, n = 0;
+    if (valid) row_bn(c, r, b, n);
+    const int f0 = w * 16 + 4 * g;
+    floatx4 wt[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wt[kc][q] = P[L.whh + (int64_t)(kc * 16 + 4 * g + q) * H + w * 16 + col];
+    const int rr = valid ? r : 0;
+    const int64_t srow = eslot(bt, b) * bt.T1;
+    struct Step {
+        floatx4 rg, zg, ng, ghn, hp, w3;
+        float dq;
+    };
+    auto load_step = [&](int t) {
+        Step s;
+        const int64_t o = ((int64_t)t * R + rr) * H + f0;
+        s.rg = ld4(ws_gr + o);
+        s.zg = ld4(ws_gz + o);
+        s.ng = ld4(ws_gn + o);
+        s.ghn = ld4(ws_ghn + o);
+        s.hp = ld4(ws_hs + o);
+        s.dq = 0.f;
+        s.w3 = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (t < c.T - 1) {
+            s.dq = dqv[(int64_t)t * R + rr];
+            const int a = (int)bt.actions[(srow + t) * c.NA + n];
+            s.w3 = ld4(P + L.w3 + (int64_t)a * H + f0);
+        }
+        return s;
+    };
+    floatx4 dh = {0.f, 0.f, 0.f, 0.f};
+    Step nx = load_step(c.T - 1);
+    int cur = 0;
+    for (int t = c.T - 1; t >= 0; --t) {
+        const Step s = nx;
+        if (t > 0) nx = load_step(t - 1);
+        if (valid && t < c.T - 1) dh += s.dq * s.w3;
+        floatx4 drp, dzp, dnp, dghn, dhd;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float dn = dh[q] * (1.f - s.zg[q]);
+            const float dz = dh[q] * (s.hp[q] - s.ng[q]);
+            dhd[q] = dh[q] * s.zg[q];
+            dnp[q] = dn * (1.f - s.ng[q] * s.ng[q]);
+            const float dr = dnp[q] * s.ghn[q];
+            drp[q] = dr * s.rg[q] * (1.f - s.rg[q]);
+            dzp[q] = dz * s.zg[q] * (1.f - s.zg[q]);
+            dghn[q] = dnp[q] * s.rg[q];
+        }
+        float* gh = sgh[cur] + col * LDG;
+        *reinterpret_cast<floatx4*>(gh + f0) = drp;
+        *reinterpret_cast<floatx4*>(gh + H + f0) = dzp;
+        *reinterpret_cast<floatx4*>(gh + 2 * H + f0) = dghn;
+        if (valid) {
+            const int64_t o3 = ((int64_t)t * R + r) * 3 * H + f0;
+            *reinterpret_cast<floatx4*>(dgi + o3) = drp;
+            *reinterpret_cast<floatx4*>(dgi + o3 + H) = dzp;
+            *reinterpret_cast<floatx4*>(dgi + o3 + 2 * H) = dnp;
+            *reinterpret_cast<floatx4*>(dgh + o3) = drp;
+            *reinterpret_cast<floatx4*>(dgh + o3 + H) = dzp;
+            *reinterpret_cast<floatx4*>(dgh + o3 + 2 * H) = dghn;
+        }
+        __syncthreads();
+        floatx4 dprev = dhd;
+        const float* ghr = sgh[cur] + col * LDG + 4 * g;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) dprev = mfma_chunk(wt[kc], ld4(ghr + kc * 16), dprev);
+        dh = dprev;
+        cur ^= 1;
+    }
+}
+
+// ---- agent entity block backward: one wave per item pair --------------------------------------------------
+struct EntBwd {
+    const float *wihT, *w2T, *woutT, *winT;
+    const float *x1, *qkv, *Pw, *x3, *dgi;
+    float *dfc2, *dout, *dqkv, *dfc1;
+};
+
+__global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, EntBwd eb) {
+    __shared__ float s_do[3][16 * LDX];
+    __shared__ float s_qkv[NE * LDQ];
+    __shared__ float s_dqkv[NE * LDQ];
+    __shared__ float s_ds[NH * 16 * NE];
+    __shared__ uint32_t s_dead[2];
+    const int lane = threadIdx.x;
+    const int i0 = blockIdx.x * 2;
+    const int col = lane & 15, g = lane >> 4;
+    if (lane < 2) {
+        const int i = i0 + lane;
+        s_dead[lane] = i < c.I ? dead_bits(c, em_bits(c, bt, i / c.T, i % c.T)) : 0xFFu;
+    }
+    wave_sync();
+    const int e = col >> 3, n = col & 7, i = i0 + e;
+    const bool valid = i < c.I && n < c.NA;
+    const int b = valid ? i / c.T : 0, t = valid ? i % c.T : 0;
+    const uint32_t dead = s_dead[0] | (s_dead[1] << 8);
+    const bool rdead = (dead >> col) & 1u;
+    for (int cc = 0; cc < 3; ++cc) {
+        const int64_t ro = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * c.NA + n;
+        // dx3 = W_ih^T dGI, relu'
+        floatx4 d3[4];
+        bias_init<4>(d3, nullptr, 0, lane);
+        mm_ptr<4>(d3, eb.wihT, 3 * EMB, 0, eb.dgi + (valid ? ro : 0) * 3 * EMB, 3 * EMB / 16, lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const floatx4 xv = ld4(eb.x3 + (valid ? ro : 0) * EMB + q * 16 + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d3[q][r] = (valid && xv[r] > 0.f) ? d3[q][r] : 0.f;
+            if (valid) *reinterpret_cast<floatx4*>(eb.dfc2 + ro * EMB + q * 16 + 4 * g) = d3[q];
+        }
+        // dx2 = W2^T dfc2, post mask -> dout
+        floatx4 d2[4];
+        bias_init<4>(d2, nullptr, 0, lane);
+        mm_reg<4, 4>(d2, eb.w2T, EMB, 0, d3, lane);
+        if (rdead || !valid) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d2[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (valid) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<floatx4*>(eb.dout + ro * EMB + q * 16 + 4 * g) = d2[q];
+        }
+        floatx4 dO[4];
+        bias_init<4>(dO, nullptr, 0, lane);
+        mm_reg<4, 4>(dO, eb.woutT, EMB, 0, d2, lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st_row(s_do[cc], LDX, q, dO[q], lane);
+    }
+    wave_sync();
+    for (int ee = 0; ee < 2; ++ee) {
+        const int ii = i0 + ee;
+        if (ii >= c.I) continue;
+        for (int q = lane; q < NE * 3 * EMB; q += 64)
+            s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = eb.qkv[(int64_t)ii * NE * 3 * EMB + q];
+        wave_sync();
+        for (int cc = 0; cc < 3; ++cc) {
+            const float* Pv = eb.Pw + ((int64_t)cc * c.I + ii) * 1024;
+            if (cc == 0) attn_bwd<false>(s_qkv, Pv, c.NA, s_do[cc] + ee * NAS * LDX, LDX, s_ds, s_dqkv, lane);
+            else attn_bwd<true>(s_qkv, Pv, c.NA, s_do[cc] + ee * NAS * LDX, LDX, s_ds, s_dqkv, lane);
+            wave_sync();
+        }
+        for (int q = lane; q < NE * 3 * EMB; q += 64)
+            eb.dqkv[(int64_t)ii * NE * 3 * EMB + q] = s_dqkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)];
+        floatx4 dx1[4];
+        bias_init<4>(dx1, nullptr, 0, lane);
+        mm_lds<4>(dx1, eb.winT, 3 * EMB, 0, s_dqkv, LDQ, 3 * EMB / 16, lane);
+        const float* x1 = eb.x1 + ((int64_t)ii * NE + col) * EMB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const floatx4 xv = ld4(x1 + q * 16 + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dx1[q][r] = xv[r] > 0.f ? dx1[q][r] : 0.f;
+            *reinterpret_cast<floatx4*>(eb.dfc1 + ((int64_t)ii * NE + col) * EMB + q * 16 + 4 * g) = dx1[q];
+        }
+        wave_sync();
+    }
+}
+
+// ---- clip_grad_norm_ + RMSprop + stats -------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ part, int n_items,
+                                                      const float* __restrict__ msum_p, float* __restrict__ params,
+                                                      float* __restrict__ grads, float* __restrict__ sq, int64_t n_params,
+                                                      float lr, float alpha, float eps, float max_norm, int NA,
+                                                      float lmbda, float* __restrict__ stats,
+                                                      const float* __restrict__ nrm_part, int n_nrm) {
+    __shared__ float red[1024];
+    const int tid = threadIdx.x;
+    float s = 0.f;
+    for (int i = tid; i < n_nrm; i += blockDim.x) s += nrm_part[i];
+    const float norm = sqrtf(mlg::block_sum_1024(s, red));
+    const float coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
+    if (i < n_params) {
+        const float gi = grads[i] * coef;
+        grads[i] = gi;
+        const float a = alpha * sq[i] + (1.f - alpha) * gi * gi;
+        sq[i] = a;
+        params[i] -= lr * gi / (sqrtf(a) + eps);
+    }
+    if (blockIdx.x == 0) {
+        float s5[5];
+        for (int k = 0; k < 5; ++k) {
+            float v = 0.f;
+            for (int j = tid; j < n_items; j += blockDim.x) v += part[(int64_t)j * 8 + k];
+            s5[k] = mlg::block_sum_1024(v, red);
+        }
+        if (tid == 0) {
+            const float ms = msum_p[0];
+            const float loss = s5[0] / ms, im = s5[1] / ms;
+            stats[0] = (1.f - lmbda) * loss + lmbda * im;
+            stats[1] = im;
+            stats[2] = norm;
+            stats[3] = s5[2] / ms;
+            stats[4] = s5[3] / (ms * NA);
+            stats[5] = s5[4] / (ms * NA);
+            stats[6] = ms;
+            stats[7] = 0.f;
+        }
+    }
+}
+
+// ---- host ---------------------------------------------------------------------------------------------------
+RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_tasks, int64_t* n_red) {
+    const RCfg& c = p.c;
+    auto at = [&](int64_t off) { return ws ? ws + off : (float*)nullptr; };
+    auto gp = [&](int64_t off) { return grads ? grads + off : (float*)nullptr; };
+    const RAgent& a = p.La;
+    const int I16 = c.I * NE, TR = c.T * c.Ron;
+    RJobs J;
+    J.n = 0;
+    J.j[J.n++] = mlg::job(at(p.w.dfc1), EMB, at(p.w.ein), c.K1, gp(a.c_w1), gp(a.c_b1), EMB, c.D0, I16);
+    J.j[J.n++] = mlg::job(at(p.w.dqkv), 3 * EMB, at(p.w.x1), EMB, gp(a.c_win), nullptr, 3 * EMB, EMB, I16);
+    J.j[J.n++] = mlg::job(at(p.w.dout), EMB, at(p.w.o), EMB, gp(a.c_wout), gp(a.c_bout), EMB, EMB, TR);
+    J.j[J.n++] = mlg::job(at(p.w.dfc2), EMB, at(p.w.x2), EMB, gp(a.c_w2), gp(a.c_b2), EMB, EMB, TR);
+    J.j[J.n++] = mlg::job(at(p.w.dgi), 3 * EMB, at(p.w.x3), EMB, gp(a.c_wih), gp(a.c_bih), 3 * EMB, EMB, TR);
+    J.j[J.n++] = mlg::job(at(p.w.dgh), 3 * EMB, at(p.w.hs_on), EMB, gp(a.c_whh), gp(a.c_bhh), 3 * EMB, EMB, TR);
+    J.j[J.n++] = mlg::job(at(p.w.d2), c.A, ws ? ws + p.w.hs_on + (int64_t)c.Ron * EMB : nullptr, EMB, gp(a.c_w3),
+                          gp(a.c_b3), c.A, EMB, TR);
+    for (int k = 0; k < 4; ++k) {
+        const RHyper& h = p.Lh;
+        const int64_t G0 = p.n_agent + (int64_t)k * h.c_total;
+        const int rows = nvar(k) * c.I * NAS;
+        J.j[J.n++] = mlg::job(at(p.w.dfc1m[k]), EMB, at(p.w.ein), c.K1, gp(G0 + h.c_w1), gp(G0 + h.c_b1), EMB, c.D0, I16);
+        J.j[J.n++] = mlg::job(at(p.w.dqkvm[k]), 3 * EMB, at(p.w.x1m[k]), EMB, gp(G0 + h.c_win), nullptr, 3 * EMB, EMB, I16);
+        J.j[J.n++] = mlg::job(at(p.w.doutm[k]), EMB, at(p.w.om[k]), EMB, gp(G0 + h.c_wout), gp(G0 + h.c_bout), EMB, EMB,
+                              rows);
+        J.j[J.n++] = mlg::job(at(p.w.dX[k]), EM, at(p.w.x2m[k]), EMB, gp(G0 + h.c_w2), gp(G0 + h.c_b2), EM, EMB, rows);
+    }
+    int64_t slab_part;
+    *slab_floats = mlg::layout_jobs(J, n_tasks, n_red, &slab_part);
+    p.w.nrm = p.w.slab + slab_part;
+    return J;
+}
+
+int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs* bufs, hipStream_t s) {
+    const RCfg& c = p.c;
+    float* ws = bufs->workspace;
+    const MlgEntityBatch& bt = bufs->batch;
+    const float* params = bufs->params;
+    const float* tparams = bufs->target_params;
+    const WsR& w = p.w;
+    auto copy = [&](const CopyJobs& J, const float* src, float* dst) {
+        hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((J.total + 255) / 256)), dim3(256), 0, s, J, src, dst);
+    };
+    auto tr = [&](const float* src, float* dst, int rows, int cols) {
+        hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((rows * cols + 255) / 256)), dim3(256), 0, s, src, dst, rows,
+                           cols);
+    };
+    // ---- pack ----
+    const CopyJobs aj = agent_jobs(p.La), hj = hyper_jobs(p.Lh);
+    copy(aj, params, ws + w.pa_on);
+    copy(aj, tparams, ws + w.pa_tg);
+    const RAgent& La = p.La;
+    tr(params + La.c_win, ws + w.a_winT, 3 * EMB, EMB);
+    tr(params + La.c_wout, ws + w.a_woutT, EMB, EMB);
+    tr(params + La.c_w2, ws + w.a_w2T, EMB, EMB);
+    tr(params + La.c_wih, ws + w.a_wihT, 3 * EMB, EMB);
+    for (int k = 0; k < 4; ++k) {
+        const int64_t G0 = p.n_agent + (int64_t)k * p.Lh.c_total;
+        copy(hj, params + G0, ws + w.ph_on[k]);
+        copy(hj, tparams + G0, ws + w.ph_tg[k]);
+        tr(params + G0 + p.Lh.c_win, ws + w.h_winT[k], 3 * EMB, EMB);
+        tr(params + G0 + p.Lh.c_wout, ws + w.h_woutT[k], EMB, EMB);
+        tr(params + G0 + p.Lh.c_w2, ws + w.h_w2T[k], EM, EMB);
+    }
+    (void)hipMemsetAsync(ws + w.d2, 0, sizeof(float) * (size_t)c.T * c.Ron * c.A, s);
+    (void)hipMemsetAsync(ws + w.dq, 0, sizeof(float) * (size_t)c.T * c.Ron, s);
+    hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + w.msum);
+    const int64_t n_ein = (int64_t)c.I * NE * c.K1;
+    hipLaunchKernelGGL(ein_kernel, dim3((unsigned)((n_ein + 255) / 256)), dim3(256), 0, s, c, bt, ws + w.ein);
+    // ---- agent forward ----
+    AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on};
+    AgentPtrs tg{ws + w.pa_tg, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ws + w.gi_tg};
+    hipLaunchKernelGGL(ent_fwd_kernel, dim3((unsigned)((c.I + 1) / 2), 2), dim3(64), 0, s, c, bt, bufs->groupA, La,
+                       ws + w.ein, on, tg);
+    const int nt_on = (c.Ron + 15) / 16, nt_tg = (c.Rtg + 15) / 16;
+    hipLaunchKernelGGL(rec_kernel, dim3((unsigned)(nt_on + nt_tg)), dim3(256), 0, s, c, La, ws + w.pa_on, ws + w.pa_tg,
+                       ws + w.gi_on, ws + w.gi_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn);
+    hipLaunchKernelGGL(q_kernel, dim3((unsigned)nt_on, (unsigned)c.T, 2), dim3(64 * (c.Ap / 16)), 0, s, c, bt, La,
+                       ws + w.pa_on, ws + w.pa_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.mac, ws + w.tmac);
+    // ---- mixer ----
+    HypPtrs hp;
+    for (int k = 0; k < 4; ++k) {
+        hp.Pon[k] = ws + w.ph_on[k];
+        hp.Ptg[k] = ws + w.ph_tg[k];
+        hp.x1m[k] = ws + w.x1m[k];
+        hp.qkvm[k] = ws + w.qkvm[k];
+        hp.Pm[k] = ws + w.Pm[k];
+        hp.om[k] = ws + w.om[k];
+        hp.x2m[k] = ws + w.x2m[k];
+        hp.X[k] = ws + w.X[k];
+        hp.Xtg[k] = ws + w.Xtg[k];
+    }
+    hipLaunchKernelGGL(hyper_fwd_kernel, dim3((unsigned)c.I, 8), dim3(64), 0, s, c, bt, bufs->groupA, p.Lh, ws + w.ein, hp);
+    MixIO io;
+    for (int k = 0; k < 4; ++k) {
+        io.X[k] = ws + w.X[k];
+        io.Xtg[k] = ws + w.Xtg[k];
+        io.dX[k] = ws + w.dX[k];
+    }
+    io.mac = ws + w.mac;
+    io.tmac = ws + w.tmac;
+    io.msum = ws + w.msum;
+    io.dq = ws + w.dq;
+    io.d2 = ws + w.d2;
+    io.part = ws + w.part;
+    hipLaunchKernelGGL(mix_td_kernel, dim3((unsigned)c.I), dim3(64), 0, s, c, bt, io);
+    HypBwd hb;
+    for (int k = 0; k < 4; ++k) {
+        hb.Pon[k] = ws + w.ph_on[k];
+        hb.woutT[k] = ws + w.h_woutT[k];
+        hb.w2T[k] = ws + w.h_w2T[k];
+        hb.winT[k] = ws + w.h_winT[k];
+        hb.x1m[k] = ws + w.x1m[k];
+        hb.qkvm[k] = ws + w.qkvm[k];
+        hb.Pm[k] = ws + w.Pm[k];
+        hb.dX[k] = ws + w.dX[k];
+        hb.doutm[k] = ws + w.doutm[k];
+        hb.dqkvm[k] = ws + w.dqkvm[k];
+        hb.dfc1m[k] = ws + w.dfc1m[k];
+    }
+    hipLaunchKernelGGL(hyper_bwd_kernel, dim3((unsigned)c.I, 4), dim3(64), 0, s, c, bt, hb);
+    // ---- agent backward ----
+    hipLaunchKernelGGL(rec_bwd_kernel, dim3((unsigned)nt_on), dim3(256), 0, s, c, bt, La, ws + w.pa_on, ws + w.hs_on,
+                       ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.dq, ws + w.dgi, ws + w.dgh);
+    EntBwd eb{ws + w.a_wihT, ws + w.a_w2T, ws + w.a_woutT, ws + w.a_winT, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.x3,
+              ws + w.dgi, ws + w.dfc2, ws + w.dout, ws + w.dqkv, ws + w.dfc1};
+    hipLaunchKernelGGL(ent_bwd_kernel, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt, eb);
+    // ---- weight gradients, clip, RMSprop ----
+    int64_t slab_floats, n_red;
+    int n_tasks;
+    RJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
+    hipLaunchKernelGGL(mlg::wgrad_kernel<MJ>, dim3((unsigned)((n_tasks + 3) / 4)), dim3(256), 0, s, J, ws + w.slab);
+    const int n_red_blocks = (int)((n_red + 255) / 256);
+    hipLaunchKernelGGL(mlg::wgrad_reduce_kernel<MJ>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + w.slab,
+                       ws + p.w.nrm);
+    const int64_t n_par = p.n_agent + p.n_mixer;
+    hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + w.part, c.I,
+                       ws + w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr, cfg->optim_alpha,
+                       cfg->optim_eps, cfg->grad_norm_clip, c.NA, c.lmbda, bufs->stats, ws + p.w.nrm, n_red_blocks);
+    return mlg::check_launch("refil_train");
+}
+
+}  // namespace
+
+extern "C" int64_t mlg_refil_param_counts(const MlgRefilLearnerCfg* c, int64_t* n_agent, int64_t* n_mixer) {
+    if (check_cfg(c)) return -1;
+    Plan p = make_plan(c, c->T);
+    if (n_agent) *n_agent = p.n_agent;
+    if (n_mixer) *n_mixer = p.n_mixer;
+    return p.n_agent + p.n_mixer;
+}
+
+extern "C" int64_t mlg_refil_workspace_floats(const MlgRefilLearnerCfg* c) {
+    if (check_cfg(c)) return -1;
+    Plan p = make_plan(c, c->T);
+    int64_t slab, n_red;
+    int tasks;
+    make_jobs(p, nullptr, nullptr, &slab, &tasks, &n_red);
+    return p.w.total + slab;
+}
+
+extern "C" int mlg_refil_train(const MlgRefilLearnerCfg* c, const MlgRefilLearnerBufs* b, void* stream) {
+    if (check_cfg(c)) return 1;
+    MLG_REQUIRE(b && b->params && b->grads && b->square_avg && b->target_params && b->workspace && b->stats && b->groupA,
+                "refil_train: null buffer");
+    const MlgEntityBatch& bt = b->batch;
+    MLG_REQUIRE(bt.entities && bt.obs_mask && bt.entity_mask && bt.actions && bt.avail && bt.reward && bt.terminated &&
+                    bt.actions_onehot && bt.filled, "refil_train: batch has null tensors");
+    MLG_REQUIRE(bt.B == c->B && bt.T1 >= c->T, "refil_train: batch B=%d T1=%d vs cfg B=%d T=%d", bt.B, bt.T1, c->B, c->T);
+    Plan p = make_plan(c, bt.T1);
+    return run_train(p, c, b, (hipStream_t)stream);
+}

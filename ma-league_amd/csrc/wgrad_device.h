@@ -1,0 +1,162 @@
+// wgrad_device.h -- weight gradients as job lists, shared by the QMIX and REFIL learners:
+// dW[M][K] = sum_rows delta[row][m] x[row][k], db[m] = sum_rows delta[row][m], split over 256-row chunks (one wave
+// per (job, 16x16 tile, chunk), MFMA with the row index as K) and summed over chunks in a fixed order
+// (deterministic). The reduce pass also emits per-block sums of squares for clip_grad_norm_.
+#pragma once
+#include "mlg_device.h"
+
+namespace mlg {
+
+constexpr int WCH = 256;  // rows per wgrad chunk
+
+// ================================================================================================
+// weight gradients: dW[M][K] = sum_rows delta[row][m] x[row][k], db[m] = sum_rows delta[row][m]
+struct WJob {
+    const float* delta;
+    const float* x;
+    float* dw;
+    float* db;
+    int64_t ldd, ldx;
+    int M, K, rows, mt, nt, chunks;
+    int task0;  // first task index
+    int64_t slab0;
+};
+template <int MJ>
+struct WJobsT {
+    WJob j[MJ];
+    int n;
+};
+
+template <int MJ>
+__device__ __forceinline__ int find_job(const WJobsT<MJ>& J, int task) {
+    int k = 0;
+    while (k + 1 < J.n && J.j[k + 1].task0 <= task) ++k;
+    return k;
+}
+
+// one wave per (job, m-tile, n-tile, row chunk); partial tile (+ bias partial when nt == 0) -> slab
+template <int MJ>
+__global__ void __launch_bounds__(256) wgrad_kernel(WJobsT<MJ> J, float* __restrict__ slab) {
+    const int lane = threadIdx.x & 63;
+    const int task = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (task >= J.j[J.n - 1].task0 + J.j[J.n - 1].mt * J.j[J.n - 1].nt * J.j[J.n - 1].chunks) return;
+    const WJob jb = J.j[find_job(J, task)];
+    const int local = task - jb.task0;
+    const int ch = local % jb.chunks, tt = local / jb.chunks;
+    const int mt = tt / jb.nt, nt = tt % jb.nt;
+    const int col = lane & 15, g = lane >> 4;
+    const int m = mt * 16 + col, k = nt * 16 + col;
+    const int r0 = ch * WCH, r1 = min(jb.rows, r0 + WCH);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    const bool mv = m < jb.M, kv = k < jb.K;
+    for (int rr = r0; rr < r1; rr += 4) {
+        const int row = rr + g;
+        const bool rv = row < r1;
+        const float a = (mv && rv) ? jb.delta[(int64_t)row * jb.ldd + m] : 0.f;
+        const float xv = (kv && rv) ? jb.x[(int64_t)row * jb.ldx + k] : 0.f;
+        acc = mfma4(a, xv, acc);
+        bsum += a;
+    }
+    float* out = slab + jb.slab0 + ((int64_t)tt * jb.chunks + ch) * 272;
+    // D layout: reg q -> (m = mt*16 + 4g + q, k = nt*16 + col)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(4 * g + q) * 16 + col] = acc[q];
+    bsum += __shfl_xor(bsum, 16);
+    bsum += __shfl_xor(bsum, 32);
+    if (g == 0) out[256 + col] = bsum;
+}
+
+// fixed-order sum over chunks -> dW, db
+__device__ __forceinline__ float block_sum_1024(float v, float* red) {
+    // deterministic tree sum over blockDim.x (power of two <= 1024) threads; result in every thread
+    const int tid = threadIdx.x;
+    red[tid] = v;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (tid < w) red[tid] += red[tid + w];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// slab partials -> dW / db; every block also emits the sum of squares of the gradients it wrote
+template <int MJ>
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(WJobsT<MJ> J, const float* __restrict__ slab,
+                                                           float* __restrict__ nrm_part) {
+    __shared__ float red[256];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (job, tile, 272)
+    int64_t acc = 0;
+    float sq = 0.f;
+    for (int q = 0; q < J.n; ++q) {
+        const WJob& jb = J.j[q];
+        const int64_t n_el = (int64_t)jb.mt * jb.nt * 272;
+        if (i >= acc && i < acc + n_el) {
+            const int64_t loc = i - acc;
+            const int tt = (int)(loc / 272), e = (int)(loc % 272);
+            const int mt = tt / jb.nt, nt = tt % jb.nt;
+            float s = 0.f;
+            const float* base = slab + jb.slab0 + (int64_t)tt * jb.chunks * 272 + e;
+            for (int ch = 0; ch < jb.chunks; ++ch) s += base[(int64_t)ch * 272];
+            if (e < 256) {
+                const int m = mt * 16 + e / 16, k = nt * 16 + e % 16;
+                if (m < jb.M && k < jb.K) {
+                    jb.dw[(int64_t)m * jb.K + k] = s;
+                    sq = s * s;
+                }
+            } else if (nt == 0 && jb.db) {
+                const int m = mt * 16 + (e - 256);
+                if (m < jb.M) {
+                    jb.db[m] = s;
+                    sq = s * s;
+                }
+            }
+            break;
+        }
+        acc += n_el;
+    }
+    const float bs = block_sum_1024(sq, red);
+    if (threadIdx.x == 0) nrm_part[blockIdx.x] = bs;
+}
+
+
+inline WJob job(const float* delta, int64_t ldd, const float* x, int64_t ldx, float* dw, float* db, int M, int K, int rows) {
+    WJob j;
+    j.delta = delta;
+    j.x = x;
+    j.dw = dw;
+    j.db = db;
+    j.ldd = ldd;
+    j.ldx = ldx;
+    j.M = M;
+    j.K = K;
+    j.rows = rows;
+    j.mt = (M + 15) / 16;
+    j.nt = (K + 15) / 16;
+    j.chunks = (rows + WCH - 1) / WCH;
+    j.task0 = 0;
+    j.slab0 = 0;
+    return j;
+}
+
+// task / slab offsets of a job list; returns the slab floats (partials + per-block norm partials) and the task count
+template <int MJ>
+inline int64_t layout_jobs(WJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t* slab_part) {
+    int tasks = 0;
+    int64_t slab = 0, red = 0;
+    for (int q = 0; q < J.n; ++q) {
+        J.j[q].task0 = tasks;
+        J.j[q].slab0 = slab;
+        tasks += J.j[q].mt * J.j[q].nt * J.j[q].chunks;
+        slab += (int64_t)J.j[q].mt * J.j[q].nt * J.j[q].chunks * 272;
+        red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
+    }
+    *n_tasks = tasks;
+    *n_red = red;
+    *slab_part = mlg_align4(slab);
+    return mlg_align4(slab) + mlg_align4((red + 255) / 256);
+}
+
+}  // namespace mlg

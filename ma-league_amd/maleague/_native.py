@@ -91,6 +91,20 @@ class MlgRefilDims(ctypes.Structure):
                                               "rnn_hidden_dim"]]
 
 
+
+class MlgRefilLearnerCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ["B", "T", "n_agents", "n_entities", "entity_shape", "n_actions",
+                                              "entity_last_action", "attn_embed_dim", "attn_n_heads", "rnn_hidden_dim",
+                                              "hypernet_embed", "mixing_embed_dim", "double_q",
+                                              "softmax_mixing_weights", "imagine"]] + \
+               [(n, ctypes.c_float) for n in ["gamma", "lmbda", "lr", "optim_alpha", "optim_eps", "grad_norm_clip"]]
+
+
+class MlgRefilLearnerBufs(ctypes.Structure):
+    _fields_ = [("batch", MlgEntityBatch)] + [(n, ctypes.c_void_p) for n in ["groupA", "params", "grads", "square_avg",
+                                                                           "target_params", "workspace", "stats"]]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
 # name -> (restype, argtypes); mirrors include/maleague.h one for one.
@@ -114,6 +128,9 @@ SIGNATURES = {
     "mlg_refil_pack_agent": (ctypes.c_int, [_P, _P, _P, _P]),
     "mlg_refil_agent_forward": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "mlg_refil_rollout": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P]),
+    "mlg_refil_param_counts": (ctypes.c_int64, [_P, _P, _P]),
+    "mlg_refil_workspace_floats": (ctypes.c_int64, [_P]),
+    "mlg_refil_train": (ctypes.c_int, [_P, _P, _P]),
     "mlg_debug_set_stamps": (ctypes.c_int, [_P]),
     "mlg_last_error": (ctypes.c_char_p, []),
     "mlg_version": (ctypes.c_char_p, []),

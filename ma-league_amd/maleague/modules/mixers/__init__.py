@@ -1,4 +1,5 @@
+from .flex_qmix import AttentionHyperNet, FlexQMixer
 from .qmix import QMixer
 from .vdn import VDNMixer
 
-__all__ = ["QMixer", "VDNMixer"]
+__all__ = ["AttentionHyperNet", "FlexQMixer", "QMixer", "VDNMixer"]

@@ -1,0 +1,109 @@
+"""GPU parity of REFILLearner.train (mlg_refil_train, config 5) against the reference's golden vectors (two
+consecutive REFILLearner.train calls, tests/golden/refil_learner.npz) and against the CPU oracle
+(oracle/refil_ref.py) on episodes produced by the HIP REFIL rollout.
+
+Tolerances (fp32, different summation orders): stats rtol 2e-4; parameters after RMSprop atol 2e-5 (RMSprop's
+first steps move weights by ~lr * sign(g) * const, so this checks sign-level gradient agreement everywhere and
+the magnitudes through the second step).
+"""
+import numpy as np
+import pytest
+import torch
+
+import refil_ref as RR
+from helpers import entity_scheme_for, refil_args
+
+pytestmark = pytest.mark.gpu
+
+
+class _Log:
+    def __init__(self):
+        self.stats = {}
+
+    def log_stat(self, k, v, t):
+        self.stats[k] = v
+
+    def info(self, *a):
+        pass
+
+
+def _batch_from(arrs, device, NE=16, ED=8, NA=8, A=21):
+    from maleague.components.episode_batch import EpisodeBatch
+    B, T1 = arrs["entities"].shape[:2]
+    info = {"n_agents": NA, "n_actions": A, "n_entities": NE, "entity_shape": ED, "episode_limit": T1 - 1}
+    scheme, groups, pre = entity_scheme_for(info, torch)
+    eb = EpisodeBatch(scheme, groups, B, T1, preprocess=pre, device=device)
+    for k, v in arrs.items():
+        eb.data.transition_data[k].copy_(torch.as_tensor(np.asarray(v)))
+    return eb
+
+
+def _learner(eb, agent_p, mixer_p, args):
+    from maleague.controllers import EntityMAC
+    from maleague.learners import REFILLearner
+    mac = EntityMAC(eb.scheme, eb.groups, args)
+    mac.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in agent_p.items()})
+    log = _Log()
+    L = REFILLearner(mac, eb.scheme, log, args, name="home")
+    if mixer_p is not None:
+        msd = {k: torch.as_tensor(np.asarray(v)) for k, v in mixer_p.items()}
+        L.mixer.load_state_dict(msd)
+        L.target_mixer.load_state_dict(msd)
+    L.target_mac.load_state(mac)
+    L.build_optimizer()
+    return L, log
+
+
+def _pre(d, prefix):
+    return {k[len(prefix):]: d[k] for k in d.files if k.startswith(prefix)}
+
+
+def test_refil_learner_two_calls_match_golden(device, golden):
+    d = golden("refil_learner.npz")
+    a = refil_args(device="cuda")
+    eb = _batch_from(_pre(d, "b."), device)
+    L, log = _learner(eb, _pre(d, "p0.agent."), _pre(d, "p0.mixer."), a)
+    for call in range(2):
+        L.train(eb, 0, episode_num=call, groupA=torch.from_numpy(d[f"c{call}.groupA"]))
+        st = L.last_stats
+        for k, v in st.items():
+            np.testing.assert_allclose(v, float(d[f"c{call}.stat.{k}"]), rtol=2e-4, atol=1e-6, err_msg=f"call {call} {k}")
+        for k, v in L.mac.agent.named_parameters():
+            np.testing.assert_allclose(v.detach().cpu().numpy(), d[f"c{call}.agent.{k}"], atol=2e-5, rtol=0,
+                                       err_msg=f"call {call} agent {k}")
+        for k, v in L.mixer.named_parameters():
+            np.testing.assert_allclose(v.detach().cpu().numpy(), d[f"c{call}.mixer.{k}"], atol=2e-5, rtol=0,
+                                       err_msg=f"call {call} mixer {k}")
+
+
+@pytest.mark.parametrize("softmax,double_q", [(False, True), (True, False)])
+def test_refil_learner_matches_oracle_on_hip_rollouts(device, softmax, double_q):
+    """Episodes from the HIP REFIL rollout (variable 3..8 agents, eps 0.3), random group draws, 2 train calls."""
+    from test_gpu_refil import _rollout
+    spec, ag, a0, nb, summ, _ = _rollout(device, B=8, T=30, seed=11, eps=0.3, test_mode=False)
+    T = int(summ["len"].max()) + 1
+    arrs = {k: v[:, :T] for k, v in nb.items() if k != "filled"} | {"filled": nb["filled"][:, :T]}
+    a = refil_args(device="cuda", softmax_mixing_weights=softmax, double_q=double_q)
+    eb = _batch_from(arrs, device)
+    torch.manual_seed(4)
+    from maleague.modules.mixers import FlexQMixer
+    mixer_p = {k: v.detach().cpu().numpy() for k, v in FlexQMixer(refil_args(device="cpu")).state_dict().items()}
+    agent_p = {k: v.detach().cpu().numpy() for k, v in ag.state_dict().items()}
+    L, _ = _learner(eb, agent_p, mixer_p, a)
+    ref = RR.REFILLearnerRef(agent_p, mixer_p, refil_args(device="cpu", softmax_mixing_weights=softmax,
+                                                          double_q=double_q))
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in arrs.items()}
+    g = torch.Generator().manual_seed(7)
+    for call in range(2):
+        groupA = torch.bernoulli(torch.rand(8, 1, 1, generator=g).repeat(1, 1, 16), generator=g).to(torch.uint8)
+        want = ref.train(batch, groupA, episode_num=call)
+        L.train(eb, 0, episode_num=call, groupA=groupA.to(device))
+        got = L.last_stats
+        for k in want:
+            np.testing.assert_allclose(got[k], want[k], rtol=2e-4, atol=1e-5, err_msg=f"call {call} {k}")
+        for k, v in L.mac.agent.named_parameters():
+            np.testing.assert_allclose(v.detach().cpu().numpy(), ref.agent[k].detach().numpy(), atol=2e-5, rtol=0,
+                                       err_msg=f"call {call} agent {k}")
+        for k, v in L.mixer.named_parameters():
+            np.testing.assert_allclose(v.detach().cpu().numpy(), ref.mixer[k].detach().numpy(), atol=2e-5, rtol=0,
+                                       err_msg=f"call {call} mixer {k}")
