@@ -7,6 +7,8 @@ of all ranks / max-over-ranks time.
 
 Modes (--mode auto picks by world size, as BASELINE.json's configs are defined):
   ai        config 2: one learner vs the scripted AI per GPU (N = 1)
+  refil     config 5: REFIL (entity-attention agent, imagined groups, FlexQMixer), 3-8 agents per env padded to 8,
+            4096 envs per GPU vs the scripted AI (entity env variant); N > 1 = independent replicas
   league    config 3 (N = 2: two PFSP self-play learners, opponent swap over RCCL) / config 4 (N >= 4:
             AlphaStar roles, half main players, half main exploiters, historical snapshots): one league player
             per GPU; every --match-len iterations a league iteration exchanges parameters (all_gather) and
@@ -38,18 +40,27 @@ def agent_flops_per_forward(N, d_in, H, A):
     return N * 2 * (d_in * H + 2 * H * 3 * H + H * A)
 
 
+def refil_flops_per_forward(NA, NE, D0, E, H, A, heads=4):
+    """Algorithmic FLOPs of one EntityMAC step per env (entity_rnn_agent.py:32-65 on padded tensors): fc1 and
+    in_trans over all entities, attention for the agent queries, out_trans / fc2 / GRUCell / fc3 per agent."""
+    hd = E // heads
+    att = 2 * heads * NA * NE * hd * 2
+    return (2 * NE * D0 * E + 2 * NE * E * 3 * E + att + 2 * NA * E * E * 2 + NA * 2 * (2 * H * 3 * H)
+            + 2 * NA * H * A)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", default="auto", choices=["auto", "ai", "league"])
+    ap.add_argument("--mode", default="auto", choices=["auto", "ai", "league", "refil"])
     ap.add_argument("--match-len", type=int, default=5, help="league: training iterations per league iteration")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--device", type=int, default=None, help="GPU index for every rank (rehearsal on one GPU)")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--episode-limit", type=int, default=100)
-    ap.add_argument("--plan", default="medium_1h_4t")
+    ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -77,22 +88,32 @@ def main():
     from maleague.runs import MultiAgentExperiment
     from maleague.utils.config import build_config, to_args
 
+    plan = a.plan or ("refil_8" if mode == "refil" else "medium_1h_4t")
     overrides = [f"batch_size_run={a.envs}", "runner=parallel", "buffer_cpu_only=False",
-                 f"env_args.match_build_plan={a.plan}", f"env_args.episode_limit={a.episode_limit}",
+                 f"env_args.match_build_plan={plan}", f"env_args.episode_limit={a.episode_limit}",
                  f"seed={rank}", "learner_log_interval=1000000000", "log_interval=1000000000",
                  "runner_log_interval=1000000000", "test_interval=1000000000000", "t_max=1000000000000",
                  "show_exp_parameters=False", "league_checkpoint_min_steps=20000", "league_checkpoint_max_steps=40000"]
-    cfg = build_config("qmix", "ma", overrides=overrides, device_index=local_rank)
+    if mode == "refil":
+        cfg = build_config("refil", "ma_entity", overrides=overrides, device_index=local_rank)
+    else:
+        cfg = build_config("qmix", "ma", overrides=overrides, device_index=local_rank)
     import numpy as np
     np.random.seed(rank)  # replay sampling (reproducible learning curve -> reproducible episode lengths)
     torch.manual_seed(rank)
     args = to_args(cfg)
     inst = None
-    if mode == "ai":
+    if mode in ("ai", "refil"):
         exp = MultiAgentExperiment(args, MainLogger(log_interval=10 ** 12))
         exp._init_stepper()
-        workload = f"qmix_5v5_{a.plan}_{a.envs}envs_ep{a.episode_limit}"
-        parallelism = f"league{world}"
+        if mode == "refil":
+            ea = args.env_args
+            workload = (f"refil_{plan}_{ea.get('min_agents', 3)}to{ea.get('max_agents', 8)}agents_{a.envs}envs_"
+                        f"ep{a.episode_limit}")
+            parallelism = f"replicas{world}"
+        else:
+            workload = f"qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
+            parallelism = f"league{world}"
     else:
         from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
         lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=8 * world)
@@ -100,10 +121,10 @@ def main():
             roles = league_roles_for(world, args)
             inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="rolebased", role=roles, seed=0)
             n_main = roles.count("main")
-            workload = f"pfsp_league_{n_main}main_{world - n_main}exploiter_qmix_5v5_{a.plan}_{a.envs}envs_ep{a.episode_limit}"
+            workload = f"pfsp_league_{n_main}main_{world - n_main}exploiter_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
         else:
             inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="matchmaking", seed=0)
-            workload = f"selfplay_pfsp_{world}learners_qmix_5v5_{a.plan}_{a.envs}envs_ep{a.episode_limit}"
+            workload = f"selfplay_pfsp_{world}learners_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
         exp = inst.experiment
         parallelism = f"league{world}_rccl"
     stepper = exp.stepper
@@ -157,35 +178,45 @@ def main():
 
     # roofline of the dominant kernel (the rollout): fp32 MFMA-bound agent cell
     info = stepper.get_env_info()
-    sides = 1 if mode == "ai" else 2
+    sides = 2 if mode == "league" else 1
     N, A = info["n_agents"] // sides, info["n_actions"]
-    d_in = info["obs_shape"] + A + N
-    fl = sides * agent_flops_per_forward(N, d_in, 64, A)
+    if mode == "refil":
+        fl = refil_flops_per_forward(N, info["n_entities"], info["entity_shape"] + A, 64, 64, A)
+    else:
+        d_in = info["obs_shape"] + A + N
+        fl = sides * agent_flops_per_forward(N, d_in, 64, A)
     # agent forwards per launch: every env steps len times and records one final action (len + 1 forwards)
     forwards = (local_env_steps + a.steps * B) / a.steps
     avg_kernel_s = sum(ev_ms) / len(ev_ms) / 1e3
     achieved = fl * forwards / avg_kernel_s
     issued = fl / (sides * N) * rows_per_launch / avg_kernel_s if mode == "ai" else None
     traffic = None
-    kernel = "rollout_v2_kernel<64>" if mode == "ai" else "rollout_sp_kernel<64>"
+    kernel = {"ai": "rollout_v2_kernel<64>", "league": "rollout_sp_kernel<64>", "refil": "refil_rollout_kernel"}[mode]
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
             traffic = json.load(f).get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
 
     cpu = None
-    if rank == 0 and world == 1 and mode == "ai" and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and mode in ("ai", "refil") and not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_baseline
-        r = cpu_baseline.run(seconds=a.cpu_seconds, B=64, episode_limit=a.episode_limit,
-                             threads=min(16, os.cpu_count() or 1))
+        threads = min(16, os.cpu_count() or 1)
+        if mode == "refil":
+            r = cpu_baseline.run_refil(seconds=a.cpu_seconds, B=32, episode_limit=a.episode_limit, threads=threads)
+            what = "C entity env + PyTorch-CPU EntityAttentionRNNAgent / REFILLearner (refil_ref)"
+        else:
+            r = cpu_baseline.run(seconds=a.cpu_seconds, B=64, episode_limit=a.episode_limit, threads=threads)
+            what = "oracle stepper + C env + PyTorch-CPU DRQN/QMIX learner"
         cpu = {"value": r["value"], "unit": "env-steps/s", "cores": r["cores"], "kind": "port",
-               "sample": f"{r['runs']} runs x 64 envs (+1 train each), {r['env_steps']} env steps in "
-                         f"{r['seconds']:.1f}s; oracle stepper + C env + PyTorch-CPU DRQN/QMIX learner"}
+               "sample": f"{r['runs']} runs x {r['B']} envs (+1 train each), {r['env_steps']} env steps in "
+                         f"{r['seconds']:.1f}s; {what}"}
     if rank == 0:
         out = {"metric": "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X",
                "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "f32", "data": "synthetic (spec-v1 5v5 battles, random-init QMIX)",
+               "vs_baseline": None, "dtype": "f32",
+               "data": ("synthetic (entity battles, 3-8 agents per env padded to 8, random-init REFIL)"
+                        if mode == "refil" else "synthetic (spec-v1 5v5 battles, random-init QMIX)"),
                "config": {"workload": workload, "mode": mode, "envs_per_gpu": B, "episode_limit": a.episode_limit,
                           "learner_batch": 32, "rnn_hidden_dim": 64, "buffer_size": 5000,
                           "parallelism": parallelism, **({"match_len": a.match_len} if inst else {})},

@@ -16,7 +16,7 @@ from ..components.replay_buffer import ReplayBuffer
 from ..components.transforms import OneHot
 from ..controllers import REGISTRY as mac_REGISTRY
 from ..learners import REGISTRY as learner_REGISTRY
-from ..steppers import REGISTRY as stepper_REGISTRY
+from ..steppers import build_stepper
 
 
 def find_latest_model_path(path: str, load_step: int = 0):
@@ -48,7 +48,7 @@ class MultiAgentExperiment:
             learner.build_optimizer()
 
     def _build_stepper(self, log_start_t=0):
-        return stepper_REGISTRY[self.args.runner](args=self.args, logger=self.logger, log_start_t=log_start_t)
+        return build_stepper(self.args, self.logger, log_start_t)
 
     def _update_args(self, update):
         self.args = SimpleNamespace(**{**vars(self.args), **update})
@@ -56,11 +56,28 @@ class MultiAgentExperiment:
     def _integrate_env_info(self):
         env_scheme = {"n_agents": int(self.env_info["n_agents"]), "n_actions": int(self.env_info["n_actions"]),
                       "state_shape": int(self.env_info["state_shape"])}
+        if getattr(self.args, "entity_scheme", False):
+            env_scheme.update(n_entities=int(self.env_info["n_entities"]),
+                              entity_shape=int(self.env_info["entity_shape"]))
         self._update_args(env_scheme)
         self.stepper.args = self.args
         return env_scheme
 
     def _build_schemes(self):
+        if getattr(self.args, "entity_scheme", False):  # REFIL entity scheme (refil_learner.py:81-100)
+            NE, ED = self.env_info["n_entities"], self.env_info["entity_shape"]
+            scheme = {
+                "entities": {"vshape": (NE, ED)},
+                "obs_mask": {"vshape": (NE, NE), "dtype": torch.uint8},
+                "entity_mask": {"vshape": (NE,), "dtype": torch.uint8},
+                "actions": {"vshape": (1,), "group": "agents", "dtype": torch.long},
+                "avail_actions": {"vshape": (self.env_info["n_actions"],), "group": "agents", "dtype": torch.int},
+                "reward": {"vshape": (1,)},
+                "terminated": {"vshape": (1,), "dtype": torch.uint8},
+            }
+            groups = {"agents": self.args.n_agents}
+            preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=self.args.n_actions)])}
+            return groups, preprocess, scheme
         scheme = {
             "state": {"vshape": self.env_info["state_shape"]},
             "obs": {"vshape": self.env_info["obs_shape"], "group": "agents"},

@@ -41,6 +41,23 @@ BUILTIN = {
         "agent_output_type": "q", "learner": "q", "double_q": True, "mixer": "qmix", "mixing_embed_dim": 32,
         "hypernet_layers": 2, "hypernet_embed": 64, "name": "qmix",
     },
+    # REFIL (config 5): the reference vendors the modules without a config; these are the values of
+    # the golden fixtures (tests/golden/make_refil_golden.py) with the qmix.yaml schedule / buffer.
+    "algs/refil": {
+        "action_selector": "epsilon_greedy", "epsilon_start": 1.0, "epsilon_finish": 0.05,
+        "epsilon_anneal_time": 50000, "runner": "episode", "buffer_size": 5000, "target_update_interval": 200,
+        "agent_output_type": "q", "learner": "refil", "double_q": True, "mixer": "flex_qmix", "mixing_embed_dim": 32,
+        "hypernet_embed": 64, "agent": "imagine_entity_attend_rnn", "mac": "entity", "attn_embed_dim": 64,
+        "attn_n_heads": 4, "pooling_type": None, "softmax_mixing_weights": False, "lmbda": 0.5,
+        "entity_last_action": True, "weight_decay": 0, "name": "refil",
+    },
+    "envs/ma_entity": {
+        "env": "ma_entity", "entity_scheme": True,
+        "env_args": {"grid_size": 20, "match_build_plan": "refil_8", "ai": "basic", "stochastic_spawns": True,
+                     "min_agents": 3, "max_agents": 8, "episode_limit": 100},
+        "test_greedy": True, "test_nepisode": 32, "test_interval": 10000, "log_interval": 10000,
+        "runner_log_interval": 10000, "learner_log_interval": 10000, "t_max": 2050000, "show_exp_parameters": True,
+    },
     "algs/vdn": {
         "action_selector": "epsilon_greedy", "epsilon_start": 1.0, "epsilon_finish": 0.05,
         "epsilon_anneal_time": 50000, "runner": "episode", "buffer_size": 5000, "target_update_interval": 200,

@@ -95,5 +95,117 @@ def run(seconds=15.0, B=64, episode_limit=100, eps=0.05, threads=None, seed=0, b
             "cores": threads, "B": B}
 
 
+def run_refil(seconds=15.0, B=32, episode_limit=100, eps=0.05, threads=None, seed=0, batch_size=32, capacity=256):
+    """Config 5 on the host: the entity env in C (env_ref.c entity variant, one call per env per step), the
+    EntityAttentionRNNAgent step batched over B envs in PyTorch-CPU (refil_ref.entity_agent), epsilon-greedy, the
+    ParallelStepper bookkeeping, and one REFILLearner.train (refil_ref.REFILLearnerRef) per run."""
+    import refil_ref as RR
+    threads = threads or os.cpu_count()
+    torch.set_num_threads(threads)
+    roles, melees = [0, 2, 1, 2, 0, 2, 1, 2], [0, 0, 0, 0, 1, 0, 0, 1]
+    NA, NE, ED = 8, 16, 8
+    A = 5 + NE
+    args = SimpleNamespace(n_agents=NA, n_entities=NE, n_actions=A, entity_shape=ED, attn_embed_dim=64,
+                           attn_n_heads=4, rnn_hidden_dim=64, hypernet_embed=64, mixing_embed_dim=32,
+                           softmax_mixing_weights=False, double_q=True, gamma=0.99, lr=5e-4, optim_alpha=0.99,
+                           optim_eps=1e-5, weight_decay=0, grad_norm_clip=10, target_update_interval=200, lmbda=0.5)
+    torch.manual_seed(seed)
+
+    def lin(o, i, bias=True):
+        m = torch.nn.Linear(i, o, bias=bias)
+        return m.weight.detach().clone(), (m.bias.detach().clone() if bias else None)
+
+    D0 = ED + A
+    ap = {}
+    ap["fc1.weight"], ap["fc1.bias"] = lin(64, D0)
+    ap["attn.in_trans.weight"], _ = lin(192, 64, False)
+    ap["attn.out_trans.weight"], ap["attn.out_trans.bias"] = lin(64, 64)
+    ap["fc2.weight"], ap["fc2.bias"] = lin(64, 64)
+    g = torch.nn.GRUCell(64, 64)
+    ap.update({"rnn.weight_ih": g.weight_ih.detach(), "rnn.weight_hh": g.weight_hh.detach(),
+               "rnn.bias_ih": g.bias_ih.detach(), "rnn.bias_hh": g.bias_hh.detach()})
+    ap["fc3.weight"], ap["fc3.bias"] = lin(A, 64)
+    mp = {}
+    for h in ("hyper_w_1", "hyper_w_final", "hyper_b_1", "V"):
+        mp[f"{h}.fc1.weight"], mp[f"{h}.fc1.bias"] = lin(64, D0)
+        mp[f"{h}.attn.in_trans.weight"], _ = lin(192, 64, False)
+        mp[f"{h}.attn.out_trans.weight"], mp[f"{h}.attn.out_trans.bias"] = lin(64, 64)
+        mp[f"{h}.fc2.weight"], mp[f"{h}.fc2.bias"] = lin(32, 64)
+    learner = RR.REFILLearnerRef(ap, mp, args)
+    envs = [envref.RefEntityEnv(roles, melees, 3, 8, episode_limit=episode_limit, seed=seed, env_index=b)
+            for b in range(B)]
+    T1 = episode_limit + 1
+    rng = np.random.RandomState(seed)
+    buffer = []
+    env_steps, runs, trains = 0, 0, 0
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < seconds:
+        bt = {"entities": np.zeros((B, T1, NE, ED), np.float32), "obs_mask": np.zeros((B, T1, NE, NE), np.uint8),
+              "entity_mask": np.zeros((B, T1, NE), np.uint8), "actions": np.zeros((B, T1, NA, 1), np.int64),
+              "avail_actions": np.zeros((B, T1, NA, A), np.int32), "reward": np.zeros((B, T1, 1), np.float32),
+              "terminated": np.zeros((B, T1, 1), np.uint8), "actions_onehot": np.zeros((B, T1, NA, A), np.float32),
+              "filled": np.zeros((B, T1, 1), np.int64)}
+
+        def observe(b, t):
+            bt["entities"][b, t], bt["obs_mask"][b, t], bt["entity_mask"][b, t] = envs[b].entities()
+            bt["avail_actions"][b, t] = envs[b].avail()
+            bt["filled"][b, t] = 1
+
+        for b in range(B):
+            envs[b].reset()
+            observe(b, 0)
+        status = np.zeros(B, np.int32)  # 0 running, 1 final action pending, 2 done
+        h = torch.zeros(B, NA, 64)
+        t = 0
+        while (status < 2).any():
+            ent = torch.from_numpy(bt["entities"][:, t])
+            la = torch.zeros(B, NE, A)
+            if t > 0:
+                la[:, :NA] = torch.from_numpy(bt["actions_onehot"][:, t - 1])
+            with torch.no_grad():
+                q, hs = RR.entity_agent(learner.agent, torch.cat([ent, la], 2).unsqueeze(1),
+                                        torch.from_numpy(bt["obs_mask"][:, t]).unsqueeze(1),
+                                        torch.from_numpy(bt["entity_mask"][:, t]).unsqueeze(1), h, args)
+            h = hs[:, 0]
+            av = bt["avail_actions"][:, t]
+            qm = np.where(av != 0, q[:, 0].numpy(), -np.inf)
+            acts = qm.argmax(-1)
+            coin = rng.rand(B, NA) < eps
+            for (b, n) in zip(*np.nonzero(coin)):
+                if status[b] < 2:
+                    acts[b, n] = rng.choice(np.nonzero(av[b, n])[0])
+            for b in range(B):
+                if status[b] == 2:
+                    continue
+                bt["actions"][b, t, :, 0] = acts[b]
+                bt["actions_onehot"][b, t, np.arange(NA), acts[b]] = 1.0
+                if status[b] == 1:
+                    status[b] = 2
+                    continue
+                rew, done, _ = envs[b].step(acts[b])
+                env_steps += 1
+                bt["reward"][b, t] = rew[0]
+                bt["terminated"][b, t] = done
+                observe(b, t + 1)
+                if done:
+                    status[b] = 1
+            t += 1
+        runs += 1
+        for b in range(B):
+            buffer.append({k: v[b] for k, v in bt.items()})
+        del buffer[:-capacity]
+        if len(buffer) >= batch_size:
+            idx = rng.choice(len(buffer), batch_size, replace=False)
+            smp = {k: torch.from_numpy(np.stack([buffer[i][k] for i in idx])) for k in buffer[0]}
+            T = int(smp["filled"].sum(1).max())
+            smp = {k: v[:, :T].clone() for k, v in smp.items()}
+            groupA = torch.bernoulli(torch.rand(batch_size, 1, 1).repeat(1, 1, NE)).to(torch.uint8)
+            learner.train(smp, groupA, runs * B)
+            trains += 1
+    elapsed = time.perf_counter() - t_start
+    return {"value": env_steps / elapsed, "env_steps": env_steps, "seconds": elapsed, "runs": runs, "trains": trains,
+            "cores": threads, "B": B}
+
+
 if __name__ == "__main__":
     print(run(seconds=10))
