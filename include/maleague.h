@@ -244,6 +244,25 @@ int mlg_refil_agent_forward(const MlgRefilDims *d, const float *packed, const fl
 int mlg_refil_rollout(const MlgEntityEnvSpec *spec, MlgEnvState *st, const MlgRefilDims *d, const float *packed,
                       MlgEntityBatch *batch, MlgRunInfo *info, float epsilon, int32_t test_mode, void *stream);
 
+/* EntityAttentionLayer.forward (src/marl/modules/layers/attention.py:24-79; in = embed = out = 64, 4 heads) over bs
+ * items: x [bs][ne][64], pre_mask [bs][nq][ne], post_mask [bs][nq] (uint8, 1 = masked) -> y [bs][nq][64]. With
+ * gy != nullptr also the backward of sum(y * gy): dx [bs][ne][64] written, dw_in [192][64], dw_out [64][64],
+ * db_out [64] accumulated (atomic adds; caller zeroes). */
+int mlg_refil_attention(const float *w_in, const float *w_out, const float *b_out, const float *x,
+                        const uint8_t *pre_mask, const uint8_t *post_mask, int32_t bs, int32_t ne, int32_t nq,
+                        int32_t n_heads, float *y, const float *gy, float *dx, float *dw_in, float *dw_out,
+                        float *db_out, void *stream);
+
+/* FlexQMixer (flex_qmix.py:55-117): packed = 4 AttentionHyperNet blocks from the flat named_parameters() vector
+ * (hyper_w_1, hyper_w_final, hyper_b_1, V); forward over R rows: agent_qs [R][NA] (plain) or [R][2 NA] with the
+ * imagine masks w_mask / i_mask [R][NE][NE] (both or neither), entities [R][NE][D0], entity_mask [R][NE]
+ * -> q_tot [R]. softmax_mixing_weights selects softmax instead of abs mixing weights. */
+int64_t mlg_refil_packed_mixer_size(const MlgRefilDims *d);
+int mlg_refil_pack_mixer(const MlgRefilDims *d, const float *flat, float *packed, void *stream);
+int mlg_refil_mixer_forward(const MlgRefilDims *d, const float *packed, const float *agent_qs, const float *entities,
+                            const uint8_t *entity_mask, const uint8_t *w_mask, const uint8_t *i_mask,
+                            int32_t softmax_mixing_weights, float *q_tot, int32_t R, void *stream);
+
 /* REFILLearner.train (src/marl/learners/refil_learner.py:102-218) as one device pipeline: EntityMAC unrolls of the
  * plain / within / interact copies + target, FlexQMixer (flex_qmix.py:55-117) plain + imagined mixing, double-Q
  * targets, the lambda-mixed TD loss, all gradients, clip_grad_norm_ and RMSprop.

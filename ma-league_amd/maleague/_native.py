@@ -128,6 +128,10 @@ SIGNATURES = {
     "mlg_refil_pack_agent": (ctypes.c_int, [_P, _P, _P, _P]),
     "mlg_refil_agent_forward": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "mlg_refil_rollout": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P]),
+    "mlg_refil_attention": (ctypes.c_int, [_P] * 6 + [_I] * 4 + [_P] * 7),
+    "mlg_refil_packed_mixer_size": (ctypes.c_int64, [_P]),
+    "mlg_refil_pack_mixer": (ctypes.c_int, [_P, _P, _P, _P]),
+    "mlg_refil_mixer_forward": (ctypes.c_int, [_P] * 7 + [_I, _P, _I, _P]),
     "mlg_refil_param_counts": (ctypes.c_int64, [_P, _P, _P]),
     "mlg_refil_workspace_floats": (ctypes.c_int64, [_P]),
     "mlg_refil_train": (ctypes.c_int, [_P, _P, _P]),

@@ -150,3 +150,43 @@ def test_rollout_fixed_team_sizes(device):
             av = nb["avail_actions"][:, 0, k:]
             assert (av[..., 0] == 1).all() and (av[..., 1:] == 0).all()
             assert (nb["actions"][:, 0, k:, 0] == 0).all()
+
+
+@pytest.mark.parametrize("tag,nq", [("na", 8), ("ne", 16)])
+def test_attention_layer_forward_backward_golden(device, golden, tag, nq):
+    """EntityAttentionLayer fwd + bwd (mlg_refil_attention) vs the reference's vectors (attention.py:24-79)."""
+    from maleague import _native
+    d = golden("refil_layers.npz")
+    t = lambda k, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(d[k])).to(device=device, dtype=dt)  # noqa
+    w_in, w_out, b_out = t("attn.p.in_trans.weight"), t("attn.p.out_trans.weight"), t("attn.p.out_trans.bias")
+    x = t("attn.x")
+    bs, ne, _ = x.shape
+    pre = t("attn.pre", torch.uint8)[:, :nq].contiguous()
+    post = t("attn.em", torch.uint8)[:, :nq].contiguous()
+    gy = t(f"attn.{tag}.g")
+    y = torch.empty(bs, nq, 64, device=device)
+    dx = torch.empty_like(x)
+    dwi, dwo, dbo = torch.zeros_like(w_in), torch.zeros_like(w_out), torch.zeros_like(b_out)
+    P = _native.ptr
+    _native.call("mlg_refil_attention", P(w_in), P(w_out), P(b_out), P(x), P(pre), P(post), bs, ne, nq, 4, P(y), P(gy),
+                 P(dx), P(dwi), P(dwo), P(dbo), _native.stream_ptr())
+    np.testing.assert_allclose(y.cpu().numpy(), d[f"attn.{tag}.y"], atol=Q_TOL, rtol=0)
+    np.testing.assert_allclose(dx.cpu().numpy(), d[f"attn.{tag}.dx"], atol=Q_TOL, rtol=0)
+    np.testing.assert_allclose(dwi.cpu().numpy(), d[f"attn.{tag}.d.in_trans.weight"], atol=Q_TOL, rtol=1e-4)
+    np.testing.assert_allclose(dwo.cpu().numpy(), d[f"attn.{tag}.d.out_trans.weight"], atol=Q_TOL, rtol=1e-4)
+    np.testing.assert_allclose(dbo.cpu().numpy(), d[f"attn.{tag}.d.out_trans.bias"], atol=Q_TOL, rtol=1e-4)
+
+
+@pytest.mark.parametrize("tag", ["abs", "soft"])
+def test_flex_qmixer_forward_golden(device, golden, tag):
+    """FlexQMixer.forward plain and with imagine groups (flex_qmix.py:73-117) vs the reference's vectors."""
+    from maleague.modules.mixers import FlexQMixer
+    d = golden("refil_layers.npz")
+    a = refil_args(softmax_mixing_weights=tag == "soft")
+    m = FlexQMixer(a).to(device)
+    m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in _params(d, f"mixer.{tag}.p.").items()})
+    g = lambda k: torch.from_numpy(d[f"mixer.{tag}.{k}"]).to(device)  # noqa: E731
+    y = m(g("qs"), (g("ent"), g("em")))
+    np.testing.assert_allclose(y.cpu().numpy(), d[f"mixer.{tag}.y"], atol=Q_TOL, rtol=1e-5)
+    y2 = m(g("qs2"), (g("ent"), g("em")), imagine_groups=(g("wm"), g("im")))
+    np.testing.assert_allclose(y2.cpu().numpy(), d[f"mixer.{tag}.y2"], atol=Q_TOL, rtol=1e-5)
