@@ -17,6 +17,45 @@
 
 using namespace refil;
 
+// Phase functions of the rollout are kept out of line by default: inlined, the compiler hoists weight loads across
+// phases and the kernel needs > 512 registers (1 wave per SIMD, spills); out of line it fits 2 waves per SIMD.
+#ifdef MLG_REFIL_NOINLINE
+#define RO_PHASE __device__ __attribute__((noinline))
+#else
+#define RO_PHASE __device__ inline
+#endif
+
+#ifdef MLG_STAMPS
+// Diagnostic build only: per-wave cycle counts of the REFIL rollout phases, g_refil_stamps[block][16]
+// (slots 0..13 phases, 14 total, 15 = 1).
+__device__ unsigned long long* g_refil_stamps = nullptr;
+struct RStamps {
+    unsigned long long acc[14], last, begin;
+    __device__ void init() {
+        for (int k = 0; k < 14; ++k) acc[k] = 0;
+        last = begin = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void mark(int k) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - last;
+        last = now;
+    }
+    __device__ void flush() {
+        if ((threadIdx.x & 63) || !g_refil_stamps) return;
+        unsigned long long* o = g_refil_stamps + ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
+        for (int k = 0; k < 14; ++k) o[k] = acc[k];
+        o[14] = __builtin_amdgcn_s_memtime() - begin;
+        o[15] = 1;
+    }
+};
+#else
+struct RStamps {
+    __device__ void init() {}
+    __device__ void mark(int) {}
+    __device__ void flush() {}
+};
+#endif
+
 namespace {
 
 // ---- packing -----------------------------------------------------------------------------------------
@@ -111,23 +150,64 @@ __device__ inline void entity_block(const float* __restrict__ P, const RAgent& L
     wave_sync();
 }
 
+// Rollout form: the entity inputs arrive as the fc1 B operand in registers (xin, lane = entity row), fc1's output
+// stays in registers as in_trans' B operand; only q (agent rows, [NAS][LDX]) and k | v ([NE][LDKV]) go to LDS.
+constexpr int LDKV = 2 * EMB + 4;
+template <int KC1>
+__device__ inline void entity_block_reg(const float* __restrict__ P, const RAgent& L, const float* win, int ldin,
+                                        const floatx4 (&xin)[KC1], float* qs, float* kvs, const uint32_t* mrow, int nq,
+                                        int ne, float* o, int lane) {
+    const int col = lane & 15;
+    floatx4 x1[4];
+    bias_init<4>(x1, P + L.b1, 0, lane);
+    mm_reg<4, KC1>(x1, P + L.w1, L.K1, 0, xin, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x1[i] = relu4(x1[i]);
+    {  // q: only the agent rows are queried
+        floatx4 acc[4];
+        bias_init<4>(acc, nullptr, 0, lane);
+        mm_reg<4, 4>(acc, win, ldin, 0, x1, lane);
+        if (col < NAS) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) st_row(qs, LDX, i, acc[i], lane);
+        }
+    }
+#pragma unroll
+    for (int m0 = 4; m0 < 12; m0 += 4) {  // k, v
+        floatx4 acc[4];
+        bias_init<4>(acc, nullptr, 0, lane);
+        mm_reg<4, 4>(acc, win, ldin, m0, x1, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st_row(kvs, LDKV, m0 - 4 + i, acc[i], lane);
+    }
+    wave_sync();
+    attn_fwd_split(qs, LDX, kvs, kvs + EMB, LDKV, mrow, nq, ne, o, LDX, nullptr, lane);
+    wave_sync();
+}
+
 // out_trans (+ post mask) -> fc2 -> ReLU -> GRUCell on the 16-row tile; h in/out (D layout).
-// dead: bit r set = tile row r is a masked agent (post_mask, attention.py:75-76).
-__device__ inline void agent_tile_post(const float* __restrict__ P, const RAgent& L, const float* o, uint32_t dead,
-                                       floatx4 (&h)[4], int lane) {
+// dead: bit r set = tile row r is a masked agent (post_mask, attention.py:75-76). wout / w2 may live in LDS (ld).
+__device__ inline void agent_tile_post_w(const float* __restrict__ P, const RAgent& L, const float* wout, int ldo,
+                                         const float* w2, int ld2, const float* o, uint32_t dead, floatx4 (&h)[4],
+                                         int lane) {
     const int col = lane & 15;
     floatx4 x2[4], x3[4];
     bias_init<4>(x2, P + L.bout, 0, lane);
-    mm_lds<4>(x2, P + L.wout, EMB, 0, o, LDX, EMB / 16, lane);
+    mm_lds<4>(x2, wout, ldo, 0, o, LDX, EMB / 16, lane);
     if ((dead >> col) & 1u) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) x2[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
     bias_init<4>(x3, P + L.b2, 0, lane);
-    mm_reg<4, 4>(x3, P + L.w2, EMB, 0, x2, lane);
+    mm_reg<4, 4>(x3, w2, ld2, 0, x2, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x3[i] = relu4(x3[i]);
     gru_tile(P + L.wih, P + L.whh, P + L.bih, P + L.bhh, P + L.brz, x3, h, lane);
+}
+
+RO_PHASE void agent_tile_post(const float* __restrict__ P, const RAgent& L, const float* o, uint32_t dead,
+                              floatx4 (&h)[4], int lane) {
+    agent_tile_post_w(P, L, P + L.wout, EMB, P + L.w2, EMB, o, dead, h, lane);
 }
 
 // fc3 action tile `at` of the tile rows (q masked to 0 for dead rows, entity_rnn_agent.py:61)
@@ -142,9 +222,8 @@ __device__ __forceinline__ floatx4 agent_q(const float* __restrict__ P, const RA
 
 // ---- rollout ------------------------------------------------------------------------------------------------
 struct RoLds {
-    float ein[NE * LDI];
-    float x1[NE * LDX];
-    float qkv[NE * LDQ];
+    float q[NAS * LDX];
+    float kv[NE * LDKV];
     float o[16 * LDX];
     float feat[2][NE][8];
     uint32_t om[2][NE];
@@ -168,7 +247,7 @@ __device__ __forceinline__ int64_t ro_slot(const MlgEntityBatch& bt, int b) {
 }
 
 // pre-transition data of step t for env e (lanes (e, u)); writes batch rows and the LDS copies
-__device__ inline void ro_observe(RoLds& S, const EnvTables& T, const RoArgs& a, const MlgEntityBatch& bt, int e, int u,
+RO_PHASE void ro_observe(RoLds& S, const EnvTables& T, const RoArgs& a, const MlgEntityBatch& bt, int e, int u,
                                   bool active, int t) {
     const bool me = active && u < a.U;
     if (me) {
@@ -228,14 +307,38 @@ __device__ inline void ro_zero_tail(const MlgEntityBatch& bt, const RoArgs& a, i
     }
 }
 
-__global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec, MlgEnvState st, RAgent L,
-                                                           const float* __restrict__ P, MlgEntityBatch bt,
-                                                           MlgRunInfo info, RoArgs a, float eps, int test_mode) {
-    __shared__ RoLds S;
-    const int lane = threadIdx.x;
+// Workgroup = RO_WAVES waves; every wave owns two envs for the whole episode (no cross-wave dependency after the
+// prologue); the waves share one LDS copy of in_trans / out_trans / fc2 (padded rows, conflict-free A reads).
+constexpr int RO_WAVES = 4;
+constexpr int LDW = EMB + 4;
+struct RoShared {
+    float win[3 * EMB * LDW];
+    float wout[EMB * LDW];
+    float w2[EMB * LDW];
+    RoLds S[RO_WAVES];
+};
+
+template <int KC1>
+__global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityEnvSpec spec, MlgEnvState st, RAgent L,
+                                                                      const float* __restrict__ P, MlgEntityBatch bt,
+                                                                      MlgRunInfo info, RoArgs a, float eps,
+                                                                      int test_mode) {
+    extern __shared__ __attribute__((aligned(16))) float ro_smem[];
+    RoShared& SH = *reinterpret_cast<RoShared*>(ro_smem);
+    for (int i = threadIdx.x; i < 3 * EMB * EMB; i += blockDim.x) SH.win[(i / EMB) * LDW + i % EMB] = P[L.win + i];
+    for (int i = threadIdx.x; i < EMB * EMB; i += blockDim.x) {
+        SH.wout[(i / EMB) * LDW + i % EMB] = P[L.wout + i];
+        SH.w2[(i / EMB) * LDW + i % EMB] = P[L.w2 + i];
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    RoLds& S = SH.S[wave];
+    RStamps stp;
+    stp.init();
+    const int lane = threadIdx.x & 63;
     const int e = (lane >> 4) & 1, u = lane & 15;
     const bool env_lane = lane < 32;
-    const int b0 = blockIdx.x * 2;
+    const int b0 = (blockIdx.x * RO_WAVES + wave) * 2;
     const MlgEnvSpec& sp = spec.base;
     if (lane < a.U) {
         S.team[lane] = sp.team[lane];
@@ -244,7 +347,6 @@ __global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec
         S.agent[lane] = lane < a.NA ? lane + 1 : 0;
     }
     for (int i = lane; i < 16 * LDX; i += 64) S.o[i] = 0.f;
-    for (int i = lane; i < NE * LDI; i += 64) S.ein[i] = 0.f;
     if (lane < 2) {
         const int b = b0 + lane;
         S.status[lane] = b < a.B ? 0 : 2;
@@ -291,21 +393,32 @@ __global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec
     for (int t = 0;; ++t) {
         const int st0 = S.status[0], st1 = S.status[1];
         if (st0 == 2 && st1 == 2) break;
+        // opaque per-iteration copy of the weight pointer: keeps the compiler from hoisting every (loop-invariant)
+        // weight load of the step out of the episode loop into registers (> 512 VGPRs, spills)
+        int64_t zoff = 0;
+        asm volatile("" : "+s"(zoff));
+        const float* __restrict__ Pw = P + zoff;
         // ---- agent phase: EntityMAC.forward(t) + epsilon-greedy for both envs ----
         for (int ee = 0; ee < 2; ++ee) {
             if (S.status[ee] == 2) continue;
-            const int D0 = a.ED + a.A;
-            for (int i = lane; i < NE * L.K1; i += 64) {
-                const int j = i / L.K1, c = i % L.K1;
-                float v = 0.f;
-                if (j < a.U) {
-                    if (c < a.ED) v = S.feat[ee][j][c];
-                    else if (c < D0 && j < a.NA && t > 0 && S.pact[ee][j] == c - a.ED) v = 1.f;
+            // fc1 B operand: lane (entity j = col, g) holds inputs k = 16 kc + 4 g + r
+            floatx4 xin[KC1];
+            const int j = col;
+#pragma unroll
+            for (int kc = 0; kc < KC1; ++kc)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int k = kc * 16 + 4 * g + r;
+                    float v = 0.f;
+                    if (j < a.U) {
+                        if (k < a.ED) v = S.feat[ee][j][k < 8 ? k : 0];
+                        else if (k < a.ED + a.A && j < a.NA && t > 0 && S.pact[ee][j] == k - a.ED) v = 1.f;
+                    }
+                    xin[kc][r] = v;
                 }
-                S.ein[j * LDI + c] = v;
-            }
-            wave_sync();
-            entity_block(P, L, S.ein, S.x1, S.qkv, S.om[ee], a.NA, a.U, S.o + ee * NAS * LDX, lane);
+            stp.mark(0);
+            entity_block_reg<KC1>(Pw, L, SH.win, LDW, xin, S.q, S.kv, S.om[ee], a.NA, a.U, S.o + ee * NAS * LDX, lane);
+            stp.mark(1);
             rows += (uint64_t)a.NA;
         }
         // tile row r = env (r >> 3), agent (r & 7); dead = agent entity masked
@@ -315,13 +428,14 @@ __global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec
             m |= ~((1u << a.NA) - 1u) & 0xFFu;  // padding rows >= n_agents
             dead |= (m & 0xFFu) << (8 * ee);
         }
-        agent_tile_post(P, L, S.o, dead, h, lane);
+        agent_tile_post_w(Pw, L, SH.wout, LDW, SH.w2, LDW, S.o, dead, h, lane);
+        stp.mark(2);
         // fc3 + masked argmax + epsilon-greedy
         const int re = col >> 3, rn = col & 7;
         const uint32_t avm = (rn < a.NA) ? S.av[re][rn] : 1u;
         ArgmaxState as{-INFINITY, 1 << 30};
         for (int at = 0; at < L.Ap / 16; ++at) {
-            const floatx4 q = agent_q(P, L, h, at, dead, lane);
+            const floatx4 q = agent_q(Pw, L, h, at, dead, lane);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int ac = at * 16 + 4 * g + r;
@@ -360,6 +474,7 @@ __global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec
             }
         }
         wave_sync();
+        stp.mark(3);
         // ---- env phase (EnvWorker "step", env_worker_process.py:32-53) ----
         const bool stepping = env_lane && S.status[e] == 0;
         if (stepping && u < a.U) {
@@ -367,8 +482,10 @@ __global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec
             S.act[e][u] = env_exec_action(T, S.x[e], S.y[e], S.hp[e], u, ag ? (int64_t)S.pact[e][ag - 1] : 0);
         }
         wave_sync();
+        stp.mark(4);
         if (stepping && u < a.U) S.nhp[e][u] = env_resolve_hp(T, S.act[e], S.hp[e], u);
         wave_sync();
+        stp.mark(5);
         if (stepping && u < a.U && S.hp[e][u] > 0) env_apply_move(S.act[e][u], &S.x[e][u], &S.y[e][u]);
         if (env_lane && u == 0) {
             const int stt = S.status[e];
@@ -409,11 +526,13 @@ __global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec
             }
         }
         wave_sync();
+        stp.mark(6);
         const bool stepped = env_lane && S.stepped[e];
         if (stepped && u < a.U) S.hp[e][u] = S.nhp[e][u];
         wave_sync();
         ro_observe(S, T, a, bt, e, u, stepped, t + 1);
         wave_sync();
+        stp.mark(7);
     }
     // ---- finish: run summary, env state, full-write tails ----
     if (live && u == 0) {
@@ -432,6 +551,8 @@ __global__ void __launch_bounds__(64) refil_rollout_kernel(MlgEntityEnvSpec spec
             if (b0 + ee < a.B) ro_zero_tail(bt, a, S.slot[ee], S.len[ee] + 1, lane);
     }
     if (info.agent_rows && lane == 0) atomicAdd((unsigned long long*)info.agent_rows, (unsigned long long)rows);
+    stp.mark(8);
+    stp.flush();
 }
 
 // ---- one EntityAttentionRNNAgent step over R items (two items per wave) -------------------------------
@@ -507,6 +628,17 @@ __global__ void __launch_bounds__(64) refil_agent_step_kernel(RAgent L, const fl
 
 }  // namespace
 
+extern "C" int mlg_refil_debug_set_stamps(void* ptr) {
+#ifdef MLG_STAMPS
+    unsigned long long* p = (unsigned long long*)ptr;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_refil_stamps), &p, sizeof(p)) != hipSuccess) return mlg::fail("set stamps");
+    return 0;
+#else
+    (void)ptr;
+    return mlg::fail("mlg_refil_debug_set_stamps: build with -DMLG_STAMPS (make stamps)");
+#endif
+}
+
 extern "C" int64_t mlg_refil_packed_agent_size(const MlgRefilDims* d) {
     if (check_dims(d)) return -1;
     return agent_layout(d).total;
@@ -558,7 +690,18 @@ extern "C" int mlg_refil_rollout(const MlgEntityEnvSpec* spec, MlgEnvState* st, 
     while (p < sp.grid) p <<= 1;
     RoArgs a{sp.U, S, d->n_actions, d->entity_shape, S, spec->min_agents, spec->max_agents, bt.B, 1.0f / (float)p};
     const RAgent L = agent_layout(d);
-    hipLaunchKernelGGL(refil_rollout_kernel, dim3((unsigned)((bt.B + 1) / 2)), dim3(64), 0, (hipStream_t)stream, *spec, *st,
-                       L, packed, bt, *info, a, test_mode ? 0.f : epsilon, test_mode);
+    auto kern = L.K1 <= 16 ? refil_rollout_kernel<1> : (L.K1 <= 32 ? refil_rollout_kernel<2> : refil_rollout_kernel<3>);
+    const size_t lds = sizeof(RoShared);
+    static bool attr_set[3] = {false, false, false};
+    const int ki = L.K1 <= 16 ? 0 : (L.K1 <= 32 ? 1 : 2);
+    if (!attr_set[ki]) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return mlg::fail("refil_rollout: LDS %zu B: %s", lds, hipGetErrorString(e));
+        attr_set[ki] = true;
+    }
+    const int per_block = 2 * RO_WAVES;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((bt.B + per_block - 1) / per_block)), dim3(64 * RO_WAVES), lds,
+                       (hipStream_t)stream, *spec, *st, L, packed, bt, *info, a, test_mode ? 0.f : epsilon, test_mode);
     return mlg::check_launch("refil_rollout");
 }

@@ -198,14 +198,15 @@ __device__ __forceinline__ void dense_lds(const float* __restrict__ W, int ldw, 
 // mrow[q]: pre-mask bits of query row q (bit j = entity j masked); nq <= 16 queries; keys k >= ne are masked.
 // Lane (h = lane >> 4, q = lane & 15). Output o row q (cols h*16..) in LDS; P[h][q][k] saved when non-null
 // (global or LDS, row stride 16). Rows with every key masked: softmax NaN -> 0 (attention.py:59).
-__device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, int ne, float* o, int ldo, float* P,
-                                int lane) {
+// General form: query rows at qb (row stride ldq), key / value rows at kb / vb (row stride ldkv).
+__device__ inline void attn_fwd_split(const float* qb, int ldq, const float* kb, const float* vb, int ldkv,
+                                      const uint32_t* mrow, int nq, int ne, float* o, int ldo, float* P, int lane) {
     const int h = lane >> 4, q = lane & 15;
     if (q >= nq) return;
     float qv[HD];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const floatx4 v = ld4(qkv + q * LDQ + h * HD + 4 * c);
+        const floatx4 v = ld4(qb + q * ldq + h * HD + 4 * c);
         qv[4 * c] = v[0]; qv[4 * c + 1] = v[1]; qv[4 * c + 2] = v[2]; qv[4 * c + 3] = v[3];
     }
     const uint32_t m = mrow[q] | (ne < 32 ? (~0u << ne) : 0u);
@@ -213,7 +214,7 @@ __device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, 
     float mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
-        const float* kr = qkv + k * LDQ + EMB + h * HD;
+        const float* kr = kb + k * ldkv + h * HD;
         float d = 0.f;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -240,7 +241,7 @@ __device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, 
         for (int k = 0; k < NE; ++k) s[k] = s[k] / sum;
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
-            const float* vr = qkv + k * LDQ + 2 * EMB + h * HD;
+            const float* vr = vb + k * ldkv + h * HD;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const floatx4 vv = ld4(vr + 4 * c);
@@ -263,6 +264,11 @@ __device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, 
         for (int c = 0; c < 4; ++c)
             *reinterpret_cast<floatx4*>(pr + 4 * c) = floatx4{s[4 * c], s[4 * c + 1], s[4 * c + 2], s[4 * c + 3]};
     }
+}
+
+__device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, int ne, float* o, int ldo, float* P,
+                                int lane) {
+    attn_fwd_split(qkv, LDQ, qkv + EMB, qkv + 2 * EMB, LDQ, mrow, nq, ne, o, ldo, P, lane);
 }
 
 // Backward of attn_fwd for one item. P: [NH][16][16] saved weights; dO: rows q < nq (cols h*16..);
@@ -397,6 +403,9 @@ __device__ inline void gru_tile(const float* __restrict__ wih, const float* __re
             ar = mfma_chunk(ld4(wh + kc * 16), h[kc], ar);
             az = mfma_chunk(ld4(wh + GATE + kc * 16), h[kc], az);
             ahn = mfma_chunk(ld4(wh + 2 * GATE + kc * 16), h[kc], ahn);
+#ifdef MLG_REFIL_LEAN
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

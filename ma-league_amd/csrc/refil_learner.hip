@@ -29,7 +29,7 @@ using namespace refil;
 namespace {
 
 constexpr int MJ = 24;
-using RJobs = mlg::WJobsT<MJ>;
+using RJobs = mlg::BJobsT<MJ>;
 
 struct RCfg {
     int B, T, T1, NA, NE, ED, D0, K1, A, Ap, I, Ron, Rtg;
@@ -1140,26 +1140,26 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     const int I16 = c.I * NE, TR = c.T * c.Ron;
     RJobs J;
     J.n = 0;
-    J.j[J.n++] = mlg::job(at(p.w.dfc1), EMB, at(p.w.ein), c.K1, gp(a.c_w1), gp(a.c_b1), EMB, c.D0, I16);
-    J.j[J.n++] = mlg::job(at(p.w.dqkv), 3 * EMB, at(p.w.x1), EMB, gp(a.c_win), nullptr, 3 * EMB, EMB, I16);
-    J.j[J.n++] = mlg::job(at(p.w.dout), EMB, at(p.w.o), EMB, gp(a.c_wout), gp(a.c_bout), EMB, EMB, TR);
-    J.j[J.n++] = mlg::job(at(p.w.dfc2), EMB, at(p.w.x2), EMB, gp(a.c_w2), gp(a.c_b2), EMB, EMB, TR);
-    J.j[J.n++] = mlg::job(at(p.w.dgi), 3 * EMB, at(p.w.x3), EMB, gp(a.c_wih), gp(a.c_bih), 3 * EMB, EMB, TR);
-    J.j[J.n++] = mlg::job(at(p.w.dgh), 3 * EMB, at(p.w.hs_on), EMB, gp(a.c_whh), gp(a.c_bhh), 3 * EMB, EMB, TR);
-    J.j[J.n++] = mlg::job(at(p.w.d2), c.A, ws ? ws + p.w.hs_on + (int64_t)c.Ron * EMB : nullptr, EMB, gp(a.c_w3),
+    J.j[J.n++] = mlg::bjob(at(p.w.dfc1), EMB, at(p.w.ein), c.K1, gp(a.c_w1), gp(a.c_b1), EMB, c.D0, I16);
+    J.j[J.n++] = mlg::bjob(at(p.w.dqkv), 3 * EMB, at(p.w.x1), EMB, gp(a.c_win), nullptr, 3 * EMB, EMB, I16);
+    J.j[J.n++] = mlg::bjob(at(p.w.dout), EMB, at(p.w.o), EMB, gp(a.c_wout), gp(a.c_bout), EMB, EMB, TR);
+    J.j[J.n++] = mlg::bjob(at(p.w.dfc2), EMB, at(p.w.x2), EMB, gp(a.c_w2), gp(a.c_b2), EMB, EMB, TR);
+    J.j[J.n++] = mlg::bjob(at(p.w.dgi), 3 * EMB, at(p.w.x3), EMB, gp(a.c_wih), gp(a.c_bih), 3 * EMB, EMB, TR);
+    J.j[J.n++] = mlg::bjob(at(p.w.dgh), 3 * EMB, at(p.w.hs_on), EMB, gp(a.c_whh), gp(a.c_bhh), 3 * EMB, EMB, TR);
+    J.j[J.n++] = mlg::bjob(at(p.w.d2), c.A, ws ? ws + p.w.hs_on + (int64_t)c.Ron * EMB : nullptr, EMB, gp(a.c_w3),
                           gp(a.c_b3), c.A, EMB, TR);
     for (int k = 0; k < 4; ++k) {
         const RHyper& h = p.Lh;
         const int64_t G0 = p.n_agent + (int64_t)k * h.c_total;
         const int rows = nvar(k) * c.I * NAS;
-        J.j[J.n++] = mlg::job(at(p.w.dfc1m[k]), EMB, at(p.w.ein), c.K1, gp(G0 + h.c_w1), gp(G0 + h.c_b1), EMB, c.D0, I16);
-        J.j[J.n++] = mlg::job(at(p.w.dqkvm[k]), 3 * EMB, at(p.w.x1m[k]), EMB, gp(G0 + h.c_win), nullptr, 3 * EMB, EMB, I16);
-        J.j[J.n++] = mlg::job(at(p.w.doutm[k]), EMB, at(p.w.om[k]), EMB, gp(G0 + h.c_wout), gp(G0 + h.c_bout), EMB, EMB,
+        J.j[J.n++] = mlg::bjob(at(p.w.dfc1m[k]), EMB, at(p.w.ein), c.K1, gp(G0 + h.c_w1), gp(G0 + h.c_b1), EMB, c.D0, I16);
+        J.j[J.n++] = mlg::bjob(at(p.w.dqkvm[k]), 3 * EMB, at(p.w.x1m[k]), EMB, gp(G0 + h.c_win), nullptr, 3 * EMB, EMB, I16);
+        J.j[J.n++] = mlg::bjob(at(p.w.doutm[k]), EMB, at(p.w.om[k]), EMB, gp(G0 + h.c_wout), gp(G0 + h.c_bout), EMB, EMB,
                               rows);
-        J.j[J.n++] = mlg::job(at(p.w.dX[k]), EM, at(p.w.x2m[k]), EMB, gp(G0 + h.c_w2), gp(G0 + h.c_b2), EM, EMB, rows);
+        J.j[J.n++] = mlg::bjob(at(p.w.dX[k]), EM, at(p.w.x2m[k]), EMB, gp(G0 + h.c_w2), gp(G0 + h.c_b2), EM, EMB, rows);
     }
     int64_t slab_part;
-    *slab_floats = mlg::layout_jobs(J, n_tasks, n_red, &slab_part);
+    *slab_floats = mlg::layout_bjobs(J, n_tasks, n_red, &slab_part);
     p.w.nrm = p.w.slab + slab_part;
     return J;
 }
@@ -1262,9 +1262,9 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     int64_t slab_floats, n_red;
     int n_tasks;
     RJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
-    hipLaunchKernelGGL(mlg::wgrad_kernel<MJ>, dim3((unsigned)((n_tasks + 3) / 4)), dim3(256), 0, s, J, ws + w.slab);
+    hipLaunchKernelGGL(mlg::wgrad_block_kernel<MJ>, dim3((unsigned)((n_tasks + 3) / 4)), dim3(256), 0, s, J, ws + w.slab);
     const int n_red_blocks = (int)((n_red + 255) / 256);
-    hipLaunchKernelGGL(mlg::wgrad_reduce_kernel<MJ>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + w.slab,
+    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<MJ>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + w.slab,
                        ws + p.w.nrm);
     const int64_t n_par = p.n_agent + p.n_mixer;
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + w.part, c.I,

@@ -160,3 +160,175 @@ inline int64_t layout_jobs(WJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t*
 }
 
 }  // namespace mlg
+
+// ================================================================================================
+// Blocked variant: one wave per (job, 64 x 64 output block, 1024-row chunk); per 4-row step every lane loads 4 delta
+// and 4 x values and issues 16 MFMAs (vs 2 loads per MFMA above), partials [block][chunk][64 * 64 + 64] summed over
+// chunks in a fixed order (deterministic).
+namespace mlg {
+
+constexpr int BCH = 1024;        // rows per chunk
+constexpr int BSLAB = 64 * 64 + 64;
+
+struct BJob {
+    const float* delta;
+    const float* x;
+    float* dw;
+    float* db;
+    int64_t ldd, ldx;
+    int M, K, rows, mb, nb, chunks;
+    int task0;
+    int64_t slab0;
+};
+template <int MJ>
+struct BJobsT {
+    BJob j[MJ];
+    int n;
+};
+
+inline BJob bjob(const float* delta, int64_t ldd, const float* x, int64_t ldx, float* dw, float* db, int M, int K,
+                 int rows) {
+    BJob j;
+    j.delta = delta;
+    j.x = x;
+    j.dw = dw;
+    j.db = db;
+    j.ldd = ldd;
+    j.ldx = ldx;
+    j.M = M;
+    j.K = K;
+    j.rows = rows;
+    j.mb = (M + 63) / 64;
+    j.nb = (K + 63) / 64;
+    j.chunks = (rows + BCH - 1) / BCH;
+    j.task0 = 0;
+    j.slab0 = 0;
+    return j;
+}
+
+template <int MJ>
+__device__ __forceinline__ int find_bjob(const BJobsT<MJ>& J, int task) {
+    int k = 0;
+    while (k + 1 < J.n && J.j[k + 1].task0 <= task) ++k;
+    return k;
+}
+
+template <int MJ>
+__global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* __restrict__ slab) {
+    const int lane = threadIdx.x & 63;
+    const int task = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const BJob& last = J.j[J.n - 1];
+    if (task >= last.task0 + last.mb * last.nb * last.chunks) return;
+    const BJob jb = J.j[find_bjob(J, task)];
+    const int local = task - jb.task0;
+    const int ch = local % jb.chunks, blk = local / jb.chunks;
+    const int mbi = blk / jb.nb, nbi = blk % jb.nb;
+    const int col = lane & 15, g = lane >> 4;
+    const int r0 = ch * BCH, r1 = min(jb.rows, r0 + BCH);
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    int mi[4], ki[4];
+    bool mv[4], kv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mi[i] = mbi * 64 + i * 16 + col;
+        ki[i] = nbi * 64 + i * 16 + col;
+        mv[i] = mi[i] < jb.M;
+        kv[i] = ki[i] < jb.K;
+    }
+    for (int rr = r0; rr < r1; rr += 4) {
+        const int row = rr + g;
+        const bool rv = row < r1;
+        const float* dr = jb.delta + (int64_t)row * jb.ldd;
+        const float* xr = jb.x + (int64_t)row * jb.ldx;
+        float a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a[i] = (mv[i] && rv) ? dr[mi[i]] : 0.f;
+            b[i] = (kv[i] && rv) ? xr[ki[i]] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bsum[i] += a[i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
+        }
+    }
+    float* out = slab + jb.slab0 + ((int64_t)blk * jb.chunks + ch) * BSLAB;
+    // D layout: acc[i][j] reg q -> (m = 16 i + 4 g + q, k = 16 j + col) within the block
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[(16 * i + 4 * g + q) * 64 + 16 * j + col] = acc[i][j][q];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float s = bsum[i];
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (g == 0) out[4096 + 16 * i + col] = s;
+    }
+}
+
+// fixed-order sum over chunks -> dW / db (bias from the nbi == 0 blocks); per-block sums of squares -> nrm_part
+template <int MJ>
+__global__ void __launch_bounds__(256) wgrad_block_reduce_kernel(BJobsT<MJ> J, const float* __restrict__ slab,
+                                                                 float* __restrict__ nrm_part) {
+    __shared__ float red[256];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t acc = 0;
+    float sq = 0.f;
+    for (int q = 0; q < J.n; ++q) {
+        const BJob& jb = J.j[q];
+        const int64_t n_el = (int64_t)jb.mb * jb.nb * BSLAB;
+        if (i >= acc && i < acc + n_el) {
+            const int64_t loc = i - acc;
+            const int blk = (int)(loc / BSLAB), e = (int)(loc % BSLAB);
+            const int mbi = blk / jb.nb, nbi = blk % jb.nb;
+            float s = 0.f;
+            const float* base = slab + jb.slab0 + (int64_t)blk * jb.chunks * BSLAB + e;
+            for (int ch = 0; ch < jb.chunks; ++ch) s += base[(int64_t)ch * BSLAB];
+            if (e < 4096) {
+                const int m = mbi * 64 + e / 64, k = nbi * 64 + e % 64;
+                if (m < jb.M && k < jb.K) {
+                    jb.dw[(int64_t)m * jb.K + k] = s;
+                    sq = s * s;
+                }
+            } else if (nbi == 0 && jb.db) {
+                const int m = mbi * 64 + (e - 4096);
+                if (m < jb.M) {
+                    jb.db[m] = s;
+                    sq = s * s;
+                }
+            }
+            break;
+        }
+        acc += n_el;
+    }
+    const float bs = block_sum_1024(sq, red);
+    if (threadIdx.x == 0) nrm_part[blockIdx.x] = bs;
+}
+
+template <int MJ>
+inline int64_t layout_bjobs(BJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t* slab_part) {
+    int tasks = 0;
+    int64_t slab = 0, red = 0;
+    for (int q = 0; q < J.n; ++q) {
+        J.j[q].task0 = tasks;
+        J.j[q].slab0 = slab;
+        tasks += J.j[q].mb * J.j[q].nb * J.j[q].chunks;
+        slab += (int64_t)J.j[q].mb * J.j[q].nb * J.j[q].chunks * BSLAB;
+        red += (int64_t)J.j[q].mb * J.j[q].nb * BSLAB;
+    }
+    *n_tasks = tasks;
+    *n_red = red;
+    *slab_part = mlg_align4(slab);
+    return mlg_align4(slab) + mlg_align4((red + 255) / 256);
+}
+
+}  // namespace mlg
