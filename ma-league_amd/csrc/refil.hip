@@ -230,6 +230,7 @@ struct RoLds {
     uint32_t em[2];
     uint32_t av[2][NAS];
     int x[2][NE], y[2][NE], hp[2][NE], act[2][NE], nhp[2][NE];
+    int pk[2][NE];  // packed unit states x | y << 8 | hp << 16 (register env rules)
     int pact[2][NAS];
     int team[NE], role[NE], melee[NE], agent[NE];
     int status[2], len[2], slot[2], stepped[2];
@@ -247,43 +248,35 @@ __device__ __forceinline__ int64_t ro_slot(const MlgEntityBatch& bt, int b) {
 }
 
 // pre-transition data of step t for env e (lanes (e, u)); writes batch rows and the LDS copies
-RO_PHASE void ro_observe(RoLds& S, const EnvTables& T, const RoArgs& a, const MlgEntityBatch& bt, int e, int u,
-                                  bool active, int t) {
+RO_PHASE void ro_observe(RoLds& S, const EnvTables& T, const EnvMasks& M, const RoArgs& a, const MlgEntityBatch& bt,
+                         int e, int u, bool active, int t) {
     const bool me = active && u < a.U;
     if (me) {
-        const int* x = S.x[e];
-        const int* y = S.y[e];
-        const int* hp = S.hp[e];
+        int pk[16];
+        load16(S.pk[e], pk);
+        const int pu = S.pk[e][u];
         const int64_t row = (S.slot[e] * (int64_t)bt.T1 + t);
         float f[8];
-        entity_feat(T, x[u], y[u], hp[u], u, a.inv_p, f);
+        entity_feat(T, pkx(pu), pky(pu), pkh(pu), u, a.inv_p, f);
         float* eg = bt.entities + (row * a.U + u) * a.ED;
         for (int k = 0; k < 8; ++k) {
             S.feat[e][u][k] = f[k];
             if (k < a.ED) eg[k] = f[k];
         }
-        uint32_t bits = 0;
+        const uint32_t bits = om_bits(M, pk, u, pu);
         uint8_t* omg = bt.obs_mask + (row * a.U + u) * a.U;
-        for (int j = 0; j < a.U; ++j) {
-            const int m = hp[u] <= 0 || hp[j] <= 0 || env_dist2(x, y, u, j) > MLG_SIGHT2;
-            bits |= (uint32_t)m << j;
-            omg[j] = (uint8_t)m;
-        }
+        for (int j = 0; j < a.U; ++j) omg[j] = (uint8_t)((bits >> j) & 1u);
         S.om[e][u] = bits;
-        bt.entity_mask[row * a.U + u] = (uint8_t)(hp[u] <= 0);
+        bt.entity_mask[row * a.U + u] = (uint8_t)(pkh(pu) <= 0);
         if (u < a.NA) {
-            uint32_t av = 0;
+            const uint32_t av = avail_bits(M, pk, u, pu);
             int32_t* ag = bt.avail + (row * a.NA + u) * a.A;
-            for (int k = 0; k < a.A; ++k) {
-                const int v = env_avail_one(T, x, y, hp, u, k);
-                av |= (uint32_t)v << k;
-                ag[k] = v;
-            }
+            for (int k = 0; k < a.A; ++k) ag[k] = (int)((av >> k) & 1u);
             S.av[e][u] = av;
         }
         if (u == 0) bt.filled[row] = 1;
     }
-    const uint64_t bal = __ballot(me && S.hp[e][u] <= 0);
+    const uint64_t bal = __ballot(me && pkh(S.pk[e][u]) <= 0);
     if (active && u == 0) S.em[e] = (uint32_t)((bal >> (16 * e)) & 0xFFFFu);
 }
 
@@ -367,6 +360,16 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
     T.grid = sp.grid;
     T.episode_limit = sp.episode_limit;
     T.stochastic = sp.stochastic;
+    EnvMasks M;
+    M.team1 = M.healer = M.tank = M.melee = 0;
+    for (int j = 0; j < a.U; ++j) {
+        M.team1 |= (uint32_t)(S.team[j] != 0) << j;
+        M.healer |= (uint32_t)(S.role[j] == 1) << j;
+        M.tank |= (uint32_t)(S.role[j] == 0) << j;
+        M.melee |= (uint32_t)(S.melee[j] != 0) << j;
+    }
+    M.U = a.U;
+    M.grid = sp.grid;
     // ---- reset (EnvWorker "reset", env_worker_process.py:54-60) ----
     const int b = b0 + e;
     const bool live = env_lane && b < a.B;
@@ -381,9 +384,11 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
         S.x[e][u] = xx;
         S.y[e][u] = yy;
         S.hp[e][u] = hh;
+        S.pk[e][u] = pk_pack(xx, yy, hh);
     }
+    if (env_lane && u >= a.U) S.pk[e][u] = 0;
     wave_sync();
-    ro_observe(S, T, a, bt, e, u, live, 0);
+    ro_observe(S, T, M, a, bt, e, u, live, 0);
     wave_sync();
     floatx4 h[4];
 #pragma unroll
@@ -477,13 +482,26 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
         stp.mark(3);
         // ---- env phase (EnvWorker "step", env_worker_process.py:32-53) ----
         const bool stepping = env_lane && S.status[e] == 0;
-        if (stepping && u < a.U) {
-            const int ag = S.agent[u];
-            S.act[e][u] = env_exec_action(T, S.x[e], S.y[e], S.hp[e], u, ag ? (int64_t)S.pact[e][ag - 1] : 0);
+        int pk[16];
+        load16(S.pk[e], pk);
+        const int pu = S.pk[e][u];
+        if (stepping && u < a.U) {  // executed action: validated policy action or scripted AI (spec §3.4)
+            int ac;
+            if (u < a.NA) {
+                const int pa = S.pact[e][u];
+                ac = (pa >= 0 && pa < MLG_ACT_BASE + a.U && ((avail_bits(M, pk, u, pu) >> pa) & 1u)) ? pa : 0;
+            } else {
+                ac = ai_action_reg(M, pk, u, pu);
+            }
+            S.act[e][u] = ac;
         }
         wave_sync();
         stp.mark(4);
-        if (stepping && u < a.U) S.nhp[e][u] = env_resolve_hp(T, S.act[e], S.hp[e], u);
+        if (stepping && u < a.U) {
+            int acts[16];
+            load16(S.act[e], acts);
+            S.nhp[e][u] = resolve_hp_reg(M, pk, acts, u, pu);
+        }
         wave_sync();
         stp.mark(5);
         if (stepping && u < a.U && S.hp[e][u] > 0) env_apply_move(S.act[e][u], &S.x[e][u], &S.y[e][u]);
@@ -528,9 +546,12 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
         wave_sync();
         stp.mark(6);
         const bool stepped = env_lane && S.stepped[e];
-        if (stepped && u < a.U) S.hp[e][u] = S.nhp[e][u];
+        if (stepped && u < a.U) {
+            S.hp[e][u] = S.nhp[e][u];
+            S.pk[e][u] = pk_pack(S.x[e][u], S.y[e][u], S.nhp[e][u]);
+        }
         wave_sync();
-        ro_observe(S, T, a, bt, e, u, stepped, t + 1);
+        ro_observe(S, T, M, a, bt, e, u, stepped, t + 1);
         wave_sync();
         stp.mark(7);
     }

@@ -446,3 +446,137 @@ __device__ __forceinline__ void entity_feat(const EnvTables& T, int x, int y, in
 }
 
 }  // namespace refil
+
+// ---- register form of the env rules for one half-wave env (lane per unit) ---------------------------------
+// Units are read as packed states pk[j] = x | y << 8 | hp << 16 (four 16-byte LDS broadcast reads per env), the
+// static unit tables as bit masks, loops fully unrolled: the same integer rules as env_avail_one / env_ai_action /
+// env_resolve_hp (mlg_device.h, oracle/env_ref.c), without per-unit LDS lookups.
+namespace refil {
+
+struct EnvMasks {
+    uint32_t team1, healer, tank, melee;
+    int U, grid;
+};
+
+__device__ __forceinline__ int pk_pack(int x, int y, int hp) { return x | (y << 8) | (hp << 16); }
+__device__ __forceinline__ int pkx(int p) { return p & 0xFF; }
+__device__ __forceinline__ int pky(int p) { return (p >> 8) & 0xFF; }
+__device__ __forceinline__ int pkh(int p) { return p >> 16; }
+
+__device__ __forceinline__ void load16(const int* src, int (&v)[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int4 w = *reinterpret_cast<const int4*>(src + 4 * q);
+        v[4 * q] = w.x;
+        v[4 * q + 1] = w.y;
+        v[4 * q + 2] = w.z;
+        v[4 * q + 3] = w.w;
+    }
+}
+
+// units j that unit i (alive) may target with action 5 + j
+// (pi = packed state of unit i itself: never index pk[] with a runtime index, that would spill it to scratch)
+__device__ __forceinline__ uint32_t target_bits(const EnvMasks& M, const int (&pk)[16], int i, int pi) {
+    const int xi = pkx(pi), yi = pky(pi);
+    const int r2 = ((M.melee >> i) & 1u) ? 2 : 9;
+    const bool heal = (M.healer >> i) & 1u;
+    const uint32_t mt = (M.team1 >> i) & 1u;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int p = pk[j], hj = pkh(p);
+        const int dx = pkx(p) - xi, dy = pky(p) - yi;
+        const uint32_t tj = (M.team1 >> j) & 1u;
+        const bool ok = heal ? (j != i && tj == mt && hj < (((M.tank >> j) & 1u) ? 64 : 32)) : (tj != mt);
+        bits |= (uint32_t)(j < M.U && hj > 0 && dx * dx + dy * dy <= r2 && ok) << j;
+    }
+    return bits;
+}
+
+// avail bits of unit i: bit a = action a available (spec §3.2)
+__device__ __forceinline__ uint32_t avail_bits(const EnvMasks& M, const int (&pk)[16], int i, int pi) {
+    if (pkh(pi) <= 0) return 1u;
+    const int x = pkx(pi), y = pky(pi);
+    uint32_t m = 0;
+    m |= (uint32_t)(y + 1 < M.grid) << 1;
+    m |= (uint32_t)(y - 1 >= 0) << 2;
+    m |= (uint32_t)(x + 1 < M.grid) << 3;
+    m |= (uint32_t)(x - 1 >= 0) << 4;
+    return m | (target_bits(M, pk, i, pi) << MLG_ACT_BASE);
+}
+
+__device__ __forceinline__ int move_toward_d(int dx, int dy) {
+    const int adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+    if (adx >= ady && dx != 0) return dx > 0 ? 3 : 4;
+    if (dy != 0) return dy > 0 ? 1 : 2;
+    return 0;
+}
+
+// scripted "basic" AI of unit i (spec §3.3), pre-step state
+__device__ __forceinline__ int ai_action_reg(const EnvMasks& M, const int (&pk)[16], int i, int pi) {
+    if (pkh(pi) <= 0) return 0;
+    const int xi = pkx(pi), yi = pky(pi);
+    const uint32_t tb = target_bits(M, pk, i, pi);
+    int best = -1, hb = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int hj = pkh(pk[j]);
+        if (((tb >> j) & 1u) && (best < 0 || hj < hb)) { best = j; hb = hj; }
+    }
+    if (best >= 0) return MLG_ACT_BASE + best;
+    const uint32_t mt = (M.team1 >> i) & 1u;
+    if ((M.healer >> i) & 1u) {
+        int near = -1, nd = 0, ndx = 0, ndy = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int p = pk[j];
+            const int dx = pkx(p) - xi, dy = pky(p) - yi, d = dx * dx + dy * dy;
+            const bool cand = j < M.U && j != i && pkh(p) > 0 && ((M.team1 >> j) & 1u) == mt;
+            if (cand && (near < 0 || d < nd)) { near = j; nd = d; ndx = dx; ndy = dy; }
+        }
+        if (near >= 0) return nd > 2 ? move_toward_d(ndx, ndy) : 0;
+    }
+    int near = -1, nd = 0, ndx = 0, ndy = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int p = pk[j];
+        const int dx = pkx(p) - xi, dy = pky(p) - yi, d = dx * dx + dy * dy;
+        const bool cand = j < M.U && pkh(p) > 0 && ((M.team1 >> j) & 1u) != mt;
+        if (cand && (near < 0 || d < nd)) { near = j; nd = d; ndx = dx; ndy = dy; }
+    }
+    return near >= 0 ? move_toward_d(ndx, ndy) : 0;
+}
+
+// new hp of unit u from all executed actions (spec §3.4)
+__device__ __forceinline__ int resolve_hp_reg(const EnvMasks& M, const int (&pk)[16], const int (&act)[16], int u,
+                                              int pu) {
+    const int hu = pkh(pu);
+    if (hu <= 0) return hu;
+    int dmg = 0, heal = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const bool hit = i < M.U && pkh(pk[i]) > 0 && act[i] == MLG_ACT_BASE + u;
+        const bool h = (M.healer >> i) & 1u;
+        heal += (hit && h) ? 4 : 0;
+        dmg += (hit && !h) ? (((M.tank >> i) & 1u) ? 3 : 6) : 0;
+    }
+    const int v = hu - dmg + heal, mx = ((M.tank >> u) & 1u) ? 64 : 32;
+    return v < 0 ? 0 : (v > mx ? mx : v);
+}
+
+// obs-mask row of unit u: bit j = u dead, j dead or out of sight
+__device__ __forceinline__ uint32_t om_bits(const EnvMasks& M, const int (&pk)[16], int u, int pu) {
+    (void)u;
+    if (pkh(pu) <= 0) return (1u << M.U) - 1u;
+    const int xu = pkx(pu), yu = pky(pu);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int p = pk[j];
+        const int dx = pkx(p) - xu, dy = pky(p) - yu;
+        bits |= (uint32_t)(j < M.U && (pkh(p) <= 0 || dx * dx + dy * dy > MLG_SIGHT2)) << j;
+    }
+    return bits;
+}
+
+}  // namespace refil
