@@ -167,7 +167,7 @@ inline int64_t layout_jobs(WJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t*
 // chunks in a fixed order (deterministic).
 namespace mlg {
 
-constexpr int BCH = 1024;        // rows per chunk
+constexpr int BCH = 1024;        // max rows per chunk
 constexpr int BSLAB = 64 * 64 + 64;
 
 struct BJob {
@@ -176,7 +176,7 @@ struct BJob {
     float* dw;
     float* db;
     int64_t ldd, ldx;
-    int M, K, rows, mb, nb, chunks;
+    int M, K, rows, mb, nb, chunks, ch_rows;
     int task0;
     int64_t slab0;
 };
@@ -200,7 +200,11 @@ inline BJob bjob(const float* delta, int64_t ldd, const float* x, int64_t ldx, f
     j.rows = rows;
     j.mb = (M + 63) / 64;
     j.nb = (K + 63) / 64;
-    j.chunks = (rows + BCH - 1) / BCH;
+    // chunk length: up to BCH rows, fewer when the job is small so that it still spreads over >= ~256 waves
+    int ch = rows / (256 / (j.mb * j.nb) + 1);
+    ch = ch < 64 ? 64 : (ch > BCH ? BCH : ch);
+    j.ch_rows = (ch + 3) & ~3;
+    j.chunks = (rows + j.ch_rows - 1) / j.ch_rows;
     j.task0 = 0;
     j.slab0 = 0;
     return j;
@@ -224,7 +228,7 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
     const int ch = local % jb.chunks, blk = local / jb.chunks;
     const int mbi = blk / jb.nb, nbi = blk % jb.nb;
     const int col = lane & 15, g = lane >> 4;
-    const int r0 = ch * BCH, r1 = min(jb.rows, r0 + BCH);
+    const int r0 = ch * jb.ch_rows, r1 = min(jb.rows, r0 + jb.ch_rows);
     floatx4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
