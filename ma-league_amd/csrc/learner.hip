@@ -20,9 +20,9 @@
 
 namespace {
 
-using WJobs = mlg::BJobsT<16>;
-using WJob = mlg::BJob;
-constexpr auto job = mlg::bjob;
+using WJobs = mlg::WJobsT<16>;
+using mlg::WJob;
+using mlg::job;
 using mlg::block_sum_1024;
 
 // ---- canonical flat parameter offsets (nn.Module named_parameters order) ------------------------
@@ -943,9 +943,19 @@ WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
         J.j[J.n++] = job(at(p.w.df2), c.E, off(la, c.HE), L1, mg(m.wf_2w), mg(m.wf_2b), c.E, c.HE, RM);
         J.j[J.n++] = job(at(p.w.dv2), 1, off(la, 2 * c.HE + c.E), L1, mg(m.v2w), mg(m.v2b), 1, c.E, RM);
     }
-    int64_t n_red, slab_part;
-    *slab_floats = mlg::layout_bjobs(J, n_tasks, &n_red, &slab_part);  // slab partials + per-block norm partials
-    p.w.nrm = p.w.slab + slab_part;
+    int tasks = 0;
+    int64_t slab = 0;
+    for (int q = 0; q < J.n; ++q) {
+        J.j[q].task0 = tasks;
+        J.j[q].slab0 = slab;
+        tasks += J.j[q].mt * J.j[q].nt * J.j[q].chunks;
+        slab += (int64_t)J.j[q].mt * J.j[q].nt * J.j[q].chunks * 272;
+    }
+    int64_t n_red = 0;
+    for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
+    *slab_floats = a4(slab) + a4((n_red + 255) / 256);  // slab partials + per-block norm partials
+    p.w.nrm = p.w.slab + a4(slab);
+    *n_tasks = tasks;
     return J;
 }
 
@@ -1013,11 +1023,11 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     int64_t slab_floats;
     int n_tasks;
     WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks);
-    hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((n_tasks + 3) / 4), dim3(256), 0, s, J, ws + p.w.slab);
+    hipLaunchKernelGGL(mlg::wgrad_kernel<16>, dim3((n_tasks + 3) / 4), dim3(256), 0, s, J, ws + p.w.slab);
     int64_t n_red = 0;  // same count as make_jobs
-    for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mb * J.j[q].nb * mlg::BSLAB;
+    for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
     const int n_red_blocks = (int)((n_red + 255) / 256);
-    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + p.w.slab,
+    hipLaunchKernelGGL(mlg::wgrad_reduce_kernel<16>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + p.w.slab,
                        ws + p.w.nrm);
     const int64_t n_par = p.n_agent + p.n_mixer;
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + p.w.part,
