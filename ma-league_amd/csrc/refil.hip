@@ -181,7 +181,10 @@ __device__ inline void entity_block_reg(const float* __restrict__ P, const RAgen
         for (int i = 0; i < 4; ++i) st_row(kvs, LDKV, m0 - 4 + i, acc[i], lane);
     }
     wave_sync();
-    attn_fwd_split(qs, LDX, kvs, kvs + EMB, LDKV, mrow, nq, ne, o, LDX, nullptr, lane);
+    if (nq <= 8)
+        attn_fwd_half(qs, LDX, kvs, kvs + EMB, LDKV, mrow, nq, ne, o, LDX, lane);
+    else
+        attn_fwd_split(qs, LDX, kvs, kvs + EMB, LDKV, mrow, nq, ne, o, LDX, nullptr, lane);
     wave_sync();
 }
 
@@ -202,7 +205,11 @@ __device__ inline void agent_tile_post_w(const float* __restrict__ P, const RAge
     mm_reg<4, 4>(x3, w2, ld2, 0, x2, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x3[i] = relu4(x3[i]);
+#ifdef MLG_REFIL_GRU_PLAIN
     gru_tile(P + L.wih, P + L.whh, P + L.bih, P + L.bhh, P + L.brz, x3, h, lane);
+#else
+    gru_tile_pipe(P + L.wih, P + L.whh, P + L.bih, P + L.bhh, P + L.brz, x3, h, lane);
+#endif
 }
 
 RO_PHASE void agent_tile_post(const float* __restrict__ P, const RAgent& L, const float* o, uint32_t dead,

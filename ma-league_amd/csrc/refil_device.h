@@ -271,6 +271,77 @@ __device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, 
     attn_fwd_split(qkv, LDQ, qkv + EMB, qkv + 2 * EMB, LDQ, mrow, nq, ne, o, ldo, P, lane);
 }
 
+
+// attn_fwd_split for nq <= 8 using all 64 lanes: lane (h = lane >> 4, q = lane & 7, half = (lane >> 3) & 1) scores
+// keys [8 half, 8 half + 8); max, sum and the weighted values are combined with the partner lane (xor 8).
+// Same softmax (exp(s - max) / sum) with a two-way split of the sums.
+__device__ inline void attn_fwd_half(const float* qb, int ldq, const float* kb, const float* vb, int ldkv,
+                                     const uint32_t* mrow, int nq, int ne, float* o, int ldo, int lane) {
+    const int h = lane >> 4, q = lane & 7, half = (lane >> 3) & 1, k0 = half * 8;
+    const bool qv_ok = q < nq;
+    float qv[HD];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const floatx4 v = ld4(qb + q * ldq + h * HD + 4 * c);
+        qv[4 * c] = v[0]; qv[4 * c + 1] = v[1]; qv[4 * c + 2] = v[2]; qv[4 * c + 3] = v[3];
+    }
+    const uint32_t m = (qv_ok ? mrow[q] : 0xFFFFFFFFu) | (ne < 32 ? (~0u << ne) : 0u);
+    float s[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        const int k = k0 + kk;
+        const float* kr = kb + k * ldkv + h * HD;
+        float d = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const floatx4 kv = ld4(kr + 4 * c);
+            d = fmaf(qv[4 * c], kv[0], d);
+            d = fmaf(qv[4 * c + 1], kv[1], d);
+            d = fmaf(qv[4 * c + 2], kv[2], d);
+            d = fmaf(qv[4 * c + 3], kv[3], d);
+        }
+        s[kk] = ((m >> k) & 1u) ? -INFINITY : d * 0.25f;
+        mx = fmaxf(mx, s[kk]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 8));
+    float ov[HD];
+#pragma unroll
+    for (int d = 0; d < HD; ++d) ov[d] = 0.f;
+    float sum = 0.f;
+    if (mx != -INFINITY) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            s[kk] = ((m >> (k0 + kk)) & 1u) ? 0.f : expf(s[kk] - mx);
+            sum += s[kk];
+        }
+    }
+    sum += __shfl_xor(sum, 8);
+    if (mx != -INFINITY) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            const float p = s[kk] / sum;
+            const float* vr = vb + (k0 + kk) * ldkv + h * HD;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const floatx4 vv = ld4(vr + 4 * c);
+                ov[4 * c] = fmaf(p, vv[0], ov[4 * c]);
+                ov[4 * c + 1] = fmaf(p, vv[1], ov[4 * c + 1]);
+                ov[4 * c + 2] = fmaf(p, vv[2], ov[4 * c + 2]);
+                ov[4 * c + 3] = fmaf(p, vv[3], ov[4 * c + 3]);
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < HD; ++d) ov[d] += __shfl_xor(ov[d], 8);
+    if (qv_ok && half == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            *reinterpret_cast<floatx4*>(o + q * ldo + h * HD + 4 * c) =
+                floatx4{ov[4 * c], ov[4 * c + 1], ov[4 * c + 2], ov[4 * c + 3]};
+    }
+}
+
 // Backward of attn_fwd for one item. P: [NH][16][16] saved weights; dO: rows q < nq (cols h*16..);
 // DS: LDS scratch [NH][16][16]; dqkv: LDS [NE][LDQ], written (ACC = false) or accumulated (ACC = true):
 // dQ rows < nq (rows >= nq get 0 when writing), dK / dV all 16 rows.
@@ -406,6 +477,60 @@ __device__ inline void gru_tile(const float* __restrict__ wih, const float* __re
 #ifdef MLG_REFIL_LEAN
             __builtin_amdgcn_sched_barrier(0);
 #endif
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float rg = sigm(ar[r]);
+            const float zg = sigm(az[r]);
+            const float ng = tanhf(ain[r] + rg * ahn[r]);
+            hn[mt][r] = ng + zg * (h[mt][r] - ng);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) h[mt] = hn[mt];
+}
+
+
+// GRUCell tile with software-pipelined weight loads: the 24 weight vectors of output chunk mt + 1 are issued
+// before the MFMAs of chunk mt (weights stream from L2 at one wave per SIMD; 2 x 96 VGPRs in flight).
+__device__ inline void gru_tile_pipe(const float* __restrict__ wih, const float* __restrict__ whh,
+                                     const float* __restrict__ bih, const float* __restrict__ bhh,
+                                     const float* __restrict__ brz, const floatx4 (&x)[4], floatx4 (&h)[4], int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    constexpr int64_t GATE = (int64_t)EMB * EMB;
+    floatx4 wb[2][24];
+    auto load = [&](int mt, floatx4 (&w)[24]) {
+        const float* wi = wih + (int64_t)(mt * 16 + col) * EMB + 4 * g;
+        const float* wh = whh + (int64_t)(mt * 16 + col) * EMB + 4 * g;
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                w[kc * 6 + q] = ld4(wi + q * GATE + kc * 16);
+                w[kc * 6 + 3 + q] = ld4(wh + q * GATE + kc * 16);
+            }
+        }
+    };
+    floatx4 hn[4];
+    load(0, wb[0]);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        if (mt + 1 < 4) load(mt + 1, wb[(mt + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const floatx4(&w)[24] = wb[mt & 1];
+        floatx4 ar = ld4(brz + mt * 16 + 4 * g);
+        floatx4 az = ld4(brz + EMB + mt * 16 + 4 * g);
+        floatx4 ain = ld4(bih + 2 * EMB + mt * 16 + 4 * g);
+        floatx4 ahn = ld4(bhh + 2 * EMB + mt * 16 + 4 * g);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            ar = mfma_chunk(w[kc * 6 + 0], x[kc], ar);
+            az = mfma_chunk(w[kc * 6 + 1], x[kc], az);
+            ain = mfma_chunk(w[kc * 6 + 2], x[kc], ain);
+            ar = mfma_chunk(w[kc * 6 + 3], h[kc], ar);
+            az = mfma_chunk(w[kc * 6 + 4], h[kc], az);
+            ahn = mfma_chunk(w[kc * 6 + 5], h[kc], ahn);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
