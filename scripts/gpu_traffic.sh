@@ -4,8 +4,11 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
+MODE=${MODE:-ai}
+OUT=gpurun_out/pmc_$MODE
+mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc/$c" -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline > gpurun_out/pmc/$c.json 2> gpurun_out/pmc/$c.err || { echo "pmc $c failed"; tail -5 gpurun_out/pmc/$c.err; exit 1; }
+  timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/$c" -o run -- python3 bench.py --mode $MODE --steps 4 --warmup 2 --no-cpu-baseline > $OUT/$c.json 2> $OUT/$c.err || { echo "pmc $c failed"; tail -5 $OUT/$c.err; exit 1; }
 done
-python3 scripts/parse_traffic.py gpurun_out/pmc > gpurun_out/pmc/traffic.json || exit 1
-cat gpurun_out/pmc/traffic.json
+python3 scripts/parse_traffic.py $OUT > $OUT/traffic.json || exit 1
+cat $OUT/traffic.json
