@@ -171,16 +171,42 @@ __device__ __forceinline__ float mask_at(const MlgBatch& bt, int b, int t) {
 
 __global__ void mask_sum_kernel(MlgBatch bt, int B, int T, float* __restrict__ msum) {
     __shared__ float red[1024];
+    // msum[1] = max_t_filled (the reference's truncation, ma_experiment.py:235-239): the learner uses transitions
+    // t < max_t_filled - 1 only; the sequential kernels stop there and the per-t kernels skip the steps beyond
+    int mx = 0;  // a wave per episode: filled steps counted with ballots
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int b = wave; b < B; b += nw) {
+        const int64_t base = bslot(bt, b) * bt.T1;
+        int n = 0;
+        for (int t0 = 0; t0 < T; t0 += 64) {
+            const int t = t0 + lane;
+            n += __popcll(__ballot(t < T && bt.filled[base + t] != 0));
+        }
+        mx = n > mx ? n : mx;
+    }
+    red[threadIdx.x] = (float)mx;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    const int Te = (int)fminf(fmaxf(red[0], 2.f), (float)T);
+    __syncthreads();
     float s = 0.f;
-    for (int i = threadIdx.x; i < B * (T - 1); i += blockDim.x) s += mask_at(bt, i / (T - 1), i % (T - 1));
+    for (int i = threadIdx.x; i < B * (Te - 1); i += blockDim.x) s += mask_at(bt, i / (Te - 1), i % (Te - 1));
     red[threadIdx.x] = s;
     __syncthreads();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) msum[0] = red[0];
+    if (threadIdx.x == 0) {
+        msum[0] = red[0];
+        msum[1] = (float)Te;
+    }
 }
+
+__device__ __forceinline__ int t_eff(const float* msum) { return (int)msum[1]; }
 
 // ================================================================================================
 // 16-row x 16-feature tile product with the activation operand in LDS, row-major [16][lda]:
@@ -208,11 +234,12 @@ template <int H>
 __global__ void __launch_bounds__(512) agent_in_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ Pon,
                                                        const float* __restrict__ Ptg, float* __restrict__ ws_in,
                                                        float* __restrict__ ws_x, float* __restrict__ gi_on,
-                                                       float* __restrict__ gi_tg) {
+                                                       float* __restrict__ gi_tg, const float* __restrict__ msum) {
     constexpr int HC = H / 16;
     constexpr int LDA = H + 4;
     __shared__ __attribute__((aligned(16))) float xs[16 * LDA];
     const int tile = blockIdx.x, t = blockIdx.y;
+    if (t >= t_eff(msum)) return;
     const bool online = blockIdx.z == 0;
     const float* P = online ? Pon : Ptg;
     float* gi = online ? gi_on : gi_tg;
@@ -273,10 +300,11 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
                                                         const float* __restrict__ gi_tg, float* __restrict__ hs_on,
                                                         float* __restrict__ hs_tg, float* __restrict__ ws_gr,
                                                         float* __restrict__ ws_gz, float* __restrict__ ws_gn,
-                                                        float* __restrict__ ws_ghn) {
+                                                        float* __restrict__ ws_ghn, const float* __restrict__ msum) {
     constexpr int HC = H / 16;
     constexpr int LDA = H + 4;
     __shared__ __attribute__((aligned(16))) float hs[2][16 * LDA];
+    const int Te = t_eff(msum);
     const int ntiles = (c.R + 15) / 16;
     const bool online = blockIdx.x < ntiles;
     const int tile = online ? blockIdx.x : blockIdx.x - ntiles;
@@ -302,10 +330,10 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
     floatx4 nr = gi_at(0, 0), nz = gi_at(0, 1), nn = gi_at(0, 2);
     __syncthreads();
     int cur = 0;
-    for (int t = 0; t < c.T; ++t) {
+    for (int t = 0; t < Te; ++t) {
         floatx4 ar = nr, az = nz;
         const floatx4 gin = nn;
-        if (t + 1 < c.T) {  // prefetch the next step's input gates
+        if (t + 1 < Te) {  // prefetch the next step's input gates
             nr = gi_at(t + 1, 0);
             nz = gi_at(t + 1, 1);
             nn = gi_at(t + 1, 2);
@@ -349,9 +377,10 @@ template <int H>
 __global__ void __launch_bounds__(512) agent_q_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
                                                       const float* __restrict__ Ptg, const float* __restrict__ hs_on,
                                                       const float* __restrict__ hs_tg, float* __restrict__ mac,
-                                                      float* __restrict__ tmac) {
+                                                      float* __restrict__ tmac, const float* __restrict__ msum) {
     constexpr int HC = H / 16;
     const int tile = blockIdx.x, t = blockIdx.y;
+    if (t >= t_eff(msum)) return;
     const bool online = blockIdx.z == 0;
     const float* P = online ? Pon : Ptg;
     const float* hsg = (online ? hs_on : hs_tg) + (int64_t)(t + 1) * c.R * H;
@@ -517,7 +546,7 @@ __global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs
     float cq[MAXN], tq[MAXN];
     for (int n = 0; n < N; ++n) cq[n] = tq[n] = 0.f;
     if (valid) gather_q(c, bt, mac, tmac, b, t, cq, tq);
-    const float m = valid ? mask_at(bt, b, t) : 0.f;
+    const float m = (valid && t < t_eff(msum_p) - 1) ? mask_at(bt, b, t) : 0.f;  // reference truncation
     const float rwd = valid ? bt.reward[bslot(bt, b) * bt.T1 + t] : 0.f;
     const float term = valid ? (float)bt.terminated[bslot(bt, b) * bt.T1 + t] : 0.f;
     const float msum = msum_p[0];
@@ -664,7 +693,8 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
                                                         const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
                                                         const float* __restrict__ ws_gz, const float* __restrict__ ws_gn,
                                                         const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
-                                                        float* __restrict__ dgi, float* __restrict__ dgh) {
+                                                        float* __restrict__ dgi, float* __restrict__ dgh,
+                                                        const float* __restrict__ msum) {
     constexpr int LDG = 3 * H + 4;
     constexpr int KC = 3 * H / 16;
     __shared__ __attribute__((aligned(16))) float sgh[2][16 * LDG];
@@ -703,10 +733,21 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
         }
         return s;
     };
+    const int Te = t_eff(msum);
+    if (valid) {  // steps past max_t_filled: zero deltas (wgrad rows)
+        for (int t = Te; t < c.T; ++t) {
+            const int64_t o3 = ((int64_t)t * R + r) * 3 * H + f0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                *reinterpret_cast<floatx4*>(dgi + o3 + q * H) = floatx4{0.f, 0.f, 0.f, 0.f};
+                *reinterpret_cast<floatx4*>(dgh + o3 + q * H) = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
     floatx4 dh = {0.f, 0.f, 0.f, 0.f};
-    Step nx = load_step(c.T - 1);
+    Step nx = load_step(Te - 1);
     int cur = 0;
-    for (int t = c.T - 1; t >= 0; --t) {
+    for (int t = Te - 1; t >= 0; --t) {
         const Step s = nx;
         if (t > 0) nx = load_step(t - 1);
         if (valid && t < c.T - 1) dh += s.dq * s.w2;
@@ -749,12 +790,17 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
 template <int H>
 __global__ void __launch_bounds__(512) agent_dx_kernel(LCfg c, const float* __restrict__ wihT,
                                                        const float* __restrict__ ws_x, const float* __restrict__ dgi,
-                                                       float* __restrict__ da) {
+                                                       float* __restrict__ da, const float* __restrict__ msum) {
     const int tile = blockIdx.x, t = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int col = lane & 15, g = lane >> 4;
     const int r = tile * 16 + col;
     const bool valid = r < c.R;
+    if (t >= t_eff(msum)) {
+        if (valid)
+            *reinterpret_cast<floatx4*>(da + ((int64_t)t * c.R + r) * H + w * 16 + 4 * g) = floatx4{0.f, 0.f, 0.f, 0.f};
+        return;
+    }
     const int64_t row = (int64_t)t * c.R + (valid ? r : 0);
     const float* wrow = wihT + (int64_t)(w * 16 + col) * 3 * H + 4 * g;
     const float* grow = dgi + row * 3 * H + 4 * g;
@@ -1006,20 +1052,21 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     const int ntiles = (c.R + 15) / 16;
     const int threads = (c.H / 16) * 64;
     hipLaunchKernelGGL((agent_in_kernel<H>), dim3(ntiles, c.T, 2), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
-                       ws + p.w.p_tg, ws + p.w.in, ws + p.w.x, ws + p.w.gi_on, ws + p.w.gi_tg);
+                       ws + p.w.p_tg, ws + p.w.in, ws + p.w.x, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.msum);
     hipLaunchKernelGGL((agent_rec_kernel<H>), dim3(2 * ntiles), dim3(threads), 0, s, c, p.L, ws + p.w.p_on, ws + p.w.p_tg,
                        ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.gr, ws + p.w.gz,
-                       ws + p.w.gn, ws + p.w.ghn);
+                       ws + p.w.gn, ws + p.w.ghn, ws + p.w.msum);
     hipLaunchKernelGGL((agent_q_kernel<H>), dim3(ntiles, c.T, 2), dim3(64 * (c.Ap / 16)), 0, s, c, p.L, ws + p.w.p_on,
-                       ws + p.w.p_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.mac, ws + p.w.tmac);
+                       ws + p.w.p_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum);
     MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
               ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
     hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(64), 0, s, c, bt, Mon, Mtg, p.mp,
                        ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
     hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on, ws + p.w.hs,
-                       ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi, ws + p.w.dgh);
+                       ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi, ws + p.w.dgh,
+                       ws + p.w.msum);
     hipLaunchKernelGGL((agent_dx_kernel<H>), dim3(ntiles, c.T), dim3(threads), 0, s, c, ws + p.w.wihT, ws + p.w.x,
-                       ws + p.w.dgi, ws + p.w.da);
+                       ws + p.w.dgi, ws + p.w.da, ws + p.w.msum);
     int64_t slab_floats;
     int n_tasks;
     WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks);

@@ -249,16 +249,42 @@ __device__ __forceinline__ float emask_at(const MlgEntityBatch& bt, int b, int t
 
 __global__ void mask_sum_kernel(MlgEntityBatch bt, int B, int T, float* __restrict__ msum) {
     __shared__ float red[1024];
+    // msum[1] = max_t_filled (the reference's truncation, ma_experiment.py:235-239): the learner uses transitions
+    // t < max_t_filled - 1 only; the sequential kernels stop there and the per-t kernels skip the steps beyond
+    int mx = 0;  // a wave per episode: filled steps counted with ballots
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int b = wave; b < B; b += nw) {
+        const int64_t base = eslot(bt, b) * bt.T1;
+        int n = 0;
+        for (int t0 = 0; t0 < T; t0 += 64) {
+            const int t = t0 + lane;
+            n += __popcll(__ballot(t < T && bt.filled[base + t] != 0));
+        }
+        mx = n > mx ? n : mx;
+    }
+    red[threadIdx.x] = (float)mx;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    const int Te = (int)fminf(fmaxf(red[0], 2.f), (float)T);
+    __syncthreads();
     float s = 0.f;
-    for (int i = threadIdx.x; i < B * (T - 1); i += blockDim.x) s += emask_at(bt, i / (T - 1), i % (T - 1));
+    for (int i = threadIdx.x; i < B * (Te - 1); i += blockDim.x) s += emask_at(bt, i / (Te - 1), i % (Te - 1));
     red[threadIdx.x] = s;
     __syncthreads();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) msum[0] = red[0];
+    if (threadIdx.x == 0) {
+        msum[0] = red[0];
+        msum[1] = (float)Te;
+    }
 }
+
+__device__ __forceinline__ int t_eff(const float* msum) { return (int)msum[1]; }
 
 // entity inputs ein[i][j][c] (K1 columns, zero padded)
 __global__ void ein_kernel(RCfg c, MlgEntityBatch bt, float* __restrict__ ein) {
@@ -321,7 +347,7 @@ struct AgentPtrs {
 
 __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
                                                      RAgent L, const float* __restrict__ ein, AgentPtrs on,
-                                                     AgentPtrs tg) {
+                                                     AgentPtrs tg, const float* __restrict__ msum) {
     __shared__ float s_ein[NE * LDI];
     __shared__ float s_x1[NE * LDX];
     __shared__ float s_qkv[NE * LDQ];
@@ -334,10 +360,13 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, 
     const int ncopy = online ? 3 : 1;
     const int R = online ? c.Ron : c.Rtg;
     const int i0 = blockIdx.x * 2;
+    const int Te = t_eff(msum);
+    const bool v0 = i0 < c.I && i0 % c.T < Te, v1 = i0 + 1 < c.I && (i0 + 1) % c.T < Te;
+    if (!v0 && !v1) return;  // both items past max_t_filled
     for (int k = lane; k < 3 * 16 * LDX; k += 64) (&s_o[0][0])[k] = 0.f;
     if (lane < 32) {
         const int e = lane >> 4, q = lane & 15, i = i0 + e;
-        if (i < c.I) {
+        if (i < c.I && i % c.T < Te) {
             const int b = i / c.T, t = i % c.T;
             const uint32_t om = om_row(c, bt, b, t, q);
             s_m[0][e][q] = om;
@@ -357,7 +386,7 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, 
     wave_sync();
     for (int e = 0; e < 2; ++e) {
         const int i = i0 + e;
-        if (i >= c.I) continue;
+        if (i >= c.I || i % c.T >= Te) continue;
         for (int k = lane; k < NE * c.K1; k += 64) s_ein[(k / c.K1) * LDI + k % c.K1] = ein[(int64_t)i * NE * c.K1 + k];
         wave_sync();
         dense_lds<true>(A.P + L.w1, L.K1, A.P + L.b1, EMB / 16, s_ein, LDI, L.K1 / 16, s_x1, LDX, lane);
@@ -376,7 +405,7 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, 
     }
     const int col = lane & 15, g = lane >> 4;
     const int e = col >> 3, n = col & 7, i = i0 + e;
-    const bool valid = i < c.I && n < c.NA;
+    const bool valid = i < c.I && n < c.NA && i % c.T < Te;
     const int b = valid ? i / c.T : 0, t = valid ? i % c.T : 0;
     const uint32_t dead = s_dead[0] | (s_dead[1] << 8);
     const bool rdead = (dead >> col) & 1u;
@@ -424,8 +453,9 @@ __global__ void __launch_bounds__(256) rec_kernel(RCfg c, RAgent L, const float*
                                                   const float* __restrict__ gi_tg, float* __restrict__ hs_on,
                                                   float* __restrict__ hs_tg, float* __restrict__ ws_gr,
                                                   float* __restrict__ ws_gz, float* __restrict__ ws_gn,
-                                                  float* __restrict__ ws_ghn) {
+                                                  float* __restrict__ ws_ghn, const float* __restrict__ msum) {
     constexpr int H = EMB, HC = 4;
+    const int Te = t_eff(msum);
     __shared__ __attribute__((aligned(16))) float hs[2][16 * LDX];
     const int nt_on = (c.Ron + 15) / 16;
     const bool online = (int)blockIdx.x < nt_on;
@@ -452,10 +482,10 @@ __global__ void __launch_bounds__(256) rec_kernel(RCfg c, RAgent L, const float*
     floatx4 nr = gi_at(0, 0), nz = gi_at(0, 1), nn = gi_at(0, 2);
     __syncthreads();
     int cur = 0;
-    for (int t = 0; t < c.T; ++t) {
+    for (int t = 0; t < Te; ++t) {
         floatx4 ar = nr, az = nz;
         const floatx4 gin = nn;
-        if (t + 1 < c.T) {
+        if (t + 1 < Te) {
             nr = gi_at(t + 1, 0);
             nz = gi_at(t + 1, 1);
             nn = gi_at(t + 1, 2);
@@ -504,11 +534,11 @@ __device__ __forceinline__ void row_bn(const RCfg& c, int r, int& b, int& n) {
 __global__ void __launch_bounds__(128) q_kernel(RCfg c, MlgEntityBatch bt, RAgent L, const float* __restrict__ Pon,
                                                 const float* __restrict__ Ptg, const float* __restrict__ hs_on,
                                                 const float* __restrict__ hs_tg, float* __restrict__ mac,
-                                                float* __restrict__ tmac) {
+                                                float* __restrict__ tmac, const float* __restrict__ msum) {
     const bool online = blockIdx.z == 0;
     const int R = online ? c.Ron : c.Rtg;
     const int tile = blockIdx.x, t = blockIdx.y;
-    if (tile * 16 >= R) return;
+    if (tile * 16 >= R || t >= t_eff(msum)) return;
     const float* P = online ? Pon : Ptg;
     const float* hsg = (online ? hs_on : hs_tg) + (int64_t)(t + 1) * R * EMB;
     float* qout = online ? mac : tmac;
@@ -545,7 +575,8 @@ struct HypPtrs {
 };
 
 __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
-                                                       RHyper L, const float* __restrict__ ein, HypPtrs hp) {
+                                                       RHyper L, const float* __restrict__ ein, HypPtrs hp,
+                                                       const float* __restrict__ msum) {
     __shared__ float s_ein[NE * LDI];
     __shared__ float s_x1[NE * LDX];
     __shared__ float s_qkv[NE * LDQ];
@@ -555,7 +586,7 @@ __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt
     const int lane = threadIdx.x;
     const int i = blockIdx.x, k = blockIdx.y & 3, net = blockIdx.y >> 2;
     const int b = i / c.T, t = i % c.T;
-    if (t == c.T - 1) {  // no mixer item: zero the wgrad inputs of the online item (never NaN garbage)
+    if (t >= t_eff(msum) - 1) {  // no (unmasked) mixer item: zero the wgrad inputs of the online item
         if (!net) {
             for (int q = lane; q < NE * EMB; q += 64) hp.x1m[k][(int64_t)i * NE * EMB + q] = 0.f;
             for (int v = 0; v < nvar(k); ++v)
@@ -669,13 +700,14 @@ __device__ __forceinline__ float mw_bwd(float dy, float y, float x, int softmax)
 }
 
 __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, MixIO io) {
+    const int Te = (int)io.msum[1];
     const int lane = threadIdx.x;
     const int i = blockIdx.x;
     const int b = i / c.T, t = i % c.T;
     const int e = lane & 31;
     const int NA = c.NA;
     float* part = io.part + (int64_t)i * 8;
-    if (t == c.T - 1) {
+    if (t >= Te - 1) {  // t = T - 1, or past max_t_filled (mask 0): no loss, zero deltas
         if (lane < 8) part[lane] = 0.f;
         for (int k = 0; k < 4; ++k)
             for (int v = 0; v < nvar(k); ++v)
@@ -843,7 +875,8 @@ struct HypBwd {
     float* dfc1m[4];
 };
 
-__global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c, MlgEntityBatch bt, HypBwd hb) {
+__global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c, MlgEntityBatch bt, HypBwd hb,
+                                                       const float* __restrict__ msum) {
     __shared__ float s_qkv[NE * LDQ];
     __shared__ float s_dqkv[NE * LDQ];
     __shared__ float s_do[32 * LDX];
@@ -853,7 +886,7 @@ __global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c, MlgEntityBatch bt
     const int b = i / c.T, t = i % c.T;
     const int V = nvar(k);
     const int col = lane & 15, g = lane >> 4;
-    if (t == c.T - 1) {
+    if (t >= t_eff(msum) - 1) {
         for (int q = lane; q < V * NAS * EMB; q += 64) {
             const int v = q / (NAS * EMB), rem = q % (NAS * EMB);
             hb.doutm[k][((int64_t)v * c.I + i) * NAS * EMB + rem] = 0.f;
@@ -918,7 +951,8 @@ __global__ void __launch_bounds__(256) rec_bwd_kernel(RCfg c, MlgEntityBatch bt,
                                                       const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
                                                       const float* __restrict__ ws_gz, const float* __restrict__ ws_gn,
                                                       const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
-                                                      float* __restrict__ dgi, float* __restrict__ dgh) {
+                                                      float* __restrict__ dgi, float* __restrict__ dgh,
+                                                      const float* __restrict__ msum) {
     constexpr int H = EMB;
     constexpr int LDG = 3 * H + 4;
     constexpr int KC = 3 * H / 16;
@@ -959,10 +993,21 @@ __global__ void __launch_bounds__(256) rec_bwd_kernel(RCfg c, MlgEntityBatch bt,
         }
         return s;
     };
+    const int Te = t_eff(msum);
+    if (valid) {  // steps past max_t_filled: zero deltas (wgrad rows)
+        for (int t = Te; t < c.T; ++t) {
+            const int64_t o3 = ((int64_t)t * R + r) * 3 * H + f0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                *reinterpret_cast<floatx4*>(dgi + o3 + q * H) = floatx4{0.f, 0.f, 0.f, 0.f};
+                *reinterpret_cast<floatx4*>(dgh + o3 + q * H) = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
     floatx4 dh = {0.f, 0.f, 0.f, 0.f};
-    Step nx = load_step(c.T - 1);
+    Step nx = load_step(Te - 1);
     int cur = 0;
-    for (int t = c.T - 1; t >= 0; --t) {
+    for (int t = Te - 1; t >= 0; --t) {
         const Step s = nx;
         if (t > 0) nx = load_step(t - 1);
         if (valid && t < c.T - 1) dh += s.dq * s.w3;
@@ -1008,7 +1053,8 @@ struct EntBwd {
     float *dfc2, *dout, *dqkv, *dfc1;
 };
 
-__global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, EntBwd eb) {
+__global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, EntBwd eb,
+                                                     const float* __restrict__ msum) {
     __shared__ float s_do[3][16 * LDX];
     __shared__ float s_qkv[NE * LDQ];
     __shared__ float s_dqkv[NE * LDQ];
@@ -1022,13 +1068,26 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, 
         s_dead[lane] = i < c.I ? dead_bits(c, em_bits(c, bt, i / c.T, i % c.T)) : 0xFFu;
     }
     wave_sync();
+    const int Te = t_eff(msum);
     const int e = col >> 3, n = col & 7, i = i0 + e;
-    const bool valid = i < c.I && n < c.NA;
-    const int b = valid ? i / c.T : 0, t = valid ? i % c.T : 0;
+    const bool row_ok = i < c.I && n < c.NA;
+    const bool valid = row_ok && i % c.T < Te;  // items past max_t_filled: zero deltas, no math
+    const int b = row_ok ? i / c.T : 0, t = row_ok ? i % c.T : 0;
     const uint32_t dead = s_dead[0] | (s_dead[1] << 8);
     const bool rdead = (dead >> col) & 1u;
+    const bool any = (i0 < c.I && i0 % c.T < Te) || (i0 + 1 < c.I && (i0 + 1) % c.T < Te);
     for (int cc = 0; cc < 3; ++cc) {
         const int64_t ro = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * c.NA + n;
+        if (!any) {
+            if (row_ok) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    *reinterpret_cast<floatx4*>(eb.dfc2 + ro * EMB + q * 16 + 4 * g) = floatx4{0.f, 0.f, 0.f, 0.f};
+                    *reinterpret_cast<floatx4*>(eb.dout + ro * EMB + q * 16 + 4 * g) = floatx4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            continue;
+        }
         // dx3 = W_ih^T dGI, relu'
         floatx4 d3[4];
         bias_init<4>(d3, nullptr, 0, lane);
@@ -1038,7 +1097,7 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, 
             const floatx4 xv = ld4(eb.x3 + (valid ? ro : 0) * EMB + q * 16 + 4 * g);
 #pragma unroll
             for (int r = 0; r < 4; ++r) d3[q][r] = (valid && xv[r] > 0.f) ? d3[q][r] : 0.f;
-            if (valid) *reinterpret_cast<floatx4*>(eb.dfc2 + ro * EMB + q * 16 + 4 * g) = d3[q];
+            if (row_ok) *reinterpret_cast<floatx4*>(eb.dfc2 + ro * EMB + q * 16 + 4 * g) = d3[q];
         }
         // dx2 = W2^T dfc2, post mask -> dout
         floatx4 d2[4];
@@ -1048,7 +1107,7 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, 
 #pragma unroll
             for (int q = 0; q < 4; ++q) d2[q] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
-        if (valid) {
+        if (row_ok) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) *reinterpret_cast<floatx4*>(eb.dout + ro * EMB + q * 16 + 4 * g) = d2[q];
         }
@@ -1062,6 +1121,11 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, 
     for (int ee = 0; ee < 2; ++ee) {
         const int ii = i0 + ee;
         if (ii >= c.I) continue;
+        if (ii % c.T >= Te) {  // past max_t_filled: zero deltas
+            for (int q = lane; q < NE * 3 * EMB; q += 64) eb.dqkv[(int64_t)ii * NE * 3 * EMB + q] = 0.f;
+            for (int q = lane; q < NE * EMB; q += 64) eb.dfc1[(int64_t)ii * NE * EMB + q] = 0.f;
+            continue;
+        }
         for (int q = lane; q < NE * 3 * EMB; q += 64)
             s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = eb.qkv[(int64_t)ii * NE * 3 * EMB + q];
         wave_sync();
@@ -1204,12 +1268,13 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on};
     AgentPtrs tg{ws + w.pa_tg, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ws + w.gi_tg};
     hipLaunchKernelGGL(ent_fwd_kernel, dim3((unsigned)((c.I + 1) / 2), 2), dim3(64), 0, s, c, bt, bufs->groupA, La,
-                       ws + w.ein, on, tg);
+                       ws + w.ein, on, tg, ws + w.msum);
     const int nt_on = (c.Ron + 15) / 16, nt_tg = (c.Rtg + 15) / 16;
     hipLaunchKernelGGL(rec_kernel, dim3((unsigned)(nt_on + nt_tg)), dim3(256), 0, s, c, La, ws + w.pa_on, ws + w.pa_tg,
-                       ws + w.gi_on, ws + w.gi_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn);
+                       ws + w.gi_on, ws + w.gi_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn,
+                       ws + w.msum);
     hipLaunchKernelGGL(q_kernel, dim3((unsigned)nt_on, (unsigned)c.T, 2), dim3(64 * (c.Ap / 16)), 0, s, c, bt, La,
-                       ws + w.pa_on, ws + w.pa_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.mac, ws + w.tmac);
+                       ws + w.pa_on, ws + w.pa_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.mac, ws + w.tmac, ws + w.msum);
     // ---- mixer ----
     HypPtrs hp;
     for (int k = 0; k < 4; ++k) {
@@ -1223,7 +1288,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hp.X[k] = ws + w.X[k];
         hp.Xtg[k] = ws + w.Xtg[k];
     }
-    hipLaunchKernelGGL(hyper_fwd_kernel, dim3((unsigned)c.I, 8), dim3(64), 0, s, c, bt, bufs->groupA, p.Lh, ws + w.ein, hp);
+    hipLaunchKernelGGL(hyper_fwd_kernel, dim3((unsigned)c.I, 8), dim3(64), 0, s, c, bt, bufs->groupA, p.Lh, ws + w.ein, hp,
+                       ws + w.msum);
     MixIO io;
     for (int k = 0; k < 4; ++k) {
         io.X[k] = ws + w.X[k];
@@ -1251,13 +1317,13 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hb.dqkvm[k] = ws + w.dqkvm[k];
         hb.dfc1m[k] = ws + w.dfc1m[k];
     }
-    hipLaunchKernelGGL(hyper_bwd_kernel, dim3((unsigned)c.I, 4), dim3(64), 0, s, c, bt, hb);
+    hipLaunchKernelGGL(hyper_bwd_kernel, dim3((unsigned)c.I, 4), dim3(64), 0, s, c, bt, hb, ws + w.msum);
     // ---- agent backward ----
     hipLaunchKernelGGL(rec_bwd_kernel, dim3((unsigned)nt_on), dim3(256), 0, s, c, bt, La, ws + w.pa_on, ws + w.hs_on,
-                       ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.dq, ws + w.dgi, ws + w.dgh);
+                       ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.dq, ws + w.dgi, ws + w.dgh, ws + w.msum);
     EntBwd eb{ws + w.a_wihT, ws + w.a_w2T, ws + w.a_woutT, ws + w.a_winT, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.x3,
               ws + w.dgi, ws + w.dfc2, ws + w.dout, ws + w.dqkv, ws + w.dfc1};
-    hipLaunchKernelGGL(ent_bwd_kernel, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt, eb);
+    hipLaunchKernelGGL(ent_bwd_kernel, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt, eb, ws + w.msum);
     // ---- weight gradients, clip, RMSprop ----
     int64_t slab_floats, n_red;
     int n_tasks;

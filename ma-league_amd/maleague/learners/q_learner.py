@@ -144,7 +144,7 @@ class QLearner(Learner):
         if need < 0:
             raise _native.NativeError(lib.mlg_last_error().decode())
         if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(int(need * 1.25) + 1024, dtype=torch.float32, device=self.device)
+            self._ws = torch.zeros(int(need * 1.25) + 1024, dtype=torch.float32, device=self.device)
         mb, keep = mlg_batch(batch)
         bufs = _native.MlgLearnerBufs(mb, self._flat.flat.data_ptr(), self._grads.data_ptr(), self._sq.data_ptr(),
                               self._tflat.flat.data_ptr(), self._ws.data_ptr(), self._stats.data_ptr())

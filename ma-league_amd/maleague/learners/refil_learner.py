@@ -103,7 +103,7 @@ class REFILLearner(Learner):
             raise _native.NativeError(lib.mlg_last_error().decode())
         if self._ws is None or self._ws.numel() < need:
             self._ws = None
-            self._ws = torch.empty(int(need * 1.1) + 1024, dtype=torch.float32, device=self.device)
+            self._ws = torch.zeros(int(need * 1.1) + 1024, dtype=torch.float32, device=self.device)
         if groupA is None:
             p = torch.rand(B, 1, device=self.device).expand(B, NE)
             groupA = torch.bernoulli(p).to(torch.uint8)

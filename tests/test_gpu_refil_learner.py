@@ -107,3 +107,22 @@ def test_refil_learner_matches_oracle_on_hip_rollouts(device, softmax, double_q)
         for k, v in L.mixer.named_parameters():
             np.testing.assert_allclose(v.detach().cpu().numpy(), ref.mixer[k].detach().numpy(), atol=2e-5, rtol=0,
                                        err_msg=f"call {call} mixer {k}")
+
+
+def test_refil_learner_padded_steps_are_inert(device, golden):
+    """The learner stops at max_t_filled on the device: the golden batch padded with 9 empty timesteps (the
+    in-place sampled view's full buffer length) trains exactly like the unpadded one (reference truncation)."""
+    d = golden("refil_learner.npz")
+    a = refil_args(device="cuda")
+    arrs = _pre(d, "b.")
+    pad = {k: np.concatenate([v, np.zeros((v.shape[0], 9) + v.shape[2:], v.dtype)], axis=1) for k, v in arrs.items()}
+    L1, _ = _learner(_batch_from(arrs, device), _pre(d, "p0.agent."), _pre(d, "p0.mixer."), a)
+    L2, _ = _learner(_batch_from(pad, device), _pre(d, "p0.agent."), _pre(d, "p0.mixer."), a)
+    for call in range(2):
+        g = torch.from_numpy(d[f"c{call}.groupA"])
+        L1.train(_batch_from(arrs, device), 0, episode_num=call, groupA=g)
+        L2.train(_batch_from(pad, device), 0, episode_num=call, groupA=g)
+        s1, s2 = L1.last_stats, L2.last_stats
+        for k in s1:
+            np.testing.assert_allclose(s2[k], s1[k], rtol=1e-5, atol=1e-7, err_msg=k)
+        np.testing.assert_allclose(L2._flat.flat.cpu().numpy(), L1._flat.flat.cpu().numpy(), atol=1e-6, rtol=0)
