@@ -19,7 +19,7 @@
 
 struct AgentLayout {
     int H, A, Ap, N, d_obs, Dob, d_in, Dip, last_action, agent_id;
-    int64_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;
+    int32_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;  // 32-bit: fewer SGPRs in kernels
 };
 
 __host__ __device__ inline int64_t mlg_align4(int64_t v) { return (v + 3) & ~int64_t(3); }
@@ -82,7 +82,7 @@ __device__ __forceinline__ floatx4 load_chunk(const float* x, int k0, int n) {
 // 16-byte bank slots).  Offsets are in floats from p.
 struct WView {
     const float* p;
-    int64_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2;
+    int32_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2;
     int ldd, ldo, ldh;
 };
 
@@ -97,7 +97,7 @@ __host__ __device__ inline WView global_view(const float* P, const AgentLayout& 
 
 // LDS image used by the rollout kernel (no dense w1d): offsets relative to the LDS base.
 struct LdsWeights {
-    int64_t w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;
+    int32_t w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;
     int ldo, ldh;
 };
 __host__ __device__ inline LdsWeights make_lds_weights(const AgentLayout& L) {

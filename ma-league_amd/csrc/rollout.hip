@@ -114,7 +114,7 @@ struct RoEnv {
 
 // Dynamic-LDS carve of the env part (4-byte words).
 struct RoEnvLds {
-    int64_t spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, list, misc, slot2, ret2;
+    int32_t spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, list, misc, slot2, ret2;
 };
 
 __host__ __device__ inline int64_t ro_take(int64_t& o, int64_t n) {
@@ -453,7 +453,7 @@ __device__ __forceinline__ void ro_record_action(const MlgEnvSpec& spec, const R
 // episode with the GRU hidden state in VGPRs. Tiles never mix sides: side s owns tiles [s tps, (s+1) tps),
 // row r of side s = env (r / nh), agent s nh + r % nh.
 struct RolloutLds {
-    int64_t wts, total;
+    int32_t wts, total;
     RoEnvLds env;
     LdsWeights lw;
     int weights_in_lds;
@@ -773,7 +773,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
 // Env phase: half-wave per env, lane per unit (v2 env above); wave w steps envs 2w and 2w + 1.
 // Barriers per step: A|B, B|C, C|env, env|A.
 struct RolloutLds2 {
-    int64_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, total;
+    int32_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, total;
     int ldo, ldh;
     RoEnvLds env;
 };
