@@ -123,27 +123,27 @@ __host__ __device__ inline int64_t ro_take(int64_t& o, int64_t n) {
     return v;
 }
 
-__host__ __device__ inline RoEnvLds make_env_lds(int64_t& o, int U, int n_agents) {
+__host__ __device__ inline RoEnvLds make_env_lds(int64_t& o, int U, int n_agents, int re = RE) {
     RoEnvLds r;
     r.spec = ro_take(o, (int64_t)(sizeof(SpecShared) / 4));
-    const int64_t eu = (int64_t)RE * U;
+    const int64_t eu = (int64_t)re * U;
     r.x = ro_take(o, eu);
     r.y = ro_take(o, eu);
     r.hp = ro_take(o, eu);
     r.nhp = ro_take(o, eu);
     r.act = ro_take(o, eu);
-    r.pact = ro_take(o, (int64_t)RE * n_agents);
-    r.prev = ro_take(o, (int64_t)RE * n_agents);
-    r.status = ro_take(o, RE);
-    r.stepped = ro_take(o, RE);
-    r.len = ro_take(o, RE);
-    r.episode = ro_take(o, RE);
-    r.ret = ro_take(o, RE);
-    r.slot = ro_take(o, RE);
-    r.list = ro_take(o, RE);
+    r.pact = ro_take(o, (int64_t)re * n_agents);
+    r.prev = ro_take(o, (int64_t)re * n_agents);
+    r.status = ro_take(o, re);
+    r.stepped = ro_take(o, re);
+    r.len = ro_take(o, re);
+    r.episode = ro_take(o, re);
+    r.ret = ro_take(o, re);
+    r.slot = ro_take(o, re);
+    r.list = ro_take(o, re);
     r.misc = ro_take(o, 4);  // [0] any env running, [1] number of running envs
-    r.slot2 = ro_take(o, RE);
-    r.ret2 = ro_take(o, RE);
+    r.slot2 = ro_take(o, re);
+    r.ret2 = ro_take(o, re);
     return r;
 }
 
@@ -774,11 +774,11 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
 // Barriers per step: A|B, B|C, C|env, env|A.
 struct RolloutLds2 {
     int32_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, total;
-    int ldo, ldh;
+    int ldo, ldh, nhb;  // nhb: hidden-state buffers (2: double buffered by step parity; 1: v6, see below)
     RoEnvLds env;
 };
 
-__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N, int rew) {
+__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N, int rew, int nhb = 2) {
     RolloutLds2 r;
     r.ldo = L.Dob + 4;
     r.ldh = L.H + 4;
@@ -791,17 +791,20 @@ __host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, i
     r.b2 = ro_take(o, L.Ap);
     r.gb = ro_take(o, 4 * L.H);
     const int rows = rew * N, rows16 = (rows + 15) / 16 * 16;
-    r.obs = ro_take(o, (int64_t)rows * r.ldo);
+    // nhb == 1 (v6): the obs rows double as the compact h' rows between the GRU and fc2 phases
+    const int64_t nobs = (int64_t)rows * r.ldo, nhx = nhb == 1 ? (int64_t)rows16 * r.ldh : 0;
+    r.obs = ro_take(o, nobs > nhx ? nobs : nhx);
     r.avail = ro_take(o, (int64_t)rows * 2);  // uint64 avail mask per agent row
     r.xb = ro_take(o, (int64_t)rows16 * r.ldh);
     r.hsz = mlg_align4((int64_t)rows * r.ldh);
-    r.hb = ro_take(o, 2 * r.hsz);
+    r.nhb = nhb;
+    r.hb = ro_take(o, nhb * r.hsz);
     r.pairtab = ro_take(o, (int64_t)N * U);
     r.avtab = ro_take(o, (int64_t)N * L.A);
     r.pk = ro_take(o, (int64_t)rew * 32);
     r.act = ro_take(o, (int64_t)rew * 32);
     r.am = ro_take(o, 16);
-    r.env = make_env_lds(o, U, N);
+    r.env = make_env_lds(o, U, N, rew < RE ? rew : RE);
     r.total = o;
     return r;
 }
@@ -823,7 +826,7 @@ __device__ void v2_prologue(const MlgEnvSpec& spec, const AgentLayout& L, const 
         for (int i = tid; i < nr * nc; i += nthr) fm[dst + (int64_t)(i / nc) * ld + i % nc] = P[src + i];
     };
     for (int64_t i = tid; i < (int64_t)rows * lay.ldo; i += nthr) fm[lay.obs + i] = 0.f;
-    for (int64_t i = tid; i < 2 * lay.hsz; i += nthr) fm[lay.hb + i] = 0.f;
+    for (int64_t i = tid; i < (int64_t)lay.nhb * lay.hsz; i += nthr) fm[lay.hb + i] = 0.f;
     rows_cp(L.w1o, lay.w1o, H, L.Dob, lay.ldo);
     if (L.last_action) rows_cp(L.w1a, lay.w1a, L.A, H, lay.ldh);
     if (L.agent_id) rows_cp(L.w1n, lay.w1n, N, H, lay.ldh);
@@ -843,7 +846,8 @@ __device__ void v2_prologue(const MlgEnvSpec& spec, const AgentLayout& L, const 
 template <int H>
 struct GruChunk {
     floatx4 wi[3][H / 16], wh[3][H / 16];
-    floatx4 br, bz, bin, bhn;
+    int gbo;  // LDS float index of the chunk's gate biases (r, z, ih_n, hh_n at +0, +H, +2H, +3H): read per
+              // unit instead of held in 16 VGPRs (the step loop is at the 256-VGPR limit)
 };
 
 template <int H>
@@ -859,10 +863,7 @@ __device__ inline void load_gru_chunk(GruChunk<H>& W, const float* __restrict__ 
             W.wi[q][kc] = ld4(P + L.wih + r);
             W.wh[q][kc] = ld4(P + L.whh + r);
         }
-    W.br = ld4(fm + lay.gb + j * 16 + 4 * g);
-    W.bz = ld4(fm + lay.gb + H + j * 16 + 4 * g);
-    W.bin = ld4(fm + lay.gb + 2 * H + j * 16 + 4 * g);
-    W.bhn = ld4(fm + lay.gb + 3 * H + j * 16 + 4 * g);
+    W.gbo = lay.gb + j * 16 + 4 * g;
 }
 
 // Compacted agent rows of one step: the living agents of the running envs ebase .. ebase + ne - 1 (amask[e]
@@ -933,8 +934,9 @@ __device__ inline void ph_fc1(const AgentLayout& L, const RolloutLds2& lay, floa
     }
 }
 
-// B: GRU cell for (tile, chunk j) -> h' (rows of running envs, hidden state indexed by env row)
-template <int H>
+// B: GRU cell for (tile, chunk j) -> h' (rows of running envs, hidden state indexed by env row). CX: h' goes to
+// a compact-row buffer instead (row cr of the tile list; v6), copied back to the env rows by phase C.
+template <int H, bool CX = false>
 __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, float* fm, const float* hc, float* hn,
                               const StepRows& SR, int N_, int j, int ti0, int dt, int lane) {
     constexpr int HC = H / 16;
@@ -946,7 +948,8 @@ __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, floa
         const int er = e * N + n;
         const float* xr = fm + lay.xb + (int64_t)cr * ldh + 4 * g;
         const float* hr = hc + (int64_t)er * ldh + 4 * g;
-        floatx4 ar = W.br, az = W.bz, ain = W.bin, ahn = W.bhn;
+        const float* gbp = fm + W.gbo;
+        floatx4 ar = ld4(gbp), az = ld4(gbp + H), ain = ld4(gbp + 2 * H), ahn = ld4(gbp + 3 * H);
 #pragma unroll
         for (int kc = 0; kc < HC; ++kc) {
             const floatx4 xin = ld4(xr + kc * 16), hin = ld4(hr + kc * 16);
@@ -966,15 +969,19 @@ __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, floa
             const float ng = tanhf(ain[r] + rg * ahn[r]);
             hv[r] = ng + zg * (ho[r] - ng);
         }
-        if (valid) *reinterpret_cast<floatx4*>(hn + (int64_t)er * ldh + j * 16 + 4 * g) = hv;
+        if (CX)
+            *reinterpret_cast<floatx4*>(hn + (int64_t)cr * ldh + j * 16 + 4 * g) = hv;
+        else if (valid)
+            *reinterpret_cast<floatx4*>(hn + (int64_t)er * ldh + j * 16 + 4 * g) = hv;
     }
 }
 
-// C: fc2 + masked argmax + epsilon-greedy per tile; records the actions (batch + LDS pending actions)
-template <int H>
+// C: fc2 + masked argmax + epsilon-greedy per tile; records the actions (batch + LDS pending actions).
+// CX: h' is read from the compact-row buffer hn and the tile's valid rows are stored to the env rows of hstore.
+template <int H, bool CX = false>
 __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, const RolloutLds2& lay, float* fm,
                               const RoEnv& R, const MlgBatch& bt, const float* hn, const StepRows& SR, int ti0, int dt,
-                              int e0, int t, float eps, int test_mode, int lane) {
+                              int e0, int t, float eps, int test_mode, int lane, float* hstore = nullptr) {
     constexpr int HC = H / 16;
     const int col = lane & 15, g = lane >> 4, N = L.N, ldh = lay.ldh, A = spec.n_actions, n_at = L.Ap / 16;
     const uint64_t* lavm = reinterpret_cast<const uint64_t*>(fm + lay.avail);
@@ -985,7 +992,12 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
         int e, n;
         const bool valid = SR.at(cr, e, n);
         const int er = e * N + n;
-        const float* hr = hn + (int64_t)er * ldh + 4 * g;
+        const float* hr = hn + (int64_t)(CX ? cr : er) * ldh + 4 * g;
+        if (CX && valid) {
+#pragma unroll
+            for (int kc = 0; kc < HC; ++kc)
+                *reinterpret_cast<floatx4*>(hstore + (int64_t)er * ldh + 4 * g + kc * 16) = ld4(hr + kc * 16);
+        }
         const uint64_t avm = lavm[er];
         ArgmaxState as{-INFINITY, 1 << 30};
         for (int at = 0; at < n_at; ++at) {
@@ -1329,6 +1341,56 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
 }
 
 // ================================================================================================
+// v6 kernel: v2 at half the size -- 4 waves, 8 envs -- so that two workgroups share a CU (LDS < 80 KB, 256
+// VGPRs per wave at one wave per SIMD per workgroup). The two workgroups' barriers are independent, so one
+// workgroup's env step (VALU / LDS latency) runs while the other's agent phases keep the matrix cores busy,
+// and a workgroup only runs as long as the longest of its 8 episodes. LDS is cut by holding the hidden
+// state once: the GRU writes h' to compact rows aliasing the obs buffer (dead between fc1 and the env
+// step), fc2 reads them there and stores the valid rows back to the env-row hidden state.
+// Barriers per step: A|B, B|C, C|env, env|A. Arithmetic identical to v2 (bit-identical batches).
+template <int H>
+__global__ void __launch_bounds__(256, 2) rollout_v6_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
+                                                           const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
+                                                           float eps, int test_mode, RolloutLds2 lay) {
+    constexpr int HC = H / 16, NW = 4, REW = 8, G = NW / HC;
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    float* fm = reinterpret_cast<float*>(smem);
+    const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
+    const int e0 = blockIdx.x * REW, T1 = bt.T1;
+    v2_prologue(spec, L, P, lay, smem, REW * N);
+    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info);
+    EnvLane E;
+    env_lane_reset(C, st, E, wave * 2 + (lane >> 5), e0, hl);
+    const int j = wave % HC, gi = wave / HC;
+    GruChunk<H> W;
+    load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
+    __syncthreads();
+    Stamps sp;
+    sp.init();
+    uint64_t rows_issued = 0;
+    float* h = fm + lay.hb;
+    float* hx = fm + lay.obs;
+    for (int t = 0; t < T1; ++t) {
+        const uint32_t run = (uint32_t)__ballot(lane < REW && C.R.status[lane & (REW - 1)] < 2);
+        if (run == 0) break;
+        const StepRows SR = make_rows(C.amask, 0, REW, lane);
+        rows_issued += SR.tiles * 16;
+        ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
+        __syncthreads();
+        ph_gru<H, true>(W, lay, fm, h, hx, SR, N, j, gi, G, lane);
+        __syncthreads();
+        ph_fc2<H, true>(spec, L, lay, fm, C.R, bt, hx, SR, wave, NW, e0, t, eps, test_mode, lane, h);
+        __syncthreads();
+        env_lane_step1(C, E, t, hl);
+        env_lane_step2(C, E, t, hl, sp);
+        if (!E.stepped && (t & 1)) env_lane_tail(C, E, 8, hl);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && info.agent_rows) atomicAdd(info.agent_rows, (unsigned long long)rows_issued);
+    env_lane_finish(C, st, E, hl);
+}
+
+// ================================================================================================
 // v4 kernel: wave-specialised, two env groups in flight. Waves 0..AW-1 are agent waves (wave w owns GRU chunk
 // w % HC of tiles w / HC, w / HC + AW / HC, ... with its weights in VGPRs), the last 4 waves are env waves (half-wave per env: envs 0-7 form group 0,
 // 8-15 group 1; env wave v steps envs 2v, 2v + 1 of both groups). Phase p runs the agent step of group
@@ -1593,14 +1655,17 @@ int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& 
                       const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
                       const RolloutLds2& lay) {
     const size_t bytes = (size_t)lay.total * 4;
-    auto kern = V == 4 ? rollout_v4_kernel<H, 4> : (V == 5 ? rollout_v4_kernel<H, 8> : rollout_v2_kernel<H>);
-    const int threads = V == 4 ? 512 : (V == 5 ? 768 : 512);
+    auto kern = V == 4 ? rollout_v4_kernel<H, 4>
+                       : (V == 5 ? rollout_v4_kernel<H, 8> : (V == 6 ? rollout_v6_kernel<H> : rollout_v2_kernel<H>));
+    const int threads = V == 4 ? 512 : (V == 5 ? 768 : (V == 6 ? 256 : 512));
+    const int rew = V == 6 ? 8 : 16;
     if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)bytes);
         if (e != hipSuccess) return mlg::fail("rollout v2: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
     }
-    hipLaunchKernelGGL(kern, dim3((bt.B + 15) / 16), dim3(threads), bytes, s, spec, st, L, P, bt, info, eps, tm, lay);
+    hipLaunchKernelGGL(kern, dim3((bt.B + rew - 1) / rew), dim3(threads), bytes, s, spec, st, L, P, bt, info, eps, tm,
+                       lay);
     return 0;
 }
 
@@ -1610,6 +1675,10 @@ int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay)
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
     const int want = (k && k[0] == 'v') ? k[1] - '0' : 2;
     if (want == 1 || (L.H != 64 && L.H != 32) || spec.U > 32) return 1;
+    if (want == 6) {  // two workgroups per CU need the layout to fit half the LDS
+        *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 8, 1);
+        if (lay->total * 4 <= LDS_LIMIT_BYTES / 2) return 6;
+    }
     *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
     if (lay->total * 4 > LDS_LIMIT_BYTES) return 1;
     return (want == 4 || want == 5) ? want : 2;
@@ -1787,6 +1856,7 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
                            : launch_rollout_v2<32, VV>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
         if (variant == 4) MLG_V(4);
         else if (variant == 5) MLG_V(5);
+        else if (variant == 6) MLG_V(6);
         else MLG_V(2);
 #undef MLG_V
         if (rc) return rc;
