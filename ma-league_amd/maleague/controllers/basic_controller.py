@@ -14,6 +14,7 @@ from ..components.action_selectors import REGISTRY as action_REGISTRY
 from ..components.batch_view import mlg_batch
 from ..exceptions import HiddenStateNotInitialized
 from ..modules.agents import REGISTRY as agent_REGISTRY
+from ..utils.checkpoint import save_module
 
 
 class MultiAgentController:
@@ -80,7 +81,7 @@ class BasicMAC(MultiAgentController):
         self.agent.cuda()
 
     def save_models(self, path, name):
-        torch.save(self.agent.state_dict(), f"{path}/{name}agent.th")
+        save_module(self.agent, f"{path}/{name}agent.th")
 
     def load_models(self, path, name):
         self.agent.load_state_dict(torch.load(f"{path}/{name}agent.th", map_location=lambda s, loc: s,

@@ -15,6 +15,7 @@ import torch
 from .. import _native
 from ..components.batch_view import mlg_batch
 from ..modules.mixers import QMixer, VDNMixer
+from ..utils.checkpoint import save_module, save_optimizer
 
 AGENT_ORDER = ["fc1.weight", "fc1.bias", "gru.weight_ih", "gru.weight_hh", "gru.bias_ih", "gru.bias_hh",
                "fc2.weight", "fc2.bias"]
@@ -188,8 +189,8 @@ class QLearner(Learner):
     def save_models(self, path, name):
         self.mac.save_models(path, name=self.name)
         if self.mixer is not None:
-            torch.save(self.mixer.state_dict(), f"{path}/{self.name}mixer.th")
-        torch.save(self.optimiser.state_dict(), f"{path}/{self.name}opt.th")
+            save_module(self.mixer, f"{path}/{self.name}mixer.th")
+        save_optimizer(self.optimiser, f"{path}/{self.name}opt.th")
 
     def load_models(self, path):
         self.mac.load_models(path, self.name)
@@ -203,6 +204,8 @@ class QLearner(Learner):
             st = self.optimiser.state.get(p, {})
             if "square_avg" in st:
                 self._sq[off:off + k].copy_(st["square_avg"].reshape(-1))
+            if "step" in st:  # one shared step counter (RMSprop steps every parameter together)
+                self._step.fill_(float(st["step"]))
             self.optimiser.state[p] = {"step": self._step, "square_avg": self._sq[off:off + k].view_as(p)}
         self.mac.agent.mark_dirty()
         self.target_mac.agent.mark_dirty()

@@ -15,6 +15,7 @@ import torch
 from .. import _native
 from ..components.batch_view import mlg_entity_batch
 from ..modules.mixers import FlexQMixer
+from ..utils.checkpoint import save_module, save_optimizer
 from .q_learner import FlatParams, Learner
 
 AGENT_ORDER = ["fc1.weight", "fc1.bias", "attn.in_trans.weight", "attn.out_trans.weight", "attn.out_trans.bias",
@@ -152,8 +153,8 @@ class REFILLearner(Learner):
     def save_models(self, path, name=None):
         name = self.name if name is None else name
         self.mac.save_models(path, name=name)
-        torch.save(self.mixer.state_dict(), f"{path}/{name}mixer.th")
-        torch.save(self.optimiser.state_dict(), f"{path}/{name}opt.th")
+        save_module(self.mixer, f"{path}/{name}mixer.th")
+        save_optimizer(self.optimiser, f"{path}/{name}opt.th")
 
     def load_models(self, path):
         self.mac.load_models(path, self.name)
@@ -167,6 +168,8 @@ class REFILLearner(Learner):
             st = self.optimiser.state.get(p, {})
             if "square_avg" in st:
                 self._sq[off:off + k].copy_(st["square_avg"].reshape(-1))
+            if "step" in st:
+                self._step.fill_(float(st["step"]))
             self.optimiser.state[p] = {"step": self._step, "square_avg": self._sq[off:off + k].view_as(p)}
         self.mac.agent.mark_dirty()
         self.target_mac.agent.mark_dirty()

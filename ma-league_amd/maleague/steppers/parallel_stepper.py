@@ -182,11 +182,13 @@ class ParallelStepper(EnvStepper):
         if not test_mode:
             self.env_steps_this_run = int(ep_len.sum())
             self._t_env += self.env_steps_this_run
-        self._post.append((run_id, host, self._t, self._t_env))
+        self._post.append((run_id, host, self._t, self._t_env, test_mode))
 
     def _finish_post(self):
         B = self.batch_size
-        for run_id, host, t_max, t_env in self._post:
+        mode_now = self.logger.test_mode
+        for run_id, host, t_max, t_env, test_mode in self._post:
+            self.logger.test_mode = test_mode  # the run's mode (its summary may resolve after a later run())
             ep_len = host[0:B]
             won = host[B:3 * B].reshape(B, 2).astype(bool)
             draw = host[3 * B:4 * B].astype(bool)
@@ -209,6 +211,7 @@ class ParallelStepper(EnvStepper):
             self.logger.collect(Collectibles.DRAW, draw[order], parallel=True)
             self.logger.collect(Collectibles.STEPS, t_max, parallel=True)
             self.logger.log(t_env)
+        self.logger.test_mode = mode_now
         self._post = []
 
     def _env_infos_of(self, run_id):

@@ -19,6 +19,10 @@ Fixtures (all float32/int64 arrays; dict keys documented per function below):
                        (fake env with scripted termination; probe shims listed in _stepper_fixture)
   pfsp.npz             PayoffWrapper.win_rates + PFSPSampling weightings
                        src/league/components/payoff_entry.py:23-30, src/league/components/self_play.py:49-65
+  checkpoint.npz       QLearner.save_models/load_models resume  src/marl/learners/q_learner.py:133-147
+  logger.npz           MainLogger collect/log aggregation  src/custom_logging/logger.py:24-173
+  ckpt_qmix/100/*.th   the reference's own checkpoint files (torch.save of state dicts; tests load them
+                       with weights_only=True)
 """
 import collections
 import collections.abc
@@ -451,6 +455,101 @@ def pfsp_fixture():
     np.savez_compressed(os.path.join(OUT, "pfsp.npz"), **out)
 
 
+def checkpoint_fixture():
+    """Checkpoint interop (q_learner.py:133-147, basic_controller.py:68-72, run_utils.py:20-37).
+
+    A reference QLearner (qmix, double-Q; the qlearner_qmix_dq setup) trains once and writes its checkpoint
+    as ckpt_qmix/100/home_qlearner_{agent,mixer,opt}.th (the layout models/{token}/{t_env}/ the experiment
+    saves). A FRESH reference learner (seed 99) then resumes from it (load_models) and trains once more.
+    checkpoint.npz: the batch (b.*), the resumed learner's untouched target mixer (tm.*: load_models does
+    not load it), the stats of the resumed call (stat.*) and all parameters after it (p2.*)."""
+    import shutil
+    th.manual_seed(7)
+    args = base_args()
+    B, T, N, d_obs, A, S = 4, 7, 5, 80, 15, 60
+    batch, scheme, groups, preprocess = make_batch(B, T, N, d_obs, A, S, [6, 3, 4, 2], seed=8)
+    mac = BasicMAC(batch.scheme, groups, args)
+    learner = QLearner(mac, batch.scheme, StatLogger(), args, name="home")
+    learner.build_optimizer()
+    learner.train(batch, 100, 0)
+    ck = os.path.join(OUT, "ckpt_qmix")
+    shutil.rmtree(ck, ignore_errors=True)
+    os.makedirs(os.path.join(ck, "100"))
+    learner.save_models(os.path.join(ck, "100"), "home")
+
+    th.manual_seed(99)
+    mac2 = BasicMAC(batch.scheme, groups, args)
+    logger2 = StatLogger()
+    learner2 = QLearner(mac2, batch.scheme, logger2, args, name="home")
+    learner2.build_optimizer()
+    out = {}
+    out.update(sd_to_np("tm.", learner2.target_mixer.state_dict()))
+    learner2.load_models(os.path.join(ck, "100"))
+    out.update(batch_to_np("b.", batch))
+    learner2.train(batch, 200, 32)
+    stats = {k.replace("home_qlearner_", ""): v for k, v, _ in logger2.stats}
+    for k in ["loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]:
+        out[f"stat.{k}"] = np.array(stats[k], dtype=np.float64)
+    out.update(sd_to_np("p2.agent.", mac2.agent.state_dict()))
+    out.update(sd_to_np("p2.target_agent.", learner2.target_mac.agent.state_dict()))
+    out.update(sd_to_np("p2.mixer.", learner2.mixer.state_dict()))
+    np.savez_compressed(os.path.join(OUT, "checkpoint.npz"), **out)
+
+
+def logger_fixture():
+    """MainLogger collect/log/preprocess (custom_logging/logger.py:24-173, collectibles.py:10-68).
+
+    Probe shims (this generator only): collections.Sized aliased (logger.py:3); custom_logging.platforms
+    stubbed with inert classes (its tensorboard/sacred sinks need packages absent here) -- only the
+    aggregation logic runs. Records a scripted sequence of collect()/log() calls (train interval, test
+    completion) and the resulting stats: logger.npz keys `k{i}` (stat name), `t{i}`, `v{i}` (float64, NaN kept)."""
+    collections.Sized = collections.abc.Sized
+    plat = types.ModuleType("custom_logging.platforms")
+    plat.CustomSacredLogger = plat.CustomTensorboardLogger = type("Inert", (), {})
+    console = types.ModuleType("custom_logging.platforms.console")
+    console.CustomConsoleLogger = type("InertConsole", (), {"info": lambda self, *a: None})
+    sys.modules["custom_logging.platforms"] = plat
+    sys.modules["custom_logging.platforms.console"] = console
+    from custom_logging.logger import MainLogger
+    from custom_logging.collectibles import Collectibles
+    from custom_logging.utils.enums import Originator
+    lg = MainLogger(console.CustomConsoleLogger(), SimpleNamespace(test_nepisode=4, runner_log_interval=100))
+
+    def run(rets, won_h, won_a, draw, steps):
+        lg.collect(Collectibles.RETURN, rets, origin=Originator.HOME, parallel=True)
+        lg.collect(Collectibles.WON, won_h, origin=Originator.HOME, parallel=True)
+        lg.collect(Collectibles.WON, won_a, origin=Originator.AWAY, parallel=True)
+        lg.collect(Collectibles.DRAW, draw, parallel=True)
+        lg.collect(Collectibles.STEPS, steps, parallel=True)  # an int with parallel=True: dropped (logger.py:135)
+
+    run([1.5, 2.0, -1.0], [True, False, True], [False, True, False], [False, False, False], 37)
+    lg.log(0)                       # first train log (log_train_stats_t starts at -1e6)
+    run([0.25], [False], [False], [True], 12)
+    lg.log(50)                      # inside the interval: nothing
+    run([3.0, 4.5], [True, True], [False, False], [False, False], 20)
+    lg.log(150)                     # logs both runs' data
+    lg.collect(Collectibles.RETURN, 7.0, origin=Originator.HOME)  # non-parallel scalar append
+    lg.collect(Collectibles.WON, True, origin=Originator.HOME)
+    lg.collect(Collectibles.DRAW, False)
+    lg.log(200)                     # interval not reached
+    lg.test_mode = True
+    run([1.0, 2.0], [True, False], [False, False], [False, True], 9)
+    lg.log(260)                     # test not finished (2 of 4)
+    run([5.0, 6.0], [False, False], [True, False], [False, False], 9)
+    lg.log(260)                     # test finished: test_* stats
+    lg.test_mode = False
+    lg.log(270)                     # 120 since the last train log: logs the scalar collects above
+    lg.log(351)                     # inside the interval again: nothing
+    out, i = {}, 0
+    for k in sorted(lg.stats):
+        for t, v in lg.stats[k]:
+            out[f"k{i}"], out[f"t{i}"] = np.array(k), np.array(t, dtype=np.int64)
+            out[f"v{i}"] = np.array(np.nan if v is None else v, dtype=np.float64)
+            i += 1
+    out["n"] = np.array(i, dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, "logger.npz"), **out)
+
+
 def _all():
     drqn_fixture()
     mac_fixture()
@@ -464,7 +563,15 @@ def _all():
 
 
 if __name__ == "__main__":
+    if "--checkpoint-only" in sys.argv:
+        checkpoint_fixture()
+        sys.exit(0)
+    if "--logger-only" in sys.argv:
+        logger_fixture()
+        sys.exit(0)
     if "--stepper-only" not in sys.argv:
         _all()
+        checkpoint_fixture()
+        logger_fixture()
     _stepper_fixture()
     print("golden fixtures written to", OUT)
