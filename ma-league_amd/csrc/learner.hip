@@ -327,17 +327,15 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
     if (valid) *reinterpret_cast<floatx4*>(hsg + (int64_t)r * H + f0) = floatx4{0.f, 0.f, 0.f, 0.f};  // HS[0]
     const int rr = valid ? r : 0;
     auto gi_at = [&](int t, int q) { return ld4(gi + ((int64_t)t * R + rr) * 3 * H + q * H + f0); };
-    floatx4 nr = gi_at(0, 0), nz = gi_at(0, 1), nn = gi_at(0, 2);
-    __syncthreads();
-    int cur = 0;
-    for (int t = 0; t < Te; ++t) {
-        floatx4 ar = nr, az = nz;
-        const floatx4 gin = nn;
-        if (t + 1 < Te) {  // prefetch the next step's input gates
-            nr = gi_at(t + 1, 0);
-            nz = gi_at(t + 1, 1);
-            nn = gi_at(t + 1, 2);
-        }
+    // input gates prefetched a step ahead into ping-pong registers: the 2x-unrolled loop consumes them in place,
+    // so the wait for the prefetch never covers this step's stores (a register copy would force vmcnt(0))
+    const __amdgpu_buffer_rsrc_t rs_h = mlg_rsrc(hsg), rs_r = mlg_rsrc(ws_gr), rs_z = mlg_rsrc(ws_gz),
+                                 rs_n = mlg_rsrc(ws_gn), rs_hn = mlg_rsrc(ws_ghn);
+    auto step = [&](int t, const floatx4 (&gc)[3], floatx4 (&gn)[3], int cur) {
+        const int tn = t + 1 < Te ? t + 1 : t;  // unconditional (clamped) prefetch: no branch in the VMEM stream
+#pragma unroll
+        for (int q = 0; q < 3; ++q) gn[q] = gi_at(tn, q);
+        floatx4 ar = gc[0], az = gc[1];
         floatx4 ahn = bhn;
         const float* hrow = hs[cur] + col * LDA + 4 * g;
 #pragma unroll
@@ -353,22 +351,28 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
         for (int q = 0; q < 4; ++q) {
             rg[q] = sigm(ar[q]);
             zg[q] = sigm(az[q]);
-            ng[q] = tanhf(gin[q] + rg[q] * ahn[q]);
+            ng[q] = tanhf(gc[2][q] + rg[q] * ahn[q]);
             hn[q] = ng[q] + zg[q] * (hp[q] - ng[q]);
         }
         *reinterpret_cast<floatx4*>(hs[cur ^ 1] + col * LDA + f0) = hn;
-        if (valid) {
-            const int64_t o = ((int64_t)t * R + r) * H + f0;
-            *reinterpret_cast<floatx4*>(hsg + o + (int64_t)R * H) = hn;  // HS[t + 1]
-            if (online) {
-                *reinterpret_cast<floatx4*>(ws_gr + o) = rg;
-                *reinterpret_cast<floatx4*>(ws_gz + o) = zg;
-                *reinterpret_cast<floatx4*>(ws_gn + o) = ng;
-                *reinterpret_cast<floatx4*>(ws_ghn + o) = ahn;
-            }
-        }
+        const int64_t o = ((int64_t)t * R + r) * H + f0;
+        st4_if(rs_h, o + (int64_t)R * H, hn, valid);  // HS[t + 1]
+        st4_if(rs_r, o, rg, valid && online);          // gates are saved by the online net only
+        st4_if(rs_z, o, zg, valid && online);
+        st4_if(rs_n, o, ng, valid && online);
+        st4_if(rs_hn, o, ahn, valid && online);
         __syncthreads();
-        cur ^= 1;
+    };
+    floatx4 ga[3], gb[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) ga[q] = gi_at(0, q);
+    __syncthreads();
+    // step 0 peeled: the loop is entered in the same VMEM state as its back edge (prefetch loads, then the
+    // stores), so the compiler's merged waitcnt for the prefetched gates still lets the stores drain
+    step(0, ga, gb, 0);
+    for (int t = 1; t < Te; t += 2) {
+        step(t, gb, ga, 1);
+        if (t + 1 < Te) step(t + 1, ga, gb, 0);
     }
 }
 
@@ -688,6 +692,7 @@ __global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs
 // reverse-time GRU backward; wave w owns hidden chunk w. W_hh^T rows of the chunk live in VGPRs, the
 // step's gate values are prefetched one step ahead, dGH is exchanged through LDS (double buffered).
 // dh_{t-1} = dh * z + W_hh^T dGH.  dX = W_ih^T dGI does not feed the recurrence: agent_dx_kernel.
+constexpr int MLG_BWD_MAXA = 96;  // fc2 rows staged in LDS by agent_bwd_kernel (host-checked)
 template <int H>
 __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ P,
                                                         const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
@@ -698,6 +703,7 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
     constexpr int LDG = 3 * H + 4;
     constexpr int KC = 3 * H / 16;
     __shared__ __attribute__((aligned(16))) float sgh[2][16 * LDG];
+    __shared__ __attribute__((aligned(16))) float w2s[MLG_BWD_MAXA * H];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int col = lane & 15, g = lane >> 4;
     const int r = blockIdx.x * 16 + col;
@@ -712,26 +718,23 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
 #pragma unroll
         for (int q = 0; q < 4; ++q) wt[kc][q] = P[L.whh + (int64_t)(kc * 16 + 4 * g + q) * H + w * 16 + col];
     const int rr = valid ? r : 0;
+    for (int i = tid; i < c.A * H; i += blockDim.x) w2s[i] = P[L.w2 + i];  // fc2 rows for dh += dq W2[a]
+    const int64_t abase = bslot(bt, b) * bt.T1 * N + n;  // loop-invariant: no dependent slot-map load per step
     struct Step {
-        floatx4 rg, zg, ng, ghn, hp, w2;
+        floatx4 rg, zg, ng, ghn, hp;
         float dq;
+        int a;
     };
-    auto load_step = [&](int t) {
-        Step s;
+    auto load_step = [&](int t, Step& s) {
         const int64_t o = ((int64_t)t * R + rr) * H + f0;
         s.rg = ld4(ws_gr + o);
         s.zg = ld4(ws_gz + o);
         s.ng = ld4(ws_gn + o);
         s.ghn = ld4(ws_ghn + o);
         s.hp = ld4(ws_hs + o);  // HS[t] = h_{t-1}
-        s.dq = 0.f;
-        s.w2 = floatx4{0.f, 0.f, 0.f, 0.f};
-        if (t < c.T - 1) {
-            s.dq = dqv[(int64_t)t * R + rr];
-            const int a = (int)bt.actions[(bslot(bt, b) * bt.T1 + t) * N + n];
-            s.w2 = ld4(P + L.w2 + (int64_t)a * H + f0);
-        }
-        return s;
+        const int tq = t < c.T - 1 ? t : c.T - 2;  // unconditional (clamped) loads; dq / action unused at T-1
+        s.dq = dqv[(int64_t)tq * R + rr];
+        s.a = t < c.T - 1 ? (int)bt.actions[abase + (int64_t)tq * N] : -1;
     };
     const int Te = t_eff(msum);
     if (valid) {  // steps past max_t_filled: zero deltas (wgrad rows)
@@ -745,12 +748,12 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
         }
     }
     floatx4 dh = {0.f, 0.f, 0.f, 0.f};
-    Step nx = load_step(Te - 1);
-    int cur = 0;
-    for (int t = Te - 1; t >= 0; --t) {
-        const Step s = nx;
-        if (t > 0) nx = load_step(t - 1);
-        if (valid && t < c.T - 1) dh += s.dq * s.w2;
+    // a step's saved gates are prefetched one step ahead into ping-pong registers (2x-unrolled loop, no copies:
+    // the wait for them never covers the previous step's stores); W2 rows come from LDS, not a dependent load
+    const __amdgpu_buffer_rsrc_t rs_gi = mlg_rsrc(dgi), rs_gh = mlg_rsrc(dgh);
+    auto step = [&](int t, const Step& s, Step& nx, int cur) {
+        load_step(t > 0 ? t - 1 : 0, nx);
+        if (valid && s.a >= 0) dh += s.dq * ld4(w2s + s.a * H + f0);
         floatx4 drp, dzp, dnp, dghn, dhd;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -767,22 +770,26 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
         *reinterpret_cast<floatx4*>(gh + f0) = drp;
         *reinterpret_cast<floatx4*>(gh + H + f0) = dzp;
         *reinterpret_cast<floatx4*>(gh + 2 * H + f0) = dghn;
-        if (valid) {
-            const int64_t o3 = ((int64_t)t * R + r) * 3 * H + f0;
-            *reinterpret_cast<floatx4*>(dgi + o3) = drp;
-            *reinterpret_cast<floatx4*>(dgi + o3 + H) = dzp;
-            *reinterpret_cast<floatx4*>(dgi + o3 + 2 * H) = dnp;
-            *reinterpret_cast<floatx4*>(dgh + o3) = drp;
-            *reinterpret_cast<floatx4*>(dgh + o3 + H) = dzp;
-            *reinterpret_cast<floatx4*>(dgh + o3 + 2 * H) = dghn;
-        }
+        const int64_t o3 = ((int64_t)t * R + r) * 3 * H + f0;
+        st4_if(rs_gi, o3, drp, valid);
+        st4_if(rs_gi, o3 + H, dzp, valid);
+        st4_if(rs_gi, o3 + 2 * H, dnp, valid);
+        st4_if(rs_gh, o3, drp, valid);
+        st4_if(rs_gh, o3 + H, dzp, valid);
+        st4_if(rs_gh, o3 + 2 * H, dghn, valid);
         __syncthreads();
         floatx4 dprev = dhd;
         const float* ghr = sgh[cur] + col * LDG + 4 * g;
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) dprev = mfma_chunk(wt[kc], ld4(ghr + kc * 16), dprev);
         dh = dprev;
-        cur ^= 1;
+    };
+    Step sa, sb;
+    load_step(Te - 1, sa);
+    step(Te - 1, sa, sb, 0);  // peeled (see agent_rec_kernel)
+    for (int t = Te - 2; t >= 0; t -= 2) {
+        step(t, sb, sa, 1);
+        if (t > 0) step(t - 1, sa, sb, 0);
     }
 }
 
@@ -877,6 +884,10 @@ int check_cfg(const MlgLearnerCfg* c) {
     MLG_REQUIRE(c->H == 32 || c->H == 64 || c->H == 128, "rnn_hidden_dim=%d unsupported (32/64/128)", c->H);
     MLG_REQUIRE(c->B >= 1 && c->T >= 2 && c->N >= 1 && c->N <= MAXN && c->A >= 1, "learner: bad sizes B=%d T=%d N=%d",
                 c->B, c->T, c->N);
+    MLG_REQUIRE(c->A <= MLG_BWD_MAXA, "learner: n_actions=%d > %d unsupported", c->A, MLG_BWD_MAXA);
+    MLG_REQUIRE((int64_t)c->T * c->B * c->N * 3 * c->H < (int64_t)1 << 29,
+                "learner: T*B*N*3H=%lld floats exceeds the 2 GB buffer-store range",
+                (long long)c->T * c->B * c->N * 3 * c->H);
     MLG_REQUIRE(c->mixer == 1 || c->mixer == 2, "learner: mixer must be vdn or qmix (IQL is not built)");
     if (c->mixer == 2) {
         MLG_REQUIRE(c->hypernet_layers == 2, "learner: qmix hypernet_layers=%d unsupported (2)", c->hypernet_layers);

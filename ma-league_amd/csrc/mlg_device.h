@@ -27,6 +27,19 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 
+// Branch-free predicated stores through a raw buffer resource: a dropped lane gets an out-of-range offset and
+// the hardware range check discards it. Inside sequential loops this keeps the VMEM stream straight-line, so
+// the compiler's waitcnt for a prefetched load counts the stores issued after it (an `if (valid)` store would
+// make it wait for every outstanding store instead). Element offsets must stay below 2^29 floats (host-checked).
+typedef unsigned int mlg_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mlg_rsrc(const float* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st4_if(__amdgpu_buffer_rsrc_t rs, int64_t off, floatx4 v, bool keep) {
+    const int byte = keep ? (int)(off * 4) : (int)0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(mlg_u32x4, v), rs, byte, 0, 0);
+}
+
 __device__ __forceinline__ floatx4 mfma_chunk(const floatx4 w, const floatx4 x, floatx4 acc) {
     acc = mfma4(w.x, x.x, acc);
     acc = mfma4(w.y, x.y, acc);
