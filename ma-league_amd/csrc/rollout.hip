@@ -560,24 +560,29 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
 __device__ inline void zero_slot_steps(const MlgBatch& bt, int slot, int z0, int z1, int N, int A, int S, int DO,
                                        int lane, int nl) {
     if (z0 >= z1) return;
-    const int64_t r0 = (int64_t)slot * bt.T1 + z0, n = z1 - z0;
+    const int64_t r0 = (int64_t)slot * bt.T1 + z0;
+    const int n = z1 - z0;  // 32-bit loop counters: fewer live VGPRs than int64 induction variables
     // obs and state rows are whole 16-byte multiples (8U and 6U floats, U even) when DO % 4 == 0 and S % 4 == 0
-    auto z16 = [&](float* p, int64_t per) {
+    auto z16 = [&](float* p, int per) {
+        float* b = p + r0 * per;
         if (per % 4 == 0) {
-            uint4* q = reinterpret_cast<uint4*>(p + r0 * per);
-            for (int64_t x = lane; x < n * per / 4; x += nl) q[x] = make_uint4(0u, 0u, 0u, 0u);
+            uint4* q = reinterpret_cast<uint4*>(b);
+            for (int x = lane; x < n * per / 4; x += nl) q[x] = make_uint4(0u, 0u, 0u, 0u);
         } else {
-            for (int64_t x = lane; x < n * per; x += nl) p[r0 * per + x] = 0.f;
+            for (int x = lane; x < n * per; x += nl) b[x] = 0.f;
         }
     };
-    z16(bt.obs, (int64_t)N * DO);
+    z16(bt.obs, N * DO);
     z16(bt.state, S);
-    for (int64_t x = lane; x < n * N * A; x += nl) {
-        bt.avail[r0 * N * A + x] = 0;
-        bt.actions_onehot[r0 * N * A + x] = 0.f;
+    int* av = bt.avail + r0 * N * A;
+    float* oh = bt.actions_onehot + r0 * N * A;
+    for (int x = lane; x < n * N * A; x += nl) {
+        av[x] = 0;
+        oh[x] = 0.f;
     }
-    for (int64_t x = lane; x < n * N; x += nl) bt.actions[r0 * N + x] = 0;
-    for (int64_t x = lane; x < n; x += nl) {
+    auto* ac = bt.actions + r0 * N;
+    for (int x = lane; x < n * N; x += nl) ac[x] = 0;
+    for (int x = lane; x < n; x += nl) {
         bt.reward[r0 + x] = 0.f;
         bt.terminated[r0 + x] = 0;
         bt.filled[r0 + x] = 0;
@@ -740,6 +745,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
         const int ag = hl < U ? SS.agent[hl] : 0;
         if (ag) lavm[e * N + ag - 1] = m;
     }
+#pragma unroll 1  // rolled: see the one-hot loop in env_lane_step1
     for (int k0 = 0; k0 < N * A; k0 += 32) {
         const int k = k0 + hl;
         if (k < N * A) {
@@ -864,6 +870,14 @@ __device__ inline void load_gru_chunk(GruChunk<H>& W, const float* __restrict__ 
             W.wh[q][kc] = ld4(P + L.whh + r);
         }
     W.gbo = lay.gb + j * 16 + 4 * g;
+    // Consume the loaded registers here, before the episode loop: the empty asm "reads" them, so the compiler's
+    // waitcnt for these loads lands outside the loop. Otherwise its loop-header merge keeps them pending and
+    // re-issues vmcnt waits at their first use inside the loop on every step -- which, vmcnt being in order,
+    // also waits for the previous step's batch stores.
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int kc = 0; kc < HC; ++kc) asm volatile("" : "+v"(W.wi[q][kc]), "+v"(W.wh[q][kc]));
 }
 
 // Compacted agent rows of one step: the living agents of the running envs ebase .. ebase + ne - 1 (amask[e]
@@ -1125,6 +1139,9 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     if (hl < N) C.R.prev[E.e * N + hl] = pact[hl];
     if (C.bt.full_write) {  // whole one-hot rows of the recorded actions
         const int64_t oh = ((int64_t)E.slot * T1 + t) * N * A;
+        // rolled: the unrolled copy's rounded trip count was the v2 kernel's last VGPR spill, and its in-loop
+        // scratch reload (vmcnt being in order) waited for every store of the step issued so far
+#pragma unroll 1
         for (int k = hl; k < N * A; k += 32) {
             const int pt = C.avtab[k];
             C.bt.actions_onehot[oh + k] = (pt & 255) == pact[pt >> 8] ? 1.0f : 0.0f;
