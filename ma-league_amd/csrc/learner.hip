@@ -376,6 +376,115 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
     }
 }
 
+// The recurrence on 4-row tiles with v_mfma_f32_4x4x1_16b_f32 (16 blocks of D[4x4] += A[4x1] B[1x4]; lane
+// 4b + i supplies A_b[i], lane 4b + j supplies B_b[j], D_b[i][j] is register i of lane 4b + j). A 16-row tile
+// per CU is MFMA-bound at 48 16x16x4 MFMAs per SIMD per step; 4-row tiles put 4x as many CUs on the
+// sequential T loop. Wave w owns hidden features 16w..16w+15: block b = 4g + fg computes gate g (r, z, W_hn h;
+// g = 3 idle) of features 16w + 4fg + i for the tile's 4 rows, W_hh rows of the block in VGPRs (H per lane).
+// Lanes 0..15 then gather z and W_hn h from lanes +16 / +32 and finish the GRU cell for (feature, row).
+// grid (2 * ntiles4): blockIdx < ntiles4 online (saves gates), else target. H/16 waves.
+template <int H>
+__global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
+                                                         const float* __restrict__ Ptg, const float* __restrict__ gi_on,
+                                                         const float* __restrict__ gi_tg, float* __restrict__ hs_on,
+                                                         float* __restrict__ hs_tg, float* __restrict__ ws_gr,
+                                                         float* __restrict__ ws_gz, float* __restrict__ ws_gn,
+                                                         float* __restrict__ ws_ghn, const float* __restrict__ msum) {
+    constexpr int LDA = H + 4;
+    __shared__ __attribute__((aligned(16))) float hs[2][4 * LDA];
+    const int Te = t_eff(msum);
+    const int nt4 = (c.R + 3) / 4;
+    const bool online = blockIdx.x < nt4;
+    const int tile = online ? blockIdx.x : blockIdx.x - nt4;
+    const float* P = online ? Pon : Ptg;
+    const float* gi = online ? gi_on : gi_tg;
+    float* hsg = online ? hs_on : hs_tg;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b = lane >> 2, q = lane & 3;  // block, and i (A / D register) or j (B / D column = row)
+    const int g = b >> 2, fg = b & 3;
+    const int R = c.R;
+    const int r = tile * 4 + q;  // this lane's row as a B / D column
+    const bool valid = r < R;
+    const int rr = valid ? r : 0;
+    const int fA = 16 * w + 4 * fg + q;  // A operand: feature row of W_hh for this lane (i = q)
+    const int fD = 16 * w + 4 * fg;      // D: features fD..fD+3 of gate g at row r
+    float wa[H];
+#pragma unroll
+    for (int k4 = 0; k4 < H / 4; ++k4) {
+        const floatx4 v = g < 3 ? ld4(P + L.whh + (int64_t)(g * H + fA) * H + 4 * k4) : floatx4{0.f, 0.f, 0.f, 0.f};
+        wa[4 * k4] = v.x;
+        wa[4 * k4 + 1] = v.y;
+        wa[4 * k4 + 2] = v.z;
+        wa[4 * k4 + 3] = v.w;
+    }
+    const floatx4 bhn = ld4(P + L.bhh + 2 * H + fD);
+    for (int i = tid; i < 4 * LDA; i += blockDim.x) hs[0][i] = 0.f;
+    const bool lead = g == 0;  // lanes 0..15: finish the cell for (features fD.., row r)
+    st4_if(mlg_rsrc(hsg), (int64_t)rr * H + fD, floatx4{0.f, 0.f, 0.f, 0.f}, lead && valid);  // HS[0]
+    // per-step inputs: this lane's gate part of GI (r for g = 0, z for g = 1) and the n part (used by g = 0)
+    const int gq = g == 1 ? 1 : 0;
+    auto gi_at = [&](int t, int part) { return ld4(gi + ((int64_t)t * R + rr) * 3 * H + part * H + fD); };
+    const __amdgpu_buffer_rsrc_t rs_h = mlg_rsrc(hsg), rs_r = mlg_rsrc(ws_gr), rs_z = mlg_rsrc(ws_gz),
+                                 rs_n = mlg_rsrc(ws_gn), rs_hn = mlg_rsrc(ws_ghn);
+    struct In {
+        floatx4 gp, gn;
+    };
+    auto load_in = [&](int t, In& d) {
+        d.gp = gi_at(t, gq);
+        d.gn = gi_at(t, 2);
+    };
+    auto step = [&](int t, const In& in, In& nx, int cur) {
+        load_in(t + 1 < Te ? t + 1 : t, nx);  // unconditional (clamped) prefetch
+        const float* hrow = hs[cur] + q * LDA;
+        floatx4 hv[H / 4];  // the whole h row first: the MFMA chain then never waits on LDS
+#pragma unroll
+        for (int k4 = 0; k4 < H / 4; ++k4) hv[k4] = ld4(hrow + 4 * k4);
+        // two accumulation chains (even / odd k quads) halve the dependent-MFMA latency; summed at the end
+        floatx4 acc0 = g == 2 ? bhn : (g == 3 ? floatx4{0.f, 0.f, 0.f, 0.f} : in.gp), acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k4 = 0; k4 < H / 4; k4 += 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                acc0 = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[4 * k4 + e], hv[k4][e], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[4 * k4 + 4 + e], hv[k4 + 1][e], acc1, 0, 0, 0);
+            }
+        }
+        const floatx4 acc = acc0 + acc1;
+        floatx4 az, ahn;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            az[e] = __shfl(acc[e], lane + 16, 64);
+            ahn[e] = __shfl(acc[e], lane + 32, 64);
+        }
+        const floatx4 hp = ld4(hs[cur] + q * LDA + fD);
+        floatx4 rg, zg, ng, hn;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            rg[e] = sigm(acc[e]);
+            zg[e] = sigm(az[e]);
+            ng[e] = tanhf(in.gn[e] + rg[e] * ahn[e]);
+            hn[e] = ng[e] + zg[e] * (hp[e] - ng[e]);
+        }
+        if (lead) *reinterpret_cast<floatx4*>(hs[cur ^ 1] + q * LDA + fD) = hn;
+        const int64_t o = ((int64_t)t * R + r) * H + fD;
+        const bool keep = lead && valid;
+        st4_if(rs_h, o + (int64_t)R * H, hn, keep);  // HS[t + 1]
+        st4_if(rs_r, o, rg, keep && online);
+        st4_if(rs_z, o, zg, keep && online);
+        st4_if(rs_n, o, ng, keep && online);
+        st4_if(rs_hn, o, ahn, keep && online);
+        __syncthreads();
+    };
+    In ia, ib;
+    load_in(0, ia);
+    __syncthreads();
+    step(0, ia, ib, 0);  // peeled (see agent_rec_kernel)
+    for (int t = 1; t < Te; t += 2) {
+        step(t, ib, ia, 1);
+        if (t + 1 < Te) step(t + 1, ia, ib, 0);
+    }
+}
+
 // grid (ntiles, T, 2), Ap/16 waves: wave = action tile. q = b2 + W2 . h_t (h_t = HS[t + 1]).
 template <int H>
 __global__ void __launch_bounds__(512) agent_q_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
@@ -793,6 +902,124 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
     }
 }
 
+// The backward recurrence on 4-row tiles (v_mfma_f32_4x4x1_16b_f32, as agent_rec4_kernel). Wave w owns hidden
+// features 16w..16w+15; block b = 4kq + fg accumulates W_hh^T dGH for features 16w + 4fg + i over the K quarter
+// kq (48 of the 3H gate rows, W_hh columns in VGPRs); the four quarter partials are summed across lanes
+// (+16, +32, +48) into lanes 0..15, which own (features 16w + 4fg.., row) for the elementwise GRU backward.
+// grid (ntiles4), H/16 waves.
+template <int H>
+__global__ void __launch_bounds__(512) agent_bwd4_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ P,
+                                                         const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
+                                                         const float* __restrict__ ws_gz, const float* __restrict__ ws_gn,
+                                                         const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
+                                                         float* __restrict__ dgi, float* __restrict__ dgh,
+                                                         const float* __restrict__ msum) {
+    constexpr int LDG = 3 * H + 4;
+    constexpr int KQ = 3 * H / 4;  // gate rows per K quarter
+    __shared__ __attribute__((aligned(16))) float sgh[2][4 * LDG];
+    __shared__ __attribute__((aligned(16))) float w2s[MLG_BWD_MAXA * H];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int blk = lane >> 2, q = lane & 3, kq = blk >> 2, fg = blk & 3;
+    const int r = blockIdx.x * 4 + q;
+    const bool valid = r < c.R;
+    const bool lead = kq == 0;  // lanes 0..15 own (features fD.., row r) after the cross-lane K reduction
+    const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
+    const int R = c.R, N = c.N;
+    const int fD = 16 * w + 4 * fg;
+    float wt[KQ];  // A operand: W_hh[kq * KQ + kk][fD + i] (i = q)
+#pragma unroll
+    for (int kk = 0; kk < KQ; ++kk) wt[kk] = P[L.whh + (int64_t)(kq * KQ + kk) * H + fD + q];
+    const int rr = valid ? r : 0;
+    for (int i = tid; i < c.A * H; i += blockDim.x) w2s[i] = P[L.w2 + i];  // fc2 rows for dh += dq W2[a]
+    const int64_t abase = bslot(bt, b) * bt.T1 * N + n;
+    struct Step {
+        floatx4 rg, zg, ng, ghn, hp;
+        float dq;
+        int a;
+    };
+    auto load_step = [&](int t, Step& s) {
+        const int64_t o = ((int64_t)t * R + rr) * H + fD;
+        s.rg = ld4(ws_gr + o);
+        s.zg = ld4(ws_gz + o);
+        s.ng = ld4(ws_gn + o);
+        s.ghn = ld4(ws_ghn + o);
+        s.hp = ld4(ws_hs + o);  // HS[t] = h_{t-1}
+        const int tq = t < c.T - 1 ? t : c.T - 2;
+        s.dq = dqv[(int64_t)tq * R + rr];
+        s.a = t < c.T - 1 ? (int)bt.actions[abase + (int64_t)tq * N] : -1;
+    };
+    const int Te = t_eff(msum);
+    if (valid && lead) {  // steps past max_t_filled: zero deltas (wgrad rows)
+        for (int t = Te; t < c.T; ++t) {
+            const int64_t o3 = ((int64_t)t * R + r) * 3 * H + fD;
+#pragma unroll
+            for (int gq = 0; gq < 3; ++gq) {
+                *reinterpret_cast<floatx4*>(dgi + o3 + gq * H) = floatx4{0.f, 0.f, 0.f, 0.f};
+                *reinterpret_cast<floatx4*>(dgh + o3 + gq * H) = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
+    floatx4 dh = {0.f, 0.f, 0.f, 0.f};
+    const __amdgpu_buffer_rsrc_t rs_gi = mlg_rsrc(dgi), rs_gh = mlg_rsrc(dgh);
+    auto step = [&](int t, const Step& s, Step& nx, int cur) {
+        load_step(t > 0 ? t - 1 : 0, nx);
+        if (valid && s.a >= 0) dh += s.dq * ld4(w2s + s.a * H + fD);
+        floatx4 drp, dzp, dnp, dghn, dhd;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float dn = dh[e] * (1.f - s.zg[e]);
+            const float dz = dh[e] * (s.hp[e] - s.ng[e]);
+            dhd[e] = dh[e] * s.zg[e];
+            dnp[e] = dn * (1.f - s.ng[e] * s.ng[e]);
+            const float dr = dnp[e] * s.ghn[e];
+            drp[e] = dr * s.rg[e] * (1.f - s.rg[e]);
+            dzp[e] = dz * s.zg[e] * (1.f - s.zg[e]);
+            dghn[e] = dnp[e] * s.rg[e];
+        }
+        if (lead) {
+            float* gh = sgh[cur] + q * LDG;
+            *reinterpret_cast<floatx4*>(gh + fD) = drp;
+            *reinterpret_cast<floatx4*>(gh + H + fD) = dzp;
+            *reinterpret_cast<floatx4*>(gh + 2 * H + fD) = dghn;
+        }
+        const int64_t o3 = ((int64_t)t * R + r) * 3 * H + fD;
+        const bool keep = valid && lead;
+        st4_if(rs_gi, o3, drp, keep);
+        st4_if(rs_gi, o3 + H, dzp, keep);
+        st4_if(rs_gi, o3 + 2 * H, dnp, keep);
+        st4_if(rs_gh, o3, drp, keep);
+        st4_if(rs_gh, o3 + H, dzp, keep);
+        st4_if(rs_gh, o3 + 2 * H, dghn, keep);
+        __syncthreads();
+        const float* ghr = sgh[cur] + q * LDG + kq * KQ;
+        floatx4 gv[KQ / 4];
+#pragma unroll
+        for (int k4 = 0; k4 < KQ / 4; ++k4) gv[k4] = ld4(ghr + 4 * k4);
+        floatx4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k4 = 0; k4 < KQ / 4; k4 += 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                p0 = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[4 * k4 + e], gv[k4][e], p0, 0, 0, 0);
+                p1 = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[4 * k4 + 4 + e], gv[k4 + 1][e], p1, 0, 0, 0);
+            }
+        }
+        floatx4 part = p0 + p1, dprev = dhd;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            dprev[e] += (part[e] + __shfl(part[e], lane + 16, 64)) +
+                        (__shfl(part[e], lane + 32, 64) + __shfl(part[e], lane + 48, 64));
+        dh = dprev;
+    };
+    Step sa, sb;
+    load_step(Te - 1, sa);
+    step(Te - 1, sa, sb, 0);  // peeled (see agent_rec_kernel)
+    for (int t = Te - 2; t >= 0; t -= 2) {
+        step(t, sb, sa, 1);
+        if (t > 0) step(t - 1, sa, sb, 0);
+    }
+}
+
 // dA = (W_ih^T dGI) * (x > 0) for every (t, row): grid (ntiles, T), HC waves (wave = feature chunk).
 template <int H>
 __global__ void __launch_bounds__(512) agent_dx_kernel(LCfg c, const float* __restrict__ wihT,
@@ -1064,18 +1291,29 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     const int threads = (c.H / 16) * 64;
     hipLaunchKernelGGL((agent_in_kernel<H>), dim3(ntiles, c.T, 2), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                        ws + p.w.p_tg, ws + p.w.in, ws + p.w.x, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.msum);
-    hipLaunchKernelGGL((agent_rec_kernel<H>), dim3(2 * ntiles), dim3(threads), 0, s, c, p.L, ws + p.w.p_on, ws + p.w.p_tg,
-                       ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.gr, ws + p.w.gz,
-                       ws + p.w.gn, ws + p.w.ghn, ws + p.w.msum);
+    static const bool rec16 = getenv("MLG_LEARNER_REC16") != nullptr;  // A/B switch: the 16-row tile recurrence
+    if (rec16)
+        hipLaunchKernelGGL((agent_rec_kernel<H>), dim3(2 * ntiles), dim3(threads), 0, s, c, p.L, ws + p.w.p_on,
+                           ws + p.w.p_tg, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.gr,
+                           ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.msum);
+    else
+        hipLaunchKernelGGL((agent_rec4_kernel<H>), dim3(2 * ((c.R + 3) / 4)), dim3(threads), 0, s, c, p.L,
+                           ws + p.w.p_on, ws + p.w.p_tg, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.hs, ws + p.w.hs_tg,
+                           ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.msum);
     hipLaunchKernelGGL((agent_q_kernel<H>), dim3(ntiles, c.T, 2), dim3(64 * (c.Ap / 16)), 0, s, c, p.L, ws + p.w.p_on,
                        ws + p.w.p_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum);
     MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
               ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
     hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(64), 0, s, c, bt, Mon, Mtg, p.mp,
                        ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
-    hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on, ws + p.w.hs,
-                       ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi, ws + p.w.dgh,
-                       ws + p.w.msum);
+    if (rec16)
+        hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
+                           ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi,
+                           ws + p.w.dgh, ws + p.w.msum);
+    else
+        hipLaunchKernelGGL((agent_bwd4_kernel<H>), dim3((c.R + 3) / 4), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
+                           ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi,
+                           ws + p.w.dgh, ws + p.w.msum);
     hipLaunchKernelGGL((agent_dx_kernel<H>), dim3(ntiles, c.T), dim3(threads), 0, s, c, ws + p.w.wihT, ws + p.w.x,
                        ws + p.w.dgi, ws + p.w.da, ws + p.w.msum);
     int64_t slab_floats;
