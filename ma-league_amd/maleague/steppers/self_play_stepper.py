@@ -27,12 +27,14 @@ class SelfPlayParallelStepper(ParallelStepper):
             raise ValueError(f"A total of {self.spec.n_agents} agents in the env do not fit in the symmetric "
                              "two-team scenario. Ensure the Self-Play scenario has two teams set to is_scripted=False")
         self.away_batch = None
+        self._away_buf = None
 
     def initialize(self, scheme, groups, preprocess, home_mac, away_mac=None):
         if away_mac is None:
             raise ValueError("self-play needs an away MAC (initialize(..., home_mac, away_mac))")
         ParallelStepper.initialize(self, scheme, groups, preprocess, home_mac)
         self.away_mac = away_mac
+        self._away_buf = None
 
     @property
     def epsilons(self):
@@ -68,8 +70,19 @@ class SelfPlayParallelStepper(ParallelStepper):
             self.home_batch = self.new_batch_fn()
             mb_h, k = mlg_batch(self.home_batch)
             keep.append(k)
-        self.away_batch = self.new_batch_fn()
-        mb_a, k = mlg_batch(self.away_batch)
+        if getattr(self.args, "reuse_away_batch", True):
+            # one away batch, rewritten in full-write mode by every run (every byte of its B slots is stored,
+            # zeros past each episode's end): no per-run allocation and ~1 GB zero fill. The batch returned by
+            # run k is therefore overwritten by run k + 1; reuse_away_batch=False gives the reference's fresh
+            # batch per run (self_play_parallel_stepper.py:95).
+            if self._away_buf is None:
+                self._away_buf = self.new_batch_fn()
+            self.away_batch = self._away_buf
+            mb_a, k = mlg_batch(self.away_batch)
+            mb_a.full_write = 1
+        else:
+            self.away_batch = self.new_batch_fn()
+            mb_a, k = mlg_batch(self.away_batch)
         keep.append(k)
         h_agent, a_agent = self.home_mac.agent, self.away_mac.agent
         d, d_a = h_agent.dims(), a_agent.dims()

@@ -131,7 +131,8 @@ def test_selfplay_identical_policies_symmetric(device):
 
 
 def test_selfplay_ring_mode_equals_plain(device):
-    """Home episodes written straight into the replay ring equal the zero-initialised EpisodeBatch."""
+    """Home episodes written straight into the replay ring, and away episodes written in full-write mode into the
+    reused away batch (pre-filled with garbage), equal the zero-initialised EpisodeBatches."""
     from maleague.components.replay_buffer import ReplayBuffer
     from maleague.envs.teams_env import VecEnvState
     stepper, home, away, args = _build(device, B=48, episode_limit=30, seed=2)
@@ -146,13 +147,19 @@ def test_selfplay_ring_mode_equals_plain(device):
         st0.episode.fill_(it)
         stepper.envs = st0
         stepper._ring = None
+        stepper.args.reuse_away_batch = False  # fresh zero-initialised away batch (reference behaviour)
         hp, ap, _ = stepper.run(test_mode=False)
         stepper.t_env -= int(stepper.last_run["ep_len"].sum())
         st1 = VecEnvState(stepper.spec, 48, device)
         st1.episode.fill_(it)
         stepper.envs = st1
         assert stepper.attach_replay(ring)
+        stepper.args.reuse_away_batch = True
+        if stepper._away_buf is not None:
+            for v in stepper._away_buf.data.transition_data.values():
+                v.fill_(7)
         hr, ar, _ = stepper.run(test_mode=False)
+        assert ar is not ap
         for k in hp.data.transition_data:
             assert torch.equal(hp[k], hr[k]), (it, k)
             assert torch.equal(ap[k], ar[k]), (it, k)
