@@ -10,7 +10,7 @@
 //               TD error, masked MSE partials, QMixer backward -> dQ and mixer deltas         (:55-98)
 //   agent_bwd   reverse-time GRU backward (dh carried in registers, dGH exchanged in LDS)    (:103)
 //   agent_dx    dX = W_ih^T dGI * relu' for every (t, row), fully parallel
-//   wgrad       every weight/bias gradient as sum_rows delta^T x, split over row chunks
+//   wgrad       every weight/bias gradient as sum_rows delta^T x, one wave per 64x64 block and row chunk
 //               (deterministic slab reduction; MFMA with the row index as K)
 //   finish      loss/stat reduction, clip_grad_norm_(10), RMSprop step                       (:104-105, learner.py:25-31)
 // Tensors saved for backward are t-major: [T][R][F] with R = B * N agent rows (r = b * N + n).
@@ -20,7 +20,7 @@
 
 namespace {
 
-using WJobs = mlg::WJobsT<16>;
+using WJobs = mlg::BJobsT<16>;
 using mlg::WJob;
 using mlg::job;
 using mlg::block_sum_1024;
@@ -1197,7 +1197,7 @@ Plan make_plan(const MlgLearnerCfg* cfg, int T1) {
 
 
 // builds the job list; with ws == nullptr only sizes are computed (pointers are offsets from 0)
-WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_tasks) {
+WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_tasks, int64_t* n_red) {
     const LCfg& c = p.c;
     float* W = ws ? ws : nullptr;
     auto at = [&](int64_t off) { return W ? W + off : (float*)nullptr; };
@@ -1207,10 +1207,10 @@ WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     WJobs J;
     J.n = 0;
     const AgentOffs& a = p.ao;
-    J.j[J.n++] = job(at(p.w.da), H, at(p.w.in), c.d_in, gp(a.fc1w), gp(a.fc1b), H, c.d_in, TR);
-    J.j[J.n++] = job(at(p.w.dgi), 3 * H, at(p.w.x), H, gp(a.wih), gp(a.bih), 3 * H, H, TR);
-    J.j[J.n++] = job(at(p.w.dgh), 3 * H, at(p.w.hs), H, gp(a.whh), gp(a.bhh), 3 * H, H, TR);
-    J.j[J.n++] = job(at(p.w.d2), c.A, at(p.w.hs) ? at(p.w.hs) + (int64_t)c.R * H : nullptr, H, gp(a.fc2w), gp(a.fc2b),
+    J.j[J.n++] = mlg::bjob(at(p.w.da), H, at(p.w.in), c.d_in, gp(a.fc1w), gp(a.fc1b), H, c.d_in, TR);
+    J.j[J.n++] = mlg::bjob(at(p.w.dgi), 3 * H, at(p.w.x), H, gp(a.wih), gp(a.bih), 3 * H, H, TR);
+    J.j[J.n++] = mlg::bjob(at(p.w.dgh), 3 * H, at(p.w.hs), H, gp(a.whh), gp(a.bhh), 3 * H, H, TR);
+    J.j[J.n++] = mlg::bjob(at(p.w.d2), c.A, at(p.w.hs) ? at(p.w.hs) + (int64_t)c.R * H : nullptr, H, gp(a.fc2w), gp(a.fc2b),
                      c.A, H, TR);
     if (c.mixer == 2) {
         const MixOffs& m = p.mo;
@@ -1219,27 +1219,17 @@ WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
         const float* d1 = at(p.w.d1);
         const float* la = at(p.w.l1act);
         auto off = [&](const float* base, int64_t k) { return base ? base + k : (const float*)nullptr; };
-        J.j[J.n++] = job(off(d1, 0), L1, at(p.w.srow), c.S, mg(m.w1_0w), mg(m.w1_0b), c.HE, c.S, RM);
-        J.j[J.n++] = job(off(d1, c.HE), L1, at(p.w.srow), c.S, mg(m.wf_0w), mg(m.wf_0b), c.HE, c.S, RM);
-        J.j[J.n++] = job(off(d1, 2 * c.HE), L1, at(p.w.srow), c.S, mg(m.b1w), mg(m.b1b), c.E, c.S, RM);
-        J.j[J.n++] = job(off(d1, 2 * c.HE + c.E), L1, at(p.w.srow), c.S, mg(m.v0w), mg(m.v0b), c.E, c.S, RM);
-        J.j[J.n++] = job(at(p.w.da2), (int64_t)c.N * c.E, off(la, 0), L1, mg(m.w1_2w), mg(m.w1_2b), c.N * c.E, c.HE, RM);
-        J.j[J.n++] = job(at(p.w.df2), c.E, off(la, c.HE), L1, mg(m.wf_2w), mg(m.wf_2b), c.E, c.HE, RM);
-        J.j[J.n++] = job(at(p.w.dv2), 1, off(la, 2 * c.HE + c.E), L1, mg(m.v2w), mg(m.v2b), 1, c.E, RM);
+        J.j[J.n++] = mlg::bjob(off(d1, 0), L1, at(p.w.srow), c.S, mg(m.w1_0w), mg(m.w1_0b), c.HE, c.S, RM);
+        J.j[J.n++] = mlg::bjob(off(d1, c.HE), L1, at(p.w.srow), c.S, mg(m.wf_0w), mg(m.wf_0b), c.HE, c.S, RM);
+        J.j[J.n++] = mlg::bjob(off(d1, 2 * c.HE), L1, at(p.w.srow), c.S, mg(m.b1w), mg(m.b1b), c.E, c.S, RM);
+        J.j[J.n++] = mlg::bjob(off(d1, 2 * c.HE + c.E), L1, at(p.w.srow), c.S, mg(m.v0w), mg(m.v0b), c.E, c.S, RM);
+        J.j[J.n++] = mlg::bjob(at(p.w.da2), (int64_t)c.N * c.E, off(la, 0), L1, mg(m.w1_2w), mg(m.w1_2b), c.N * c.E, c.HE, RM);
+        J.j[J.n++] = mlg::bjob(at(p.w.df2), c.E, off(la, c.HE), L1, mg(m.wf_2w), mg(m.wf_2b), c.E, c.HE, RM);
+        J.j[J.n++] = mlg::bjob(at(p.w.dv2), 1, off(la, 2 * c.HE + c.E), L1, mg(m.v2w), mg(m.v2b), 1, c.E, RM);
     }
-    int tasks = 0;
-    int64_t slab = 0;
-    for (int q = 0; q < J.n; ++q) {
-        J.j[q].task0 = tasks;
-        J.j[q].slab0 = slab;
-        tasks += J.j[q].mt * J.j[q].nt * J.j[q].chunks;
-        slab += (int64_t)J.j[q].mt * J.j[q].nt * J.j[q].chunks * 272;
-    }
-    int64_t n_red = 0;
-    for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
-    *slab_floats = a4(slab) + a4((n_red + 255) / 256);  // slab partials + per-block norm partials
-    p.w.nrm = p.w.slab + a4(slab);
-    *n_tasks = tasks;
+    int64_t slab_part;
+    *slab_floats = mlg::layout_bjobs(J, n_tasks, n_red, &slab_part);  // slab partials + per-block norm partials
+    p.w.nrm = p.w.slab + slab_part;
     return J;
 }
 
@@ -1316,15 +1306,14 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
                            ws + p.w.dgh, ws + p.w.msum);
     hipLaunchKernelGGL((agent_dx_kernel<H>), dim3(ntiles, c.T), dim3(threads), 0, s, c, ws + p.w.wihT, ws + p.w.x,
                        ws + p.w.dgi, ws + p.w.da, ws + p.w.msum);
-    int64_t slab_floats;
+    int64_t slab_floats, n_red;
     int n_tasks;
-    WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks);
-    hipLaunchKernelGGL(mlg::wgrad_kernel<16>, dim3((n_tasks + 3) / 4), dim3(256), 0, s, J, ws + p.w.slab);
-    int64_t n_red = 0;  // same count as make_jobs
-    for (int q = 0; q < J.n; ++q) n_red += (int64_t)J.j[q].mt * J.j[q].nt * 272;
+    WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
+    hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((n_tasks + 3) / 4)), dim3(256), 0, s, J,
+                       ws + p.w.slab);
     const int n_red_blocks = (int)((n_red + 255) / 256);
-    hipLaunchKernelGGL(mlg::wgrad_reduce_kernel<16>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + p.w.slab,
-                       ws + p.w.nrm);
+    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J,
+                       ws + p.w.slab, ws + p.w.nrm);
     const int64_t n_par = p.n_agent + p.n_mixer;
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + p.w.part,
                        p.w.n_mix_tiles, ws + p.w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr,
@@ -1346,9 +1335,9 @@ extern "C" int64_t mlg_qlearner_param_counts(const MlgLearnerCfg* c, int64_t* n_
 extern "C" int64_t mlg_qlearner_workspace_floats(const MlgLearnerCfg* c) {
     if (check_cfg(c)) return -1;
     Plan p = make_plan(c, c->T);
-    int64_t slab;
+    int64_t slab, n_red;
     int tasks;
-    make_jobs(p, nullptr, nullptr, &slab, &tasks);
+    make_jobs(p, nullptr, nullptr, &slab, &tasks, &n_red);
     return p.w.total + slab;
 }
 

@@ -244,22 +244,31 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
         mv[i] = mi[i] < jb.M;
         kv[i] = ki[i] < jb.K;
     }
-    for (int rr = r0; rr < r1; rr += 4) {
-        const int row = rr + g;
-        const bool rv = row < r1;
-        const float* dr = jb.delta + (int64_t)row * jb.ldd;
-        const float* xr = jb.x + (int64_t)row * jb.ldx;
-        float a[4], b[4];
+    // two 4-row steps per iteration: both steps' loads are issued before the first step's MFMAs (same
+    // accumulation order as one step per iteration)
+    for (int rr = r0; rr < r1; rr += 8) {
+        float a[2][4], b[2][4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            a[i] = (mv[i] && rv) ? dr[mi[i]] : 0.f;
-            b[i] = (kv[i] && rv) ? xr[ki[i]] : 0.f;
+        for (int h = 0; h < 2; ++h) {
+            const int row = rr + 4 * h + g;
+            const bool rv = row < r1;
+            const float* dr = jb.delta + (int64_t)row * jb.ldd;
+            const float* xr = jb.x + (int64_t)row * jb.ldx;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a[h][i] = (mv[i] && rv) ? dr[mi[i]] : 0.f;
+                b[h][i] = (kv[i] && rv) ? xr[ki[i]] : 0.f;
+            }
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            bsum[i] += a[i];
+        for (int h = 0; h < 2; ++h) {
+            if (h == 1 && rr + 4 >= r1) break;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
+            for (int i = 0; i < 4; ++i) {
+                bsum[i] += a[h][i];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(a[h][i], b[h][j], acc[i][j]);
+            }
         }
     }
     float* out = slab + jb.slab0 + ((int64_t)blk * jb.chunks + ch) * BSLAB;
@@ -296,7 +305,15 @@ __global__ void __launch_bounds__(256) wgrad_block_reduce_kernel(BJobsT<MJ> J, c
             const int mbi = blk / jb.nb, nbi = blk % jb.nb;
             float s = 0.f;
             const float* base = slab + jb.slab0 + (int64_t)blk * jb.chunks * BSLAB + e;
-            for (int ch = 0; ch < jb.chunks; ++ch) s += base[(int64_t)ch * BSLAB];
+            int ch = 0;
+            for (; ch + 8 <= jb.chunks; ch += 8) {  // 8 loads in flight, summed in chunk order
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(ch + u) * BSLAB];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s += v[u];
+            }
+            for (; ch < jb.chunks; ++ch) s += base[(int64_t)ch * BSLAB];
             if (e < 4096) {
                 const int m = mbi * 64 + e / 64, k = nbi * 64 + e % 64;
                 if (m < jb.M && k < jb.K) {
