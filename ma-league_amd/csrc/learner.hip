@@ -646,11 +646,15 @@ struct MixOut {
 };
 
 template <int HE, int E>
-__global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs Mon, MixPtrs Mtg, MixPack mp,
+__global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs Mon, MixPtrs Mtg, MixPack mp,
                                                     const float* __restrict__ mac, const float* __restrict__ tmac,
                                                     const float* __restrict__ msum_p, MixOut o) {
     using Mx = Mixer<HE, E>;
-    const int lane = threadIdx.x, col = lane & 15, g = lane >> 4;
+    // two waves per 16-row tile: wave 0 runs the target mixer forward and hands y's target to wave 1 through LDS,
+    // wave 1 runs the online forward, TD and the mixer backward (VDN: wave 1 alone)
+    __shared__ float tgt_sh[16];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, g = lane >> 4;
+    if (c.mixer != 2 && wv == 0) return;
     const int rm = blockIdx.x * 16 + col;
     const int Tm = c.T - 1;
     const bool valid = rm < c.RM;
@@ -668,11 +672,17 @@ __global__ void __launch_bounds__(64) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs
     float qtot, tgt;
     floatx4 l1[Mx::L1T], pre[Mx::TE], hid[Mx::TE], wfp[Mx::TE];
     if (c.mixer == 2) {
-        {
+        if (wv == 0) {
             floatx4 tl1[Mx::L1T], tpre[Mx::TE], thid[Mx::TE], twfp[Mx::TE];
-            tgt = Mx::forward(Mtg, mp, S, N, s1, tq, tl1, tpre, thid, twfp, lane);
+            const float tv = Mx::forward(Mtg, mp, S, N, s1, tq, tl1, tpre, thid, twfp, lane);
+            if (g == 0) tgt_sh[col] = tv;
+            qtot = 0.f;
+        } else {
+            qtot = Mx::forward(Mon, mp, S, N, s0, cq, l1, pre, hid, wfp, lane);
         }
-        qtot = Mx::forward(Mon, mp, S, N, s0, cq, l1, pre, hid, wfp, lane);
+        __syncthreads();
+        if (wv == 0) return;
+        tgt = tgt_sh[col];
     } else {  // VDN (vdn.py:9)
         qtot = 0.f;
         tgt = 0.f;
@@ -1294,7 +1304,7 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
                        ws + p.w.p_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum);
     MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
               ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
-    hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(64), 0, s, c, bt, Mon, Mtg, p.mp,
+    hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, Mtg, p.mp,
                        ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
     if (rec16)
         hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
