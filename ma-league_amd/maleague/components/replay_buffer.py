@@ -4,6 +4,9 @@ Lives on the training device (HBM) so sampling and training never cross PCIe.
 """
 from __future__ import annotations
 
+import weakref
+from types import SimpleNamespace
+
 import numpy as np
 import torch
 
@@ -16,14 +19,36 @@ class ReplayBuffer(EpisodeBatch):
         self.buffer_size = buffer_size
         self.buffer_index = 0
         self.episodes_in_buffer = 0
+        self._outstanding = []  # weakrefs to RingEpisodeBatches written into the ring but not inserted yet
+
+    def has_outstanding(self) -> bool:
+        """True while a rollout's episodes sit in the ring's next slots uncommitted (written in place, not yet
+        passed to insert_episode_batch). A stepper must not write another run there: that would overwrite them,
+        while the reference leaves the buffer untouched until insert."""
+        self._outstanding = [r for r in getattr(self, "_outstanding", []) if r() is not None and r().attached]
+        return bool(self._outstanding)
+
+    def _register(self, ring_batch: "RingEpisodeBatch"):
+        if not hasattr(self, "_outstanding"):
+            self._outstanding = []
+        self._outstanding.append(weakref.ref(ring_batch))
+
+    def _detach_outstanding(self):
+        """Give every uncommitted ring batch its own copy before a plain insert overwrites its slots."""
+        for r in getattr(self, "_outstanding", []):
+            rb = r()
+            if rb is not None and rb.attached:
+                rb.detach()
+        self._outstanding = []
 
     def insert_episode_batch(self, ep_batch: EpisodeBatch):
-        if isinstance(ep_batch, RingEpisodeBatch) and ep_batch.ring is self and not ep_batch.committed:
+        if isinstance(ep_batch, RingEpisodeBatch) and ep_batch.attached and ep_batch.ring is self:
             if ep_batch.slot0 != self.buffer_index:
                 raise RuntimeError("ring episodes must be inserted in the order they were written")
             self._advance(ep_batch.batch_size)
             ep_batch.committed = True
             return
+        self._detach_outstanding()
         room = self.buffer_size - self.buffer_index
         if ep_batch.batch_size > room:
             # split at the wrap point and insert both halves (replay_buffer.py:37-41)
@@ -100,12 +125,24 @@ class RingEpisodeBatch(EpisodeBatch):
         self.scheme, self.groups, self.preprocess = ring.scheme, ring.groups, ring.preprocess
         self.batch_size, self.max_seq_length, self.device = batch_size, ring.max_seq_length, ring.device
         self._data = None
+        ring._register(self)
+
+    @property
+    def attached(self) -> bool:
+        """Still backed by (uncommitted) ring slots: insert_episode_batch only advances the ring's indices."""
+        return self.ring is not None and not self.committed
+
+    def detach(self):
+        """Materialise the episodes into their own tensors (the ring slots are about to be reused); the batch
+        then behaves like a plain EpisodeBatch (insert copies it)."""
+        d = self.data
+        self._data = SimpleNamespace(transition_data={k: v.clone() for k, v in d.transition_data.items()},
+                                     episode_data={k: v.clone() for k, v in d.episode_data.items()})
+        self.ring = None
 
     @property
     def data(self):
         if self._data is None:
-            from types import SimpleNamespace
-            import torch
             size, B = self.ring.buffer_size, self.batch_size
             if self.slot0 + B <= size:
                 sel = lambda v: v[self.slot0:self.slot0 + B]  # noqa: E731
@@ -142,7 +179,6 @@ class SampledEpisodeBatch(EpisodeBatch):
     @property
     def data(self):
         if self._data is None:
-            from types import SimpleNamespace
             idx = self.rows.long()
             self._data = SimpleNamespace(
                 transition_data={k: v.index_select(0, idx) for k, v in self.ring.data.transition_data.items()},

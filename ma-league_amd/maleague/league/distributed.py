@@ -13,6 +13,7 @@ matchmaking is local and needs no coordinator process.
 """
 from __future__ import annotations
 
+import logging
 from typing import List
 
 import numpy as np
@@ -20,6 +21,8 @@ import torch
 import torch.distributed as dist
 
 from .payoff import PayoffEntry, PayoffWrapper, PFSPSampling
+
+log = logging.getLogger(__name__)
 
 
 class DistributedLeague:
@@ -37,6 +40,7 @@ class DistributedLeague:
         self.current = None            # [n_players, n_params]
         self.historical = None         # [max_historical, n_params]
         self.historical_meta: List[tuple] = []  # (pid, parent pid, trained_steps)
+        self.pool_full_skips = 0  # checkpoint requests dropped because the historical pool was full
 
     def player(self) -> int:
         return self.rank % self.n
@@ -96,10 +100,16 @@ class DistributedLeague:
     def exchange(self, flat: torch.Tensor, trained_steps: int, checkpoint: bool):
         """all_gather [params | trained_steps | checkpoint flag] of every player; refresh the replicated pool and
         append a historical snapshot for every player that asked for a checkpoint (in player order, so every
-        rank assigns the same historical pids). Returns the list of new historical pids."""
+        rank assigns the same historical pids). trained_steps travels as two float32 halves (steps mod 2^24 and
+        steps >> 24), exact up to 2^48 (the reference's checkpoint thresholds are 2e9 / 4e9 steps). Returns the
+        list of new (historical pid, parent pid); a player whose request found the pool full is not in it (and
+        a warning is logged), so the caller resets its checkpoint clock only for snapshots actually taken."""
         n_p = flat.numel()
-        msg = torch.cat([flat.detach().reshape(-1).to(torch.float32),
-                         torch.tensor([float(trained_steps), 1.0 if checkpoint else 0.0], device=flat.device)])
+        steps = int(trained_steps)
+        if not 0 <= steps < 2 ** 48:
+            raise ValueError(f"trained_steps {steps} outside the exchange's exact range [0, 2^48)")
+        meta_in = [float(steps & 0xFFFFFF), float(steps >> 24), 1.0 if checkpoint else 0.0]
+        msg = torch.cat([flat.detach().reshape(-1).to(torch.float32), torch.tensor(meta_in, device=flat.device)])
         gathered = self.share_params(msg)
         allm = torch.stack(gathered)[: self.n]
         if self.current is None:
@@ -107,17 +117,21 @@ class DistributedLeague:
             cap = self.capacity - self.n
             self.historical = torch.empty(max(cap, 0), n_p, dtype=torch.float32, device=flat.device)
         self.current.copy_(allm[:, :n_p])
-        meta = allm[:, n_p:].detach().cpu().numpy()
+        meta = allm[:, n_p:].detach().cpu().numpy().astype(np.int64)
         new = []
         for pid in range(self.n):
-            if meta[pid, 1] > 0.5:
+            if meta[pid, 2] > 0:
                 k = len(self.historical_meta)
                 if self.n + k >= self.capacity:
-                    continue  # pool full: keep the existing snapshots
+                    self.pool_full_skips += 1
+                    if self.pool_full_skips == 1 or self.pool_full_skips % 100 == 0:
+                        log.warning("league: historical pool full (%d snapshots): checkpoint of player %d skipped "
+                                    "(%d skips so far; raise max_historical)", k, pid, self.pool_full_skips)
+                    continue
                 self.historical[k].copy_(self.current[pid])
                 hp = self.n + k
-                self.historical_meta.append((hp, pid, int(meta[pid, 0])))
-                new.append(hp)
+                self.historical_meta.append((hp, pid, int(meta[pid, 0] + (meta[pid, 1] << 24))))
+                new.append((hp, pid))
         return new
 
     def params_of(self, pid: int) -> torch.Tensor:

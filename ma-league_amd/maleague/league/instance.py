@@ -88,9 +88,9 @@ class LeagueInstance:
         steps = int(home.agent.trained_steps)
         self.me.trained_steps = steps
         ckpt = self.me.ready_to_checkpoint(self.view()) if self.mode == "rolebased" else False
-        self.league.exchange(agent_vector(home), steps, ckpt)
-        if ckpt:
-            self.me.checkpoint()
+        taken = self.league.exchange(agent_vector(home), steps, ckpt)
+        if ckpt and any(parent == self.pid for _, parent in taken):
+            self.me.checkpoint()  # only when the snapshot exists (pool not full): otherwise it asks again
         self.league.barrier()
         view = self.view()
         if self.matchmaker is not None:

@@ -127,8 +127,13 @@ class REFILLearner(Learner):
         if callable(t_env):
             t_env = t_env()
         if t_env - self.log_stats_t >= self.args.learner_log_interval:
+            # the reference REFIL learner logs unprefixed keys, im_loss only for imagine agents
+            # (refil_learner.py:185-195; unlike QLearner's "{name}loss" keys)
+            imagine = "imagine" in str(getattr(self.args, "agent", ""))
             for k, v in self.last_stats.items():
-                self.logger.log_stat(self.name + k, v, t_env)
+                if k == "im_loss" and not imagine:
+                    continue
+                self.logger.log_stat(k, v, t_env)
             self.log_stats_t = t_env
 
     @property

@@ -281,6 +281,10 @@ class ParallelStepper(EnvStepper):
         if test_mode:
             sel.epsilon = 0.0
         ring = self._ring if not test_mode else None
+        if ring is not None and ring.has_outstanding():
+            # the previous train-mode run's episodes still occupy the ring's next slots (not inserted yet):
+            # this run goes to a fresh batch, as in the reference, which leaves the buffer untouched until insert
+            ring = None
         if ring is not None:
             slot0 = ring.buffer_index
             mb, keep = self._to_mlg(ring)

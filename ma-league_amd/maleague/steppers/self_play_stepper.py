@@ -60,6 +60,10 @@ class SelfPlayParallelStepper(ParallelStepper):
         eps_a = self._epsilon_of(self.away_mac, test_mode)
         keep = []
         ring = self._ring if not test_mode else None
+        if ring is not None and ring.has_outstanding():
+            # the previous train-mode run's episodes still occupy the ring's next slots (not inserted yet):
+            # this run goes to a fresh batch, as in the reference, which leaves the buffer untouched until insert
+            ring = None
         if ring is not None:
             slot0 = ring.buffer_index
             mb_h, k = mlg_batch(ring)

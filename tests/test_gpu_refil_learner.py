@@ -74,6 +74,8 @@ def test_refil_learner_two_calls_match_golden(device, golden):
         for k, v in L.mixer.named_parameters():
             np.testing.assert_allclose(v.detach().cpu().numpy(), d[f"c{call}.mixer.{k}"], atol=2e-5, rtol=0,
                                        err_msg=f"call {call} mixer {k}")
+    # the reference REFIL learner logs unprefixed keys (refil_learner.py:185-195), im_loss for imagine agents
+    assert set(log.stats) == {"loss", "im_loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"}
 
 
 @pytest.mark.parametrize("softmax,double_q", [(False, True), (True, False)])

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import scheme_for
+from helpers import qmix_args, scheme_for
 
 
 def _mk_batch(B, T, N, d_obs, A, S, lengths, seed):
@@ -119,3 +119,72 @@ def test_env_oracle_self_consistency():
                 assert t < 29 or True
                 break
         assert done
+
+
+def test_stepper_two_runs_before_insert_keep_the_ring_intact(monkeypatch):
+    """a second train-mode run() before insert_episode_batch must not overwrite the first run's
+    episodes (which the zero-copy path writes straight into the ring's next slots): it goes to a fresh batch,
+    like the reference, whose buffer is untouched until insert. The kernel launch is replaced by a fake that
+    stamps each run's id into its target (CPU: no GPU calls)."""
+    from types import SimpleNamespace
+    from maleague.components.replay_buffer import ReplayBuffer, RingEpisodeBatch
+    from maleague.components.epsilon_schedules import DecayThenFlatSchedule
+    from maleague.custom_logging import MainLogger
+    from maleague.steppers import ParallelStepper
+    import maleague.steppers.parallel_stepper as ps
+
+    class _Ev:
+        def record(self):
+            pass
+
+        def synchronize(self):
+            pass
+
+    monkeypatch.setattr(ps.torch.cuda, "Event", lambda *a, **k: _Ev())
+    B, T = 4, 11
+    args = qmix_args(batch_size_run=B, device="cpu", env_args={"match_build_plan": "medium_1h_4t", "grid_size": 20,
+                                                               "stochastic_spawns": True, "episode_limit": T - 1})
+    stepper = ParallelStepper(args, MainLogger())
+    info = stepper.get_env_info()
+    scheme, groups, preprocess = scheme_for(info, torch)
+    sel = SimpleNamespace(schedule=DecayThenFlatSchedule(1.0, 0.05, 50000), epsilon=1.0)
+    stepper.initialize(scheme, groups, preprocess, SimpleNamespace(init_hidden=lambda batch_size: None,
+                                                                   action_selector=sel))
+    ring = ReplayBuffer(scheme, groups, 10, T, preprocess=preprocess, device="cpu")
+    assert stepper.attach_replay(ring)
+    stamp = [0]
+
+    def fake_to_mlg(batch):
+        return SimpleNamespace(target=batch, B=B, ring_slot0=0, ring_size=0, full_write=0), []
+
+    def fake_launch(mb, eps, test_mode):
+        stamp[0] += 1
+        obs = mb.target.data.transition_data["obs"]
+        if mb.target is ring:  # kernel writes slots [ring_slot0, +B) mod size
+            for b in range(mb.B):
+                obs[(mb.ring_slot0 + b) % mb.ring_size].fill_(stamp[0])
+        else:
+            obs.fill_(stamp[0])
+        stepper._info[0:B] = 3
+
+    monkeypatch.setattr(stepper, "_to_mlg", fake_to_mlg)
+    monkeypatch.setattr(stepper, "_launch_mb", fake_launch)
+    b1, _ = stepper.run(test_mode=False)
+    assert isinstance(b1, RingEpisodeBatch) and ring.has_outstanding()
+    b2, _ = stepper.run(test_mode=False)  # second run before any insert: fresh batch, ring untouched
+    assert not isinstance(b2, RingEpisodeBatch)
+    assert (b1["obs"] == 1).all() and (b2["obs"] == 2).all()
+    ring.insert_episode_batch(b1)
+    ring.insert_episode_batch(b2)
+    assert (ring["obs"][0:B] == 1).all() and (ring["obs"][B:2 * B] == 2).all()
+    assert ring.buffer_index == 2 * B and not ring.has_outstanding()
+    # back to the zero-copy path once nothing is outstanding
+    b3, _ = stepper.run(test_mode=False)
+    assert isinstance(b3, RingEpisodeBatch) and b3.slot0 == 2 * B
+    # inserting a plain batch first detaches the uncommitted ring episodes before their slots are overwritten
+    b4, _ = stepper.run(test_mode=False)
+    ring.insert_episode_batch(b4)
+    assert not b3.attached and (b3["obs"] == 3).all()
+    ring.insert_episode_batch(b3)
+    # b4 took slots 8, 9, 0, 1 (wrap at 10), b3 the next four
+    assert (ring["obs"][8:10] == 4).all() and (ring["obs"][0:2] == 4).all() and (ring["obs"][2:6] == 3).all()

@@ -4,6 +4,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -273,3 +274,39 @@ def test_league_instances_gloo_world4_alphastar():
             assert (opp >= 4) == is_hist
             if rank >= 2:  # exploiters only ever face main players or main players' checkpoints
                 assert opp in (0, 1) or any(h[0] == opp and h[1] in (0, 1) for h in meta0)
+
+
+def test_exchange_exact_steps_and_full_pool(caplog):
+    """trained_steps past 2^24 survive the exchange exactly (reference thresholds 2e9 / 4e9), and a
+    checkpoint request that finds the historical pool full is reported as not taken (and logged)."""
+    import logging
+    from maleague.league import DistributedLeague
+    lg = DistributedLeague(n_players=1, device="cpu", max_historical=1)
+    flat = torch.arange(5, dtype=torch.float32)
+    steps = 4_000_000_007
+    assert lg.exchange(flat, steps, True) == [(1, 0)]
+    assert lg.historical_meta == [(1, 0, steps)]
+    with caplog.at_level(logging.WARNING, logger="maleague.league.distributed"):
+        assert lg.exchange(flat + 1, steps + 1, True) == []
+    assert lg.pool_full_skips == 1 and "pool full" in caplog.text
+    assert lg.historical_meta == [(1, 0, steps)] and torch.equal(lg.params_of(1), flat)
+    with pytest.raises(ValueError):
+        lg.exchange(flat, 2 ** 48, False)
+
+
+def test_checkpoint_clock_kept_when_pool_full():
+    """LeagueInstance.sync resets the player's checkpoint clock only when its snapshot was actually stored."""
+    from types import SimpleNamespace
+    from maleague.league import DistributedLeague, LeagueInstance
+    args = SimpleNamespace(matchmaking="pfsp", league_checkpoint_min_steps=100, league_checkpoint_max_steps=200,
+                           env_args={})
+    lg = DistributedLeague(n_players=1, device="cpu", seed=0, max_historical=1)
+    exp = _FakeExperiment(0)
+    inst = LeagueInstance(args, None, lg, mode="rolebased", role=["main"], seed=0, experiment=exp)
+    calls = []
+    inst.me.ready_to_checkpoint = lambda view: True
+    inst.me.checkpoint = lambda: calls.append(len(lg.historical_meta))
+    inst.sync()
+    assert calls == [1]          # snapshot stored -> clock reset
+    inst.sync()
+    assert calls == [1] and lg.pool_full_skips == 1  # pool full -> no reset, the player asks again
