@@ -5,8 +5,9 @@ the HBM replay buffer + one QLearner.train on 32 sampled episodes (MultiAgentExp
 src/runs/train/ma_experiment.py:224-241). value = env steps (t_env increments, parallel_stepper.py:178-179)
 of all ranks / max-over-ranks time.
 
-Modes (--mode auto picks by world size, as BASELINE.json's configs are defined):
-  ai        config 2: one learner vs the scripted AI per GPU (N = 1)
+Modes (--mode auto = ai at every N: the metric's config-2 workload per GPU, weak scaling):
+  ai        config 2: one learner vs the scripted AI per GPU; N > 1 = N independent learners (one per GPU,
+            4096 envs each, no data-path collective: learners never exchange anything on the rollout/learn path)
   refil     config 5: REFIL (entity-attention agent, imagined groups, FlexQMixer), 3-8 agents per env padded to 8,
             4096 envs per GPU vs the scripted AI (entity env variant); N > 1 = independent replicas
   league    config 3 (N = 2: two PFSP self-play learners, opponent swap over RCCL) / config 4 (N >= 4:
@@ -72,7 +73,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if a.device is not None:
         local_rank = a.device
-    mode = a.mode if a.mode != "auto" else ("ai" if world == 1 else "league")
+    mode = a.mode if a.mode != "auto" else "ai"
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -113,7 +114,7 @@ def main():
             parallelism = f"replicas{world}"
         else:
             workload = f"qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
-            parallelism = f"league{world}"
+            parallelism = f"replicas{world}"
     else:
         from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
         lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=8 * world)

@@ -779,13 +779,21 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
 // Env phase: half-wave per env, lane per unit (v2 env above); wave w steps envs 2w and 2w + 1.
 // Barriers per step: A|B, B|C, C|env, env|A.
 struct RolloutLds2 {
-    int32_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, total;
+    int32_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, rmap, total;
     int ldo, ldh, nhb;  // nhb: hidden-state buffers (2: double buffered by step parity; 1: v6, see below)
+    int xpl;            // v7: x held as three bf16 planes per row, row stride XPL_STRIDE words (0: fp32 rows)
+    int rms;            // v7: words per wave row map
     RoEnvLds env;
 };
 
-__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N, int rew, int nhb = 2) {
+// v7 x planes: row = 3 pieces x 64 bf16 (128 B each) + 16 B pad -> 100 words, so the 16 rows of an MFMA B read
+// start on distinct bank quads (100 mod 64 = 36).
+constexpr int XPL_STRIDE = 100;
+
+__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N, int rew, int nhb = 2,
+                                                         int xpl = 0) {
     RolloutLds2 r;
+    r.xpl = xpl;
     r.ldo = L.Dob + 4;
     r.ldh = L.H + 4;
     int64_t o = 0;
@@ -801,7 +809,7 @@ __host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, i
     const int64_t nobs = (int64_t)rows * r.ldo, nhx = nhb == 1 ? (int64_t)rows16 * r.ldh : 0;
     r.obs = ro_take(o, nobs > nhx ? nobs : nhx);
     r.avail = ro_take(o, (int64_t)rows * 2);  // uint64 avail mask per agent row
-    r.xb = ro_take(o, (int64_t)rows16 * r.ldh);
+    r.xb = ro_take(o, (int64_t)rows16 * (xpl ? XPL_STRIDE : r.ldh));
     r.hsz = mlg_align4((int64_t)rows * r.ldh);
     r.nhb = nhb;
     r.hb = ro_take(o, nhb * r.hsz);
@@ -810,6 +818,8 @@ __host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, i
     r.pk = ro_take(o, (int64_t)rew * 32);
     r.act = ro_take(o, (int64_t)rew * 32);
     r.am = ro_take(o, 16);
+    r.rms = rows16 + 16;
+    r.rmap = ro_take(o, 8 * r.rms);  // v7: one compact-row map per wave
     r.env = make_env_lds(o, U, N, rew < RE ? rew : RE);
     r.total = o;
     return r;
@@ -923,6 +933,12 @@ __device__ inline StepRows make_rows(const uint32_t* amask, int ebase, int ne, i
 }
 
 // A: fc1 + ReLU for (tile, chunk j) over tiles ti0, ti0 + dt, ...  -> x (compact rows)
+__device__ __forceinline__ unsigned int cvt_pk_bf16(float lo, float hi) {
+    unsigned int r;
+    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+    return r;
+}
+
 template <int H>
 __device__ inline void ph_fc1(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* prev,
                               const StepRows& SR, int j, int ti0, int dt, int t, int lane) {
@@ -990,6 +1006,241 @@ __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, floa
     }
 }
 
+// ---- v7 row map -------------------------------------------------------------------------------------------
+// Compacted agent rows of the step (as StepRows) as an LDS table private to the wave: entry cr = env e << 8 |
+// agent n << 1 | 1 (0 for tile padding). Lanes 0-15 (one per env) scatter their env's living agents after a
+// 16-lane scan of the agent counts; the wave reads its own table back (LDS is in order within a wave), so no
+// workgroup barrier and no SGPR-resident prefix array. Returns the tile count.
+__device__ __forceinline__ int rmap_er(int rm, int N) { return (rm >> 8) * N + ((rm >> 1) & 127); }
+
+__device__ inline int make_rmap(const uint32_t* amask, int* wmap, int lane) {
+    const int l16 = lane & 15;
+    const uint32_t m = amask[l16];
+    int c = __builtin_popcount(m);
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+        const int v = __shfl_up(c, d, 16);
+        if (l16 >= d) c += v;
+    }
+    const int rows = __builtin_amdgcn_readlane(c, 15);
+    if (lane < 16) {
+        int p = c - __builtin_popcount(m);
+        for (uint32_t mm = m; mm; mm &= mm - 1) wmap[p++] = (lane << 8) | (__builtin_ctz(mm) << 1) | 1;
+        wmap[rows + lane] = 0;  // padding rows of the last tile
+    }
+    return (rows + 15) >> 4;
+}
+
+// v7 A: fc1 + ReLU for (tile, chunk j) as ph_fc1 (same fp32 arithmetic), rows from the wave's row map, x stored
+// as three bf16 planes (x = p0 + p1 + p2 exactly) = the GRU's B operands, split once here.
+template <int H>
+__device__ inline void ph_fc1_g8(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* rmap, const int* prev,
+                                 int tiles, int j, int ti0, int dt, int t, int lane) {
+    const int col = lane & 15, g = lane >> 4, N = L.N, ldo = lay.ldo, ldh = lay.ldh, KO = L.Dob / 16;
+    const float* lobs = fm + lay.obs;
+    for (int ti = ti0; ti < tiles; ti += dt) {
+        int zero = 0;
+        asm volatile("" : "+s"(zero));
+        const int cr = ti * 16 + col;
+        const int rm = rmap[cr];
+        const bool valid = rm & 1;
+        const int n = (rm >> 1) & 127, er = rmap_er(rm, N);
+        floatx4 acc = ld4(fm + lay.b1 + zero + j * 16 + 4 * g);
+        const int pa = (valid && t > 0) ? prev[er] : -1;
+        if (L.last_action && pa >= 0) acc += ld4(fm + lay.w1a + pa * ldh + j * 16 + 4 * g);
+        if (L.agent_id) acc += ld4(fm + lay.w1n + n * ldh + j * 16 + 4 * g);
+        const float* orow = lobs + er * ldo + 4 * g;
+        const float* wrow = fm + lay.w1o + zero + (j * 16 + col) * ldo + 4 * g;
+        for (int kc = 0; kc < KO; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), ld4(orow + kc * 16), acc);
+        unsigned int* xr = reinterpret_cast<unsigned int*>(fm + lay.xb + cr * XPL_STRIDE) + (j * 16 + 4 * g) / 2;
+        float v[4] = {fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f), fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f)};
+#pragma unroll
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            const unsigned int a = cvt_pk_bf16(v[0], v[1]), b = cvt_pk_bf16(v[2], v[3]);
+            *reinterpret_cast<uint2*>(xr + lvl * 32) = make_uint2(a, b);
+            if (lvl < 2) {
+                v[0] -= __uint_as_float(a << 16);
+                v[1] -= __uint_as_float(a & 0xFFFF0000u);
+                v[2] -= __uint_as_float(b << 16);
+                v[3] -= __uint_as_float(b & 0xFFFF0000u);
+            }
+        }
+    }
+}
+
+// ---- v7 GRU: fp32 products emulated on the bf16 matrix cores (split-bf16 "bf16x6") -------------------------
+// Every fp32 operand a is split into three bf16 pieces a = a0 + a1 + a2 (round to nearest each; the sum is
+// exact: a0 holds the top 8 significant bits, a1 the next 8, a2 the rest, which fits a bf16), and a product
+// a*b is summed as the six partial products with i + j <= 2 (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0) in fp32 MFMA
+// accumulators. The three dropped terms are below 2^-24 of |a b| (a1b2, a2b1: ~2^-26; a2b2: ~2^-34), so each
+// product carries fp32-class error, from fp32 operands, in 6 x 16 = 96 matrix-core cycles per 16x16x32 step
+// instead of 8 x 32 = 256 for v_mfma_f32_16x16x4_f32 (MI355X_MICROARCH.md cycle table). Accumulation is fp32
+// inside the MFMA, in a different order than the v1/v2 fmaf chains: v7 results equal v2's to fp32 rounding,
+// not bit for bit.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+    bf16x8 p[3];
+};
+
+// 8 fp32 -> three bf16x8 pieces (element j of every piece belongs to input j).
+__device__ __forceinline__ Split3 split3(floatx4 a, floatx4 b) {
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    Split3 s;
+#ifdef MLG_G8_NOSPLIT  // timing ablation only: one conversion, copied to all pieces
+    {
+        u32x4 w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
+        s.p[0] = s.p[1] = s.p[2] = __builtin_bit_cast(bf16x8, w);
+        return s;
+    }
+#endif
+#pragma unroll
+    for (int lvl = 0; lvl < 3; ++lvl) {
+        u32x4 w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned int pk = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
+            w[q] = pk;
+            if (lvl < 2) {  // remainders (exact in fp32)
+                v[2 * q] -= __uint_as_float(pk << 16);
+                v[2 * q + 1] -= __uint_as_float(pk & 0xFFFF0000u);
+            }
+        }
+        s.p[lvl] = __builtin_bit_cast(bf16x8, w);
+    }
+    return s;
+}
+
+__device__ __forceinline__ floatx4 mfma_bf16(bf16x8 a, bf16x8 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc += A . B over one 32-wide K step with the six partial products (small terms first).
+__device__ __forceinline__ floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 c) {
+#ifdef MLG_G8_P1  // timing ablation only: the leading product alone
+    return mfma_bf16(a.p[0], b.p[0], c);
+#endif
+    c = mfma_bf16(a.p[2], b.p[0], c);
+    c = mfma_bf16(a.p[1], b.p[1], c);
+    c = mfma_bf16(a.p[0], b.p[2], c);
+    c = mfma_bf16(a.p[1], b.p[0], c);
+    c = mfma_bf16(a.p[0], b.p[1], c);
+    c = mfma_bf16(a.p[0], b.p[0], c);
+    return c;
+}
+
+// Wave w owns hidden features 8w .. 8w+7 (H = 64, 8 waves): three 16-row A blocks per 32-wide K step,
+//   rz_i = [W_ir ; W_iz] (rows 0-7 r, 8-15 z of its features)   with B = x
+//   rz_h = [W_hr ; W_hz]                                         with B = h   (same accumulator rows)
+//   n    = [W_in ; W_hn]  with B = x (rows 0-7 used) and with B = h (rows 8-15 used)
+// so each weight is held once in the workgroup (72 VGPRs of bf16 pieces, v2: 96 VGPRs of fp32, every chunk
+// twice). Gate pre-activations of one (feature, agent row) end up split over lanes l and l + 32; one
+// permlane32_swap per register pair gives each lane two complete features.
+struct GruG8 {
+    Split3 rzi[2], rzh[2], n[2];
+    int rz_bias, in_bias, hn_bias;  // LDS float indices of this lane's 4 bias rows
+};
+
+__device__ inline void load_gru_g8(GruG8& W, const float* __restrict__ P, const AgentLayout& L, const RolloutLds2& lay,
+                                   int w, int lane) {
+    const int H = L.H, row = lane & 15, g = lane >> 4, f = 8 * w + (row & 7), hi = row >> 3;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int k = 32 * kk + 8 * g;
+        const float* ri = P + L.wih + (int64_t)(hi * H + f) * H + k;        // r (hi = 0) / z (hi = 1) row of W_ih
+        const float* rh = P + L.whh + (int64_t)(hi * H + f) * H + k;
+        const float* rn = P + (hi ? L.whh : L.wih) + (int64_t)(2 * H + f) * H + k;  // W_in (rows 0-7) / W_hn (8-15)
+        W.rzi[kk] = split3(ld4(ri), ld4(ri + 4));
+        W.rzh[kk] = split3(ld4(rh), ld4(rh + 4));
+        W.n[kk] = split3(ld4(rn), ld4(rn + 4));
+    }
+    // accumulator rows 4g .. 4g+3: g = 0, 1 -> r / W_in of features 8w + 4g ..; g = 2, 3 -> z / W_hn of 8w + 4(g-2) ..
+    const int fo = 8 * w + 4 * (g & 1);
+    W.rz_bias = lay.gb + (g < 2 ? fo : H + fo);
+    W.in_bias = lay.gb + 2 * H + fo;
+    W.hn_bias = lay.gb + 3 * H + fo;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            asm volatile("" : "+v"(W.rzi[kk].p[q]), "+v"(W.rzh[kk].p[q]), "+v"(W.n[kk].p[q]));
+}
+
+// Gates of v7: hardware exp / reciprocal (v_exp_f32, v_rcp_f32; ~1 ulp each) -- v7 is fp32-class, not bit-equal
+// to v2, so the ~70-instruction libm expf / tanhf / IEEE division are not needed; tanh(x) = 2 sigmoid(2x) - 1.
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float fast_tanh(float x) { return 2.f * fast_sigmoid(2.f * x) - 1.f; }
+
+// B: GRU cell of every tile for the wave's 8 features -> h' (env-row hidden state). x comes as bf16 planes from
+// fc1 (split once), h is split here; the compact-row -> env-row map was stored by fc1.
+template <int H>
+__device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* fm, const int* rmap, const float* hc,
+                                 float* hn, int tiles, int N, int w, int lane) {
+    const int col = lane & 15, g = lane >> 4, ldh = lay.ldh;
+    const bool upper = lane >= 32;
+    // this lane's two output features after the exchange: lower lanes 8w+4g+{0,1}, upper 8w+4(g-2)+2+{0,1}
+    const int fo = 8 * w + 4 * (g & 1) + (upper ? 2 : 0);
+    for (int ti = 0; ti < tiles; ++ti) {
+        const int cr = ti * 16 + col;
+        const int rm = rmap[cr];
+        const bool valid = rm & 1;
+        const int er = rmap_er(rm, N);
+        const bf16x8* xp = reinterpret_cast<const bf16x8*>(fm + lay.xb + (int64_t)cr * XPL_STRIDE) + g;
+        const float* hr = hc + (int64_t)er * ldh + 8 * g;
+        floatx4 arz = ld4(fm + W.rz_bias), arzh = floatx4{0.f, 0.f, 0.f, 0.f};
+        floatx4 anx = ld4(fm + W.in_bias), anh = ld4(fm + W.hn_bias);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            Split3 xs;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) xs.p[p] = xp[p * 8 + 4 * kk];  // plane p: +128 B; K step kk: +64 B
+            const Split3 hs = split3(ld4(hr + 32 * kk), ld4(hr + 32 * kk + 4));
+            arz = mfma_x6(W.rzi[kk], xs, arz);
+            anx = mfma_x6(W.n[kk], xs, anx);
+            arzh = mfma_x6(W.rzh[kk], hs, arzh);
+            anh = mfma_x6(W.n[kk], hs, anh);
+        }
+        arz += arzh;
+        // lanes l < 32 hold r (rows 4g..) and W_in x; lanes l + 32 hold z and W_hn h of the same features
+        float r0, r1, z0, z1;
+        {
+            auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(arz[0]), __float_as_uint(arz[2]), false, false);
+            auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(arz[1]), __float_as_uint(arz[3]), false, false);
+            r0 = __uint_as_float(s0[0]);
+            z0 = __uint_as_float(s0[1]);
+            r1 = __uint_as_float(s1[0]);
+            z1 = __uint_as_float(s1[1]);
+        }
+        float ni0, ni1, nh0, nh1;
+        {
+            auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(anh[0]), __float_as_uint(anx[2]), false, false);
+            auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(anh[1]), __float_as_uint(anx[3]), false, false);
+            // lower: own anx[0..1] = W_in x, received (in the anx[2..3] slot) W_hn h; upper: received W_in x in the
+            // anh[0..1] slot, own anh[2..3] = W_hn h
+            ni0 = upper ? __uint_as_float(s0[0]) : anx[0];
+            ni1 = upper ? __uint_as_float(s1[0]) : anx[1];
+            nh0 = upper ? anh[2] : __uint_as_float(s0[1]);
+            nh1 = upper ? anh[3] : __uint_as_float(s1[1]);
+        }
+        const float2 ho = *reinterpret_cast<const float2*>(hc + (int64_t)er * ldh + fo);
+        float2 hv;
+        {
+            const float rg = fast_sigmoid(r0), zg = fast_sigmoid(z0);
+            const float ng = fast_tanh(ni0 + rg * nh0);
+            hv.x = ng + zg * (ho.x - ng);
+        }
+        {
+            const float rg = fast_sigmoid(r1), zg = fast_sigmoid(z1);
+            const float ng = fast_tanh(ni1 + rg * nh1);
+            hv.y = ng + zg * (ho.y - ng);
+        }
+        if (valid) *reinterpret_cast<float2*>(hn + (int64_t)er * ldh + fo) = hv;
+    }
+}
+
 // C: fc2 + masked argmax + epsilon-greedy per tile; records the actions (batch + LDS pending actions).
 // CX: h' is read from the compact-row buffer hn and the tile's valid rows are stored to the env rows of hstore.
 template <int H, bool CX = false>
@@ -1045,6 +1296,70 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
                     }
                 }
             }
+            R.pact[e * N + n] = act;
+            const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
+            bt.actions[bt_off] = act;
+            if (!bt.full_write) bt.actions_onehot[bt_off * A + act] = 1.0f;
+        }
+    }
+}
+
+// v7 C: fc2 + masked argmax + epsilon-greedy per tile, rows from the fc1 row map. The epsilon draws do not depend
+// on Q, so they are made before the fc2 chain (their latency overlaps the MFMAs), and fc2 accumulates the four
+// 16-wide K chunks in separate chains (fp32-class like the rest of v7; same selection rule as ph_fc2).
+template <int H>
+__device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, const RolloutLds2& lay, float* fm,
+                                 const int* rmap, const RoEnv& R, const MlgBatch& bt, const float* hn, int tiles, int ti0,
+                                 int dt, int e0, int t, float eps, int test_mode, int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4, N = L.N, ldh = lay.ldh, A = spec.n_actions, n_at = L.Ap / 16;
+    const uint64_t* lavm = reinterpret_cast<const uint64_t*>(fm + lay.avail);
+    for (int ti = ti0; ti < tiles; ti += dt) {
+        int zero = 0;
+        asm volatile("" : "+s"(zero));
+        const int cr = ti * 16 + col;
+        const int rm = rmap[cr];
+        const bool valid = rm & 1;
+        const int e = rm >> 8, n = (rm >> 1) & 127, er = e * N + n;
+        const uint64_t avm = lavm[er];
+        int ract = -1;  // epsilon-greedy (action_selectors.py:44-62), counter RNG of spec §3.7: random action or -1
+        if (!test_mode && eps > 0.f && valid && g == 0) {
+            const uint64_t key = mlg_env_key(spec.seed, e0 + e);
+            const uint64_t r1 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n));
+            if (mlg_u01(r1) < eps) {
+                const uint64_t r2 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)n));
+                const int na = __popcll(avm);  // random_available on the mask: k-th available action
+                ract = 0;
+                if (na > 0) {
+                    const int k = (int)(((r2 >> 40) * (uint64_t)na) >> 24);
+                    uint64_t m = avm;
+                    for (int i = 0; i < k; ++i) m &= m - 1;
+                    ract = __ffsll((long long)m) - 1;
+                }
+            }
+        }
+        const float* hr = hn + (int64_t)er * ldh + 4 * g;
+        ArgmaxState as{-INFINITY, 1 << 30};
+        for (int at = 0; at < n_at; ++at) {
+            const float* w2r = fm + lay.w2 + zero + (int64_t)(at * 16 + col) * ldh + 4 * g;
+            floatx4 qk[HC];
+#pragma unroll
+            for (int kc = 0; kc < HC; ++kc)
+                qk[kc] = mfma_chunk(ld4(w2r + kc * 16), ld4(hr + kc * 16), floatx4{0.f, 0.f, 0.f, 0.f});
+            floatx4 q = ld4(fm + lay.b2 + zero + at * 16 + 4 * g);
+#pragma unroll
+            for (int kc = 0; kc < HC; ++kc) q += qk[kc];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // masked argmax (argmax_accumulate on the bit mask)
+                const int a = at * 16 + 4 * g + r;
+                if (a >= A) continue;
+                const float v = ((avm >> a) & 1ull) ? q[r] : -INFINITY;
+                if (amax_better(v, a, as.bv, as.bi)) { as.bv = v; as.bi = a; }
+            }
+        }
+        int act = argmax_reduce(as);
+        if (valid && g == 0) {
+            if (ract >= 0) act = ract;
             R.pact[e * N + n] = act;
             const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
             bt.actions[bt_off] = act;
@@ -1250,9 +1565,16 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
     sp.mark(6);
     // observation at t + 1 (incl. envs that just terminated)
     v2_pair_pass(C.M, U, hl, E.u, C.pk + E.e * 32);
+#ifdef MLG_DUP_PAIR
+    v2_pair_pass(C.M, U, hl, E.u, C.pk + E.e * 32);
+#endif
     sp.mark(7);
     v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
                C.inv_p, sp);
+#ifdef MLG_DUP_OBS
+    v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
+               C.inv_p, sp);
+#endif
 }
 
 // Full-write mode: a finished env's half-wave zeroes a few more steps of its slot's tail.
@@ -1307,7 +1629,7 @@ __device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2&
 // ================================================================================================
 // v2 kernel: 8 waves, 16 envs; every wave does agent work (chunk j = w % HC of tiles w / HC, ...) and then
 // the env step of envs 2w, 2w + 1. Barriers per step: A|B, B|C, C|env, env|A.
-template <int H>
+template <int H, bool G8 = false>
 __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
                                                            const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
                                                            float eps, int test_mode, RolloutLds2 lay) {
@@ -1321,8 +1643,12 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
     EnvLane E;
     env_lane_reset(C, st, E, wave * 2 + (lane >> 5), e0, hl);
     const int j = wave % HC, gi = wave / HC;
-    GruChunk<H> W;
-    load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
+    GruChunk<G8 ? 16 : H> W;  // v7 (G8) holds the split-bf16 weights of its 8 features instead
+    GruG8 W8;
+    if constexpr (G8)
+        load_gru_g8(W8, P, L, lay, wave, lane);
+    else
+        load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
     __syncthreads();
     Stamps sp;
     sp.init();
@@ -1330,17 +1656,50 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
     for (int t = 0; t < T1; ++t) {
         const uint32_t run = (uint32_t)__ballot(lane < REW && C.R.status[lane & (REW - 1)] < 2);
         if (run == 0) break;
-        const StepRows SR = make_rows(C.amask, 0, 16, lane);
-        rows_issued += SR.tiles * 16;
         const float* hc = fm + lay.hb + (t & 1) * lay.hsz;
         float* hn = fm + lay.hb + ((t & 1) ^ 1) * lay.hsz;
-        ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
+        StepRows SR;
+        int tiles;
+        int* wmap = smem + lay.rmap + wave * lay.rms;
+        if constexpr (G8) {
+            tiles = make_rmap(C.amask, wmap, lane);
+            ph_fc1_g8<H>(L, lay, fm, wmap, C.R.prev, tiles, j, gi, G, t, lane);
+#ifdef MLG_DUP_FC1  // timing ablation only: the phase twice (idempotent)
+            ph_fc1_g8<H>(L, lay, fm, wmap, C.R.prev, tiles, j, gi, G, t, lane);
+#endif
+        } else {
+            SR = make_rows(C.amask, 0, 16, lane);
+            tiles = SR.tiles;
+            ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
+#ifdef MLG_DUP_FC1
+            ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
+#endif
+        }
+        rows_issued += tiles * 16;
         sp.mark(0);
         __syncthreads();
-        ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
+        if constexpr (G8)
+            ph_gru_g8<H>(W8, lay, fm, wmap, hc, hn, tiles, N, wave, lane);
+        else
+            ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
+#ifdef MLG_DUP_GRU
+        if constexpr (G8)
+            ph_gru_g8<H>(W8, lay, fm, wmap, hc, hn, tiles, N, wave, lane);
+        else
+            ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
+#endif
         sp.mark(1);
         __syncthreads();
-        ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
+        if constexpr (G8)
+            ph_fc2_g8<H>(spec, L, lay, fm, wmap, C.R, bt, hn, tiles, wave, NW, e0, t, eps, test_mode, lane);
+        else
+            ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
+#ifdef MLG_DUP_FC2
+        if constexpr (G8)
+            ph_fc2_g8<H>(spec, L, lay, fm, wmap, C.R, bt, hn, tiles, wave, NW, e0, t, eps, test_mode, lane);
+        else
+            ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
+#endif
         sp.mark(2);
         __syncthreads();
         sp.mark(3);
@@ -1673,7 +2032,9 @@ int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& 
                       const RolloutLds2& lay) {
     const size_t bytes = (size_t)lay.total * 4;
     auto kern = V == 4 ? rollout_v4_kernel<H, 4>
-                       : (V == 5 ? rollout_v4_kernel<H, 8> : (V == 6 ? rollout_v6_kernel<H> : rollout_v2_kernel<H>));
+                       : (V == 5 ? rollout_v4_kernel<H, 8>
+                                 : (V == 6 ? rollout_v6_kernel<H>
+                                           : (V == 7 ? rollout_v2_kernel<64, true> : rollout_v2_kernel<H>)));
     const int threads = V == 4 ? 512 : (V == 5 ? 768 : (V == 6 ? 256 : 512));
     const int rew = V == 6 ? 8 : 16;
     if (bytes > 64 * 1024) {
@@ -1698,6 +2059,11 @@ int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay)
     }
     *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
     if (lay->total * 4 > LDS_LIMIT_BYTES) return 1;
+    if (want == 7 && L.H == 64) {
+        *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16, 2, 1);
+        if (lay->total * 4 <= LDS_LIMIT_BYTES) return 7;
+        *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
+    }
     return (want == 4 || want == 5) ? want : 2;
 }
 
@@ -1874,6 +2240,7 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
         if (variant == 4) MLG_V(4);
         else if (variant == 5) MLG_V(5);
         else if (variant == 6) MLG_V(6);
+        else if (variant == 7) rc = launch_rollout_v2<64, 7>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
         else MLG_V(2);
 #undef MLG_V
         if (rc) return rc;

@@ -36,7 +36,7 @@ for k in os.environ.get("MLG_BENCH_KERNELS", "v2").split(","):
         stepper.envs = VecEnvState(stepper.spec, B, "cuda")
         stepper.t_env = 10 ** 6
         stepper.timing = []
-        stepper.run(test_mode=False)
+        stepper.run(test_mode=bool(int(os.environ.get("TEST_MODE", "0"))))
         torch.cuda.synchronize()
         if r >= 2:
             ms.append(stepper.timing[0][0].elapsed_time(stepper.timing[0][1]))

@@ -282,7 +282,7 @@ def test_rollout_headline_config_properties(device):
             np.testing.assert_array_equal(nb["obs"][b, t + 1], r.obs())
 
 
-@pytest.mark.parametrize("kernel", ["v6", "v5", "v4", "v2", "v1"])
+@pytest.mark.parametrize("kernel", ["v7", "v6", "v5", "v4", "v2", "v1"])
 def test_rollout_ring_mode_zero_copy_insert(device, kernel, monkeypatch):
     """Train-mode rollouts written straight into the replay ring (full-write mode, wrap-around, garbage in the
     slots beforehand) equal the ordinary zero-initialised EpisodeBatch bit for bit, and the buffer indices
@@ -339,3 +339,62 @@ def test_rollout_v2_equals_v1(device, plan, kernel, monkeypatch):
         assert torch.equal(v, out[kernel][0][kk]), kk
     for kk, v in out["v1"][1].items():
         assert torch.equal(v, out[kernel][1][kk]), kk
+
+
+def test_rollout_second_run_before_insert_leaves_ring_episodes(device):
+    """A second train-mode run before insert_episode_batch goes to a fresh batch: the first run's episodes,
+    written in place into the ring, are not overwritten (the reference leaves the buffer untouched until insert)."""
+    from maleague.components.replay_buffer import ReplayBuffer, RingEpisodeBatch
+    stepper, mac, args = _build_stepper(device, plan="medium_1h_4t", B=48, episode_limit=30, seed=2)
+    info = stepper.get_env_info()
+    scheme, groups, preprocess = scheme_for(info, torch)
+    ring = ReplayBuffer(scheme, groups, 100, 31, preprocess=preprocess, device=device)
+    assert stepper.attach_replay(ring)
+    stepper.t_env = 20000
+    b1, _ = stepper.run(test_mode=False)
+    snap = {k: v.clone() for k, v in b1.data.transition_data.items()}
+    b2, _ = stepper.run(test_mode=False)
+    assert isinstance(b1, RingEpisodeBatch) and not isinstance(b2, RingEpisodeBatch)
+    for k, v in snap.items():
+        assert torch.equal(b1[k], v), k
+    assert not torch.equal(b1["actions"], b2["actions"])
+    ring.insert_episode_batch(b1)
+    ring.insert_episode_batch(b2)
+    for k, v in snap.items():
+        assert torch.equal(ring[k][:48], v), k
+        assert torch.equal(ring[k][48:96], b2[k]), k
+
+
+@pytest.mark.parametrize("plan", ["medium_1h_4t", "medium", "small"])
+def test_rollout_v7_split_bf16_gru_matches_fp32(device, plan, monkeypatch):
+    """v7: the GRU products run on the bf16 matrix cores as split-bf16 fp32 emulation (three bf16 pieces per
+    operand, six partial products, fp32 accumulation). Along v7's own recorded trajectory (test mode, epsilon 0)
+    the fp32 oracle DRQN (oracle/learner_ref.py, drqn_agent.py:29-35) must rate every recorded action as an
+    available argmax up to a 1e-5 tie, and v7 must reproduce v2's episodes bit for bit except where a near-tie
+    of the Q values flips an argmax (env transitions of v7 are the v2 env code)."""
+    from maleague.envs.teams_env import VecEnvState
+    B, TL = 100, 60
+    stepper, mac, args = _build_stepper(device, plan=plan, B=B, episode_limit=TL, seed=3)
+    out = {}
+    for k in ("v2", "v7"):
+        monkeypatch.setenv("MLG_ROLLOUT_KERNEL", k)
+        stepper.envs = VecEnvState(stepper.spec, B, device)
+        b, _ = stepper.run(test_mode=True)
+        out[k] = (np_batch(b), stepper.last_run["ep_len"].numpy().copy())
+    nb, L = out["v7"]
+    tb = {kk: torch.from_numpy(v) for kk, v in nb.items()}
+    p = {kk: v.detach().cpu() for kk, v in mac.agent.state_dict().items()}
+    q, _ = LR.mac_unroll(p, tb, args.n_agents, T=TL + 1)
+    q = q.numpy()
+    av = nb["avail_actions"].astype(bool)
+    worst = 0.0
+    for b_ in range(B):
+        for t in range(int(L[b_]) + 1):  # every step incl. the final action after termination
+            qm = np.where(av[b_, t], q[b_, t], -np.inf)
+            best = qm.max(axis=-1)
+            chosen = np.take_along_axis(qm, nb["actions"][b_, t], axis=-1)[:, 0]
+            assert np.isfinite(chosen).all(), (b_, t)  # chosen action available
+            worst = max(worst, float((best - chosen).max()))
+    assert worst <= 1e-5, worst
+    same = [all(np.array_equal(out["v2"][0][kk][b_], nb[kk][b_]) for kk in nb) for b_ in range(B)]
+    assert np.mean(same) >= 0.9, np.mean(same)
