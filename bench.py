@@ -193,7 +193,7 @@ def main():
     issued = fl / (sides * N) * rows_per_launch / avg_kernel_s if mode == "ai" else None
     traffic = None
     kc1 = (info.get("entity_shape", 0) + A + 15) // 16 if mode == "refil" else 0
-    kernel = {"ai": "rollout_v2_kernel<64>", "league": "rollout_sp_kernel<64>",
+    kernel = {"ai": "rollout_v2_kernel<64, true>", "league": "rollout_sp_kernel<64>",
               "refil": f"refil_rollout_kernel<{kc1}>"}[mode]
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:

@@ -1361,9 +1361,11 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
         if (valid && g == 0) {
             if (ract >= 0) act = ract;
             R.pact[e * N + n] = act;
+#ifndef MLG_ABL_FC2_NOSTORE  // timing ablation only
             const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
             bt.actions[bt_off] = act;
             if (!bt.full_write) bt.actions_onehot[bt_off * A + act] = 1.0f;
+#endif
         }
     }
 }
@@ -2047,11 +2049,11 @@ int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& 
     return 0;
 }
 
-// v2 when the shape allows it (H 32/64, U <= 32, LDS fits), else v1. MLG_ROLLOUT_KERNEL=v1|v2|v4 forces a
-// variant (v4 / v5: the wave-specialised kernel with 4 / 8 agent waves).
+// v7 for H = 64 and v2 for H = 32 when the shape allows it (U <= 32, LDS fits), else v1. MLG_ROLLOUT_KERNEL=
+// v1|v2|v4|v5|v6|v7 forces a variant (v4 / v5: the wave-specialised kernel with 4 / 8 agent waves).
 int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay) {
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
-    const int want = (k && k[0] == 'v') ? k[1] - '0' : 2;
+    const int want = (k && k[0] == 'v') ? k[1] - '0' : (L.H == 64 ? 7 : 2);
     if (want == 1 || (L.H != 64 && L.H != 32) || spec.U > 32) return 1;
     if (want == 6) {  // two workgroups per CU need the layout to fit half the LDS
         *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 8, 1);

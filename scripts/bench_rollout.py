@@ -29,7 +29,7 @@ torch.manual_seed(0)
 mac = BasicMAC(proto.scheme, groups, args)
 stepper.initialize(scheme, groups, preprocess, mac)
 out = {}
-for k in os.environ.get("MLG_BENCH_KERNELS", "v2").split(","):
+for k in os.environ.get("MLG_BENCH_KERNELS", "v7").split(","):
     os.environ["MLG_ROLLOUT_KERNEL"] = k
     ms = []
     for r in range(REPS + 2):

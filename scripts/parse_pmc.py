@@ -15,8 +15,8 @@ for f in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recu
             if "rollout" not in k:
                 continue
             name = row.get("Counter_Name")
-            tot[(k[:60], name)] += float(row.get("Counter_Value", 0))
-            disp[(k[:60], name)].add(row.get("Dispatch_Id"))
+            tot[(k[:75], name)] += float(row.get("Counter_Value", 0))
+            disp[(k[:75], name)].add(row.get("Dispatch_Id"))
 for (k, name), v in sorted(tot.items()):
     n = max(1, len(disp[(k, name)]))
-    print(f"{k:60s} {name:28s} per_dispatch={v / n:16.0f}  dispatches={n}")
+    print(f"{k:75s} {name:28s} per_dispatch={v / n:16.0f}  dispatches={n}")
