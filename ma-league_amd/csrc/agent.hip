@@ -9,41 +9,7 @@ namespace {
 __global__ void pack_agent_kernel(AgentLayout L, MlgAgentParams p, float* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L.total) return;
-    const int H = L.H;
-    float v = 0.f;
-    if (i < L.w1o) {  // dense fc1 [H][Dip]
-        const int64_t r = i / L.Dip, c = i % L.Dip;
-        v = c < L.d_in ? p.fc1_w[r * L.d_in + c] : 0.f;
-    } else if (i < L.w1a) {  // obs columns [H][Dob]
-        const int64_t k = i - L.w1o, r = k / L.Dob, c = k % L.Dob;
-        v = c < L.d_obs ? p.fc1_w[r * L.d_in + c] : 0.f;
-    } else if (i < L.w1n) {  // last-action columns transposed [A][H]
-        const int64_t k = i - L.w1a, a = k / H, r = k % H;
-        v = p.fc1_w[r * L.d_in + L.d_obs + a];
-    } else if (i < L.b1) {  // agent-id columns transposed [N][H]
-        const int64_t k = i - L.w1n, n = k / H, r = k % H;
-        v = p.fc1_w[r * L.d_in + L.d_obs + (L.last_action ? L.A : 0) + n];
-    } else if (i < L.wih) {
-        v = p.fc1_b[i - L.b1];
-    } else if (i < L.bih) {
-        v = p.w_ih[i - L.wih];
-    } else if (i < L.whh) {
-        v = p.b_ih[i - L.bih];
-    } else if (i < L.bhh) {
-        v = p.w_hh[i - L.whh];
-    } else if (i < L.brz) {
-        v = p.b_hh[i - L.bhh];
-    } else if (i < L.w2) {
-        const int64_t k = i - L.brz;
-        v = p.b_ih[k] + p.b_hh[k];
-    } else if (i < L.b2) {
-        const int64_t k = i - L.w2, r = k / H, c = k % H;
-        v = r < L.A ? p.fc2_w[r * H + c] : 0.f;
-    } else {
-        const int64_t k = i - L.b2;
-        v = k < L.Ap && k < L.A ? p.fc2_b[k] : 0.f;
-    }
-    out[i] = v;
+    out[i] = pack_agent_elem(L, p, i);
 }
 
 // DRQN forward over R rows; one wave per 16-row tile.  DENSE: inputs[R][d_in].

@@ -14,6 +14,8 @@
 //               (deterministic slab reduction; MFMA with the row index as K)
 //   finish      loss/stat reduction, clip_grad_norm_(10), RMSprop step                       (:104-105, learner.py:25-31)
 // Tensors saved for backward are t-major: [T][R][F] with R = B * N agent rows (r = b * N + n).
+#include <algorithm>
+
 #include "agent_device.h"
 #include "mlg_host.h"
 #include "wgrad_device.h"
@@ -113,18 +115,8 @@ __host__ __device__ inline int64_t a4(int64_t v) { return mlg_align4(v); }
 
 // ================================================================================================
 // packing
-__global__ void transpose_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols) {
-    // dst[c][r] = src[r][c]
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)rows * cols) return;
-    const int r = (int)(i / cols), c = (int)(i % cols);
-    dst[(int64_t)c * rows + r] = src[i];
-}
-
-__global__ void pack_mixer_kernel(MixPack mp, MixOffs mo, const float* __restrict__ P, float* __restrict__ out, int N,
-                                  int S, int E, int HE) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= mp.total) return;
+__device__ __forceinline__ float pack_mixer_elem(const MixPack& mp, const MixOffs& mo, const float* __restrict__ P,
+                                                 int64_t i, int S, int E, int HE) {
     float v = 0.f;
     if (i < mp.mb1) {
         const int r = (int)(i / mp.Sp), c = (int)(i % mp.Sp);
@@ -154,7 +146,7 @@ __global__ void pack_mixer_kernel(MixPack mp, MixOffs mo, const float* __restric
     } else if (i < mp.bv2p + 16) {
         if (i == mp.bv2p) v = P[mo.v2b];
     }
-    out[i] = v;
+    return v;
 }
 
 // episode b of the batch -> its slot in the tensors (sampled view of the replay buffer: rows[b])
@@ -169,8 +161,8 @@ __device__ __forceinline__ float mask_at(const MlgBatch& bt, int b, int t) {
     return m;
 }
 
-__global__ void mask_sum_kernel(MlgBatch bt, int B, int T, float* __restrict__ msum) {
-    __shared__ float red[1024];
+// One 1024-thread block: sum of the mask and max_t_filled (msum[0], msum[1]).
+__device__ void mask_sum_block(const MlgBatch& bt, int B, int T, float* __restrict__ msum, float* red) {
     // msum[1] = max_t_filled (the reference's truncation, ma_experiment.py:235-239): the learner uses transitions
     // t < max_t_filled - 1 only; the sequential kernels stop there and the per-t kernels skip the steps beyond
     int mx = 0;  // a wave per episode: filled steps counted with ballots
@@ -203,6 +195,59 @@ __global__ void mask_sum_kernel(MlgBatch bt, int B, int T, float* __restrict__ m
     if (threadIdx.x == 0) {
         msum[0] = red[0];
         msum[1] = (float)Te;
+    }
+}
+
+// Fused learner prologue (one launch instead of eight): block 0 sums the mask (mask_sum_block); the other blocks
+// pack the online / target agent weights (pack_agent_elem), transpose W_ih (dX pass), pack the online / target
+// QMixer hypernets (pack_mixer_elem) and zero the sparse delta buffers d2 and dq.
+struct PrepJob {
+    AgentLayout L;
+    MlgAgentParams ap_on, ap_tg;
+    float *p_on, *p_tg;
+    const float* wih;  // [3H][H] -> wihT [H][3H]
+    float* wihT;
+    int rows3, cols;
+    MixPack mp;
+    MixOffs mo;
+    const float *mix_src_on, *mix_src_tg;
+    float *mix_on, *mix_tg;
+    int N, S, E, HE, mixer;
+    float *d2, *dq;
+    int64_t n_d2, n_dq;
+    MlgBatch bt;
+    int B, T;
+    float* msum;
+};
+
+__global__ void __launch_bounds__(1024) prep_kernel(PrepJob J) {
+    __shared__ float red[1024];
+    if (blockIdx.x == 0) {
+        mask_sum_block(J.bt, J.B, J.T, J.msum, red);
+        return;
+    }
+    const int64_t na = J.L.total, nt = (int64_t)J.rows3 * J.cols, nm = J.mixer == 2 ? J.mp.total : 0;
+    const int64_t total = 2 * na + nt + 2 * nm + J.n_d2 + J.n_dq;
+    for (int64_t i = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)(gridDim.x - 1) * blockDim.x) {
+        int64_t k = i;
+        if (k < na) { J.p_on[k] = pack_agent_elem(J.L, J.ap_on, k); continue; }
+        k -= na;
+        if (k < na) { J.p_tg[k] = pack_agent_elem(J.L, J.ap_tg, k); continue; }
+        k -= na;
+        if (k < nt) {  // wihT[c][r] = wih[r][c]
+            const int r = (int)(k / J.cols), c = (int)(k % J.cols);
+            J.wihT[(int64_t)c * J.rows3 + r] = J.wih[k];
+            continue;
+        }
+        k -= nt;
+        if (k < nm) { J.mix_on[k] = pack_mixer_elem(J.mp, J.mo, J.mix_src_on, k, J.S, J.E, J.HE); continue; }
+        k -= nm;
+        if (k < nm) { J.mix_tg[k] = pack_mixer_elem(J.mp, J.mo, J.mix_src_tg, k, J.S, J.E, J.HE); continue; }
+        k -= nm;
+        if (k < J.n_d2) { J.d2[k] = 0.f; continue; }
+        k -= J.n_d2;
+        J.dq[k] = 0.f;
     }
 }
 
@@ -1250,22 +1295,48 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     const MlgBatch& bt = bufs->batch;
     const float* params = bufs->params;
     const float* tparams = bufs->target_params;
-    // ---- pack ----
-    auto pack_agent = [&](const float* flat, float* out) {
-        MlgAgentDims d{c.d_obs, c.A, c.N, c.H, c.d_in, c.last_action, c.agent_id};
-        MlgAgentParams ap{flat + p.ao.fc1w, flat + p.ao.fc1b, flat + p.ao.wih, flat + p.ao.bih,
-                          flat + p.ao.whh, flat + p.ao.bhh, flat + p.ao.fc2w, flat + p.ao.fc2b};
-        return mlg_pack_agent(&d, &ap, out, s);
+    // ---- fused prologue: pack online / target agent + mixer, W_ih^T, zero d2 / dq, mask sum ----
+    auto agent_ptrs = [&](const float* flat) {
+        return MlgAgentParams{flat + p.ao.fc1w, flat + p.ao.fc1b, flat + p.ao.wih, flat + p.ao.bih,
+                              flat + p.ao.whh, flat + p.ao.bhh, flat + p.ao.fc2w, flat + p.ao.fc2b};
     };
-    if (pack_agent(params, ws + p.w.p_on) || pack_agent(tparams, ws + p.w.p_tg)) return 1;
-    const int n3 = 3 * c.H * c.H;
-    hipLaunchKernelGGL(transpose_kernel, dim3((n3 + 255) / 256), dim3(256), 0, s, params + p.ao.wih, ws + p.w.wihT, 3 * c.H, c.H);
+    PrepJob pj;
+    pj.L = p.L;
+    pj.ap_on = agent_ptrs(params);
+    pj.ap_tg = agent_ptrs(tparams);
+    pj.p_on = ws + p.w.p_on;
+    pj.p_tg = ws + p.w.p_tg;
+    pj.wih = params + p.ao.wih;
+    pj.wihT = ws + p.w.wihT;
+    pj.rows3 = 3 * c.H;
+    pj.cols = c.H;
+    pj.mp = p.mp;
+    pj.mo = p.mo;
+    pj.mix_src_on = params + p.n_agent;
+    pj.mix_src_tg = tparams + p.n_agent;
+    pj.mix_on = ws + p.w.mix_on;
+    pj.mix_tg = ws + p.w.mix_tg;
+    pj.N = c.N;
+    pj.S = c.S;
+    pj.E = c.E;
+    pj.HE = c.HE;
+    pj.mixer = c.mixer;
+    pj.d2 = ws + p.w.d2;  // d2 is sparse: zero it (and dq) every call
+    pj.dq = ws + p.w.dq;
+    pj.n_d2 = (int64_t)c.T * c.R * c.A;
+    pj.n_dq = (int64_t)c.T * c.R;
+    pj.bt = bt;
+    pj.B = c.B;
+    pj.T = c.T;
+    pj.msum = ws + p.w.msum;
+    {
+        const int64_t work = 2 * p.L.total + 3 * (int64_t)c.H * c.H + (c.mixer == 2 ? 2 * p.mp.total : 0) + pj.n_d2 + pj.n_dq;
+        const int blocks = 1 + (int)std::min<int64_t>((work + 1023) / 1024, 512);
+        hipLaunchKernelGGL(prep_kernel, dim3(blocks), dim3(1024), 0, s, pj);
+    }
     MixPtrs Mon{}, Mtg{};
     if (c.mixer == 2) {
         const int64_t g0 = p.n_agent;
-        const int nb = (int)((p.mp.total + 255) / 256);
-        hipLaunchKernelGGL(pack_mixer_kernel, dim3(nb), dim3(256), 0, s, p.mp, p.mo, params + g0, ws + p.w.mix_on, c.N, c.S, c.E, c.HE);
-        hipLaunchKernelGGL(pack_mixer_kernel, dim3(nb), dim3(256), 0, s, p.mp, p.mo, tparams + g0, ws + p.w.mix_tg, c.N, c.S, c.E, c.HE);
         auto ptrs = [&](const float* flat, const float* pk) {
             MixPtrs m;
             m.m1 = pk + p.mp.m1;
@@ -1283,10 +1354,6 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
         Mon = ptrs(params, ws + p.w.mix_on);
         Mtg = ptrs(tparams, ws + p.w.mix_tg);
     }
-    // d2 is sparse: zero it (and dq) every call
-    (void)hipMemsetAsync(ws + p.w.d2, 0, sizeof(float) * (size_t)c.T * c.R * c.A, s);
-    (void)hipMemsetAsync(ws + p.w.dq, 0, sizeof(float) * (size_t)c.T * c.R, s);
-    hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + p.w.msum);
     const int ntiles = (c.R + 15) / 16;
     const int threads = (c.H / 16) * 64;
     hipLaunchKernelGGL((agent_in_kernel<H>), dim3(ntiles, c.T, 2), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
