@@ -22,10 +22,10 @@ struct AgentLayout {
     int32_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;  // 32-bit: fewer SGPRs in kernels
 };
 
-__host__ __device__ inline int64_t mlg_align4(int64_t v) { return (v + 3) & ~int64_t(3); }
+__host__ __device__ constexpr int64_t mlg_align4(int64_t v) { return (v + 3) & ~int64_t(3); }
 
-__host__ __device__ inline AgentLayout make_agent_layout(const MlgAgentDims& d) {
-    AgentLayout L;
+__host__ __device__ constexpr AgentLayout make_agent_layout(const MlgAgentDims& d) {
+    AgentLayout L{};
     L.H = d.hidden;
     L.A = d.n_actions;
     L.Ap = (d.n_actions + 15) / 16 * 16;
@@ -315,7 +315,9 @@ __device__ __forceinline__ int argmax_reduce(ArgmaxState s) {
     for (int m = 16; m <= 32; m <<= 1) {
         const float ov = __shfl_xor(s.bv, m);
         const int oi = __shfl_xor(s.bi, m);
-        if (amax_better(ov, oi, s.bv, s.bi)) { s.bv = ov; s.bi = oi; }
+        const bool take = amax_better(ov, oi, s.bv, s.bi);
+        s.bv = take ? ov : s.bv;
+        s.bi = take ? oi : s.bi;
     }
     return s.bi;
 }

@@ -225,7 +225,8 @@ __device__ __forceinline__ void env_apply_move(int a, int* xu, int* yu) {
 // ------------------------------------------------------------------------------------------------
 // argmax with torch.max semantics on CPU: NaN wins, ties -> lowest index.
 __device__ __forceinline__ bool amax_better(float v, int i, float bv, int bi) {
-    const bool vn = v != v, bn = bv != bv;
-    if (vn || bn) return vn && (!bn || i < bi);
-    return v > bv || (v == bv && i < bi);
+    // branch-free form of: NaN beats any number (lowest index among NaNs), else larger value, ties -> lower index
+    const bool vn = v != v, bn = bv != bv, lower = i < bi;
+    const bool ord = (v > bv) | ((v == bv) & lower);
+    return vn ? (!bn | lower) : (!bn & ord);
 }

@@ -14,6 +14,8 @@
 //   per-env reductions) -> obs/state/avail of t+1 straight into the EpisodeBatch in HBM.
 // Bookkeeping is the reference's intended one: an env that terminates while
 // stepping at t still receives (and records) an action at t+1, then stops.
+#include <cstring>
+
 #include "agent_device.h"
 #include "mlg_host.h"
 
@@ -117,14 +119,14 @@ struct RoEnvLds {
     int32_t spec, x, y, hp, nhp, act, pact, prev, status, stepped, len, episode, ret, slot, list, misc, slot2, ret2;
 };
 
-__host__ __device__ inline int64_t ro_take(int64_t& o, int64_t n) {
+__host__ __device__ constexpr int64_t ro_take(int64_t& o, int64_t n) {
     const int64_t v = o;
     o += mlg_align4(n);
     return v;
 }
 
-__host__ __device__ inline RoEnvLds make_env_lds(int64_t& o, int U, int n_agents, int re = RE) {
-    RoEnvLds r;
+__host__ __device__ constexpr RoEnvLds make_env_lds(int64_t& o, int U, int n_agents, int re = RE) {
+    RoEnvLds r{};
     r.spec = ro_take(o, (int64_t)(sizeof(SpecShared) / 4));
     const int64_t eu = (int64_t)re * U;
     r.x = ro_take(o, eu);
@@ -790,9 +792,9 @@ struct RolloutLds2 {
 // start on distinct bank quads (100 mod 64 = 36).
 constexpr int XPL_STRIDE = 100;
 
-__host__ __device__ inline RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N, int rew, int nhb = 2,
-                                                         int xpl = 0) {
-    RolloutLds2 r;
+__host__ __device__ constexpr RolloutLds2 make_rollout_lds2(const AgentLayout& L, int U, int N, int rew, int nhb = 2,
+                                                            int xpl = 0) {
+    RolloutLds2 r{};
     r.xpl = xpl;
     r.ldo = L.Dob + 4;
     r.ldh = L.H + 4;
@@ -1322,39 +1324,51 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
         const bool valid = rm & 1;
         const int e = rm >> 8, n = (rm >> 1) & 127, er = e * N + n;
         const uint64_t avm = lavm[er];
-        int ract = -1;  // epsilon-greedy (action_selectors.py:44-62), counter RNG of spec §3.7: random action or -1
-        if (!test_mode && eps > 0.f && valid && g == 0) {
-            const uint64_t key = mlg_env_key(spec.seed, e0 + e);
-            const uint64_t r1 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n));
-            if (mlg_u01(r1) < eps) {
-                const uint64_t r2 = mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)n));
-                const int na = __popcll(avm);  // random_available on the mask: k-th available action
-                ract = 0;
-                if (na > 0) {
-                    const int k = (int)(((r2 >> 40) * (uint64_t)na) >> 24);
-                    uint64_t m = avm;
-                    for (int i = 0; i < k; ++i) m &= m - 1;
-                    ract = __ffsll((long long)m) - 1;
-                }
-            }
-        }
-        const float* hr = hn + (int64_t)er * ldh + 4 * g;
+        const float* hr = hn + er * ldh + 4 * g;
         ArgmaxState as{-INFINITY, 1 << 30};
-        for (int at = 0; at < n_at; ++at) {
-            const float* w2r = fm + lay.w2 + zero + (int64_t)(at * 16 + col) * ldh + 4 * g;
-            floatx4 qk[HC];
+        // epsilon-greedy coin (action_selectors.py:44-62, counter RNG of spec §3.7): computed by every lane with no
+        // branch, so it issues between the fc2 MFMAs; only the rare exploring lanes take the branch below
+        const uint64_t key = mlg_env_key(spec.seed, e0 + e);
+        const uint32_t ep = R.episode[e];
+        const bool explore = !test_mode && eps > 0.f &&
+                             mlg_u01(mlg_rng(key, mlg_ctr(ep, (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n))) < eps;
+        auto q_block = [&](int at) {  // Q rows at*16 .. at*16+15 of this lane's agent row; all operands loaded first
+            const float* w2r = fm + lay.w2 + zero + (at * 16 + col) * ldh + 4 * g;
+            floatx4 wk[HC], hk[HC], qk[HC];
 #pragma unroll
-            for (int kc = 0; kc < HC; ++kc)
-                qk[kc] = mfma_chunk(ld4(w2r + kc * 16), ld4(hr + kc * 16), floatx4{0.f, 0.f, 0.f, 0.f});
-            floatx4 q = ld4(fm + lay.b2 + zero + at * 16 + 4 * g);
+            for (int kc = 0; kc < HC; ++kc) {
+                wk[kc] = ld4(w2r + kc * 16);
+                hk[kc] = ld4(hr + kc * 16);
+            }
+            const floatx4 b = ld4(fm + lay.b2 + zero + at * 16 + 4 * g);
+#pragma unroll
+            for (int kc = 0; kc < HC; ++kc) qk[kc] = mfma_chunk(wk[kc], hk[kc], floatx4{0.f, 0.f, 0.f, 0.f});
+            floatx4 q = b;
 #pragma unroll
             for (int kc = 0; kc < HC; ++kc) q += qk[kc];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {  // masked argmax (argmax_accumulate on the bit mask)
+            for (int r = 0; r < 4; ++r) {  // masked argmax (argmax_accumulate on the bit mask), branch-free
                 const int a = at * 16 + 4 * g + r;
-                if (a >= A) continue;
-                const float v = ((avm >> a) & 1ull) ? q[r] : -INFINITY;
-                if (amax_better(v, a, as.bv, as.bi)) { as.bv = v; as.bi = a; }
+                const float v = (a < A && ((avm >> a) & 1ull)) ? q[r] : -INFINITY;
+                const bool take = a < A && amax_better(v, a, as.bv, as.bi);
+                as.bv = take ? v : as.bv;
+                as.bi = take ? a : as.bi;
+            }
+        };
+        if (n_at == 1)
+            q_block(0);
+        else
+            for (int at = 0; at < n_at; ++at) q_block(at);
+        int ract = -1;  // random available action of an exploring agent
+        if (explore && valid && g == 0) {
+            const uint64_t r2 = mlg_rng(key, mlg_ctr(ep, (uint32_t)t, MLG_PURPOSE_RAND, (uint32_t)n));
+            const int na = __popcll(avm);  // random_available on the mask: k-th available action
+            ract = 0;
+            if (na > 0) {
+                const int k = (int)(((r2 >> 40) * (uint64_t)na) >> 24);
+                uint64_t m = avm;
+                for (int i = 0; i < k; ++i) m &= m - 1;
+                ract = __ffsll((long long)m) - 1;
             }
         }
         int act = argmax_reduce(as);
@@ -1631,10 +1645,21 @@ __device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2&
 // ================================================================================================
 // v2 kernel: 8 waves, 16 envs; every wave does agent work (chunk j = w % HC of tiles w / HC, ...) and then
 // the env step of envs 2w, 2w + 1. Barriers per step: A|B, B|C, C|env, env|A.
-template <int H, bool G8 = false>
-__global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
-                                                           const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
-                                                           float eps, int test_mode, RolloutLds2 lay) {
+// Static shape (SN agents, SU units > 0; v7 only): the agent and LDS layouts are compile-time constants (the
+// headline 5v5 and the 3v3 plans, obs_last_action / obs_agent_id on), so their ~50 offsets are immediates instead
+// of SGPRs -- the generic kernel spills SGPRs into VGPR lanes inside the step loop. Same code otherwise.
+template <int H, bool G8, int SN, int SU>
+struct StaticShape {
+    static constexpr bool on = SN > 0;
+    static constexpr MlgAgentDims dims{8 * SU, 5 + SU, SN, H, 8 * SU + 5 + SU + SN, 1, 1};
+    static constexpr AgentLayout L = on ? make_agent_layout(dims) : AgentLayout{};
+    static constexpr RolloutLds2 lay = on ? make_rollout_lds2(L, SU, SN, 16, 2, G8 ? 1 : 0) : RolloutLds2{};
+};
+
+template <int H, bool G8>
+__device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
+                                                const float* __restrict__ P, const MlgBatch& bt, const MlgRunInfo& info,
+                                                float eps, int test_mode, const RolloutLds2& lay) {
     constexpr int HC = H / 16, NW = 8, REW = 16, G = NW / HC;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     float* fm = reinterpret_cast<float*>(smem);
@@ -1680,6 +1705,7 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
         rows_issued += tiles * 16;
         sp.mark(0);
         __syncthreads();
+        if constexpr (G8) sp.mark(5);  // v7 stamps: barrier A wait in slot 5, barrier B wait in slot 13
         if constexpr (G8)
             ph_gru_g8<H>(W8, lay, fm, wmap, hc, hn, tiles, N, wave, lane);
         else
@@ -1692,6 +1718,7 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
 #endif
         sp.mark(1);
         __syncthreads();
+        if constexpr (G8) sp.mark(13);
         if constexpr (G8)
             ph_fc2_g8<H>(spec, L, lay, fm, wmap, C.R, bt, hn, tiles, wave, NW, e0, t, eps, test_mode, lane);
         else
@@ -1716,6 +1743,17 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
     sp.flush();
     if (threadIdx.x == 0 && info.agent_rows) atomicAdd(info.agent_rows, (unsigned long long)rows_issued);
     env_lane_finish(C, st, E, hl);
+}
+
+template <int H, bool G8 = false, int SN = 0, int SU = 0>
+__global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
+                                                           const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
+                                                           float eps, int test_mode, RolloutLds2 lay) {
+    using S = StaticShape<H, G8, SN, SU>;
+    if constexpr (S::on)
+        rollout_v2_body<H, G8>(spec, st, S::L, P, bt, info, eps, test_mode, S::lay);
+    else
+        rollout_v2_body<H, G8>(spec, st, L, P, bt, info, eps, test_mode, lay);
 }
 
 // ================================================================================================
@@ -2028,6 +2066,13 @@ int launch_rollout(int grid, int threads, hipStream_t s, const MlgEnvSpec& spec,
     return launch_rollout_t<H, TPW, false>(grid, threads, s, spec, st, L, sd, info, tm, lay);
 }
 
+// v7 with a compile-time shape when the layout matches one (StaticShape), else the generic v7.
+template <int SN, int SU>
+bool static_shape_matches(const AgentLayout& L, const RolloutLds2& lay) {
+    using S = StaticShape<64, true, SN, SU>;
+    return memcmp(&L, &S::L, sizeof(AgentLayout)) == 0 && memcmp(&lay, &S::lay, sizeof(RolloutLds2)) == 0;
+}
+
 template <int H, int V>
 int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
                       const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
@@ -2037,6 +2082,10 @@ int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& 
                        : (V == 5 ? rollout_v4_kernel<H, 8>
                                  : (V == 6 ? rollout_v6_kernel<H>
                                            : (V == 7 ? rollout_v2_kernel<64, true> : rollout_v2_kernel<H>)));
+    if (V == 7 && !getenv("MLG_ROLLOUT_GENERIC")) {
+        if (static_shape_matches<5, 10>(L, lay)) kern = rollout_v2_kernel<64, true, 5, 10>;
+        else if (static_shape_matches<3, 6>(L, lay)) kern = rollout_v2_kernel<64, true, 3, 6>;
+    }
     const int threads = V == 4 ? 512 : (V == 5 ? 768 : (V == 6 ? 256 : 512));
     const int rew = V == 6 ? 8 : 16;
     if (bytes > 64 * 1024) {

@@ -32,6 +32,9 @@ if os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v1":
     names = ["agent", "barrier_after_agent", "-", "-"]
     names += ["E1_exec_actions", "E2_resolve(+bar)", "E3_reduce(+bar)", "obs(+bar)", "state", "avail",
               "zero+list+barrier"]
+elif os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v7":
+    names = ["A_fc1", "B_gru", "C_fc2_select", "barrier_after_C", "E1_exec(+E2)", "barrier_A",
+             "E3_reduce", "pair_pass", "status/tail-zero", "obs", "barrier_end", "avail", "state", "barrier_B"]
 else:
     names = ["A_fc1", "B_gru(+barrier A)", "C_fc2_select(+barrier B)", "barrier_after_C", "E1_exec", "E2_resolve",
              "E3_reduce", "pair_pass", "status/tail-zero", "obs", "barrier_end", "avail", "state"]

@@ -365,14 +365,18 @@ def test_rollout_second_run_before_insert_leaves_ring_episodes(device):
         assert torch.equal(ring[k][48:96], b2[k]), k
 
 
+@pytest.mark.parametrize("generic", [False, True])
 @pytest.mark.parametrize("plan", ["medium_1h_4t", "medium", "small"])
-def test_rollout_v7_split_bf16_gru_matches_fp32(device, plan, monkeypatch):
+def test_rollout_v7_split_bf16_gru_matches_fp32(device, plan, generic, monkeypatch):
     """v7: the GRU products run on the bf16 matrix cores as split-bf16 fp32 emulation (three bf16 pieces per
     operand, six partial products, fp32 accumulation). Along v7's own recorded trajectory (test mode, epsilon 0)
     the fp32 oracle DRQN (oracle/learner_ref.py, drqn_agent.py:29-35) must rate every recorded action as an
     available argmax up to a 1e-5 tie, and v7 must reproduce v2's episodes bit for bit except where a near-tie
-    of the Q values flips an argmax (env transitions of v7 are the v2 env code)."""
+    of the Q values flips an argmax (env transitions of v7 are the v2 env code). generic: the runtime-shape kernel
+    instead of the compile-time-shape instantiation (5v5 / 3v3 plans)."""
     from maleague.envs.teams_env import VecEnvState
+    if generic:
+        monkeypatch.setenv("MLG_ROLLOUT_GENERIC", "1")
     B, TL = 100, 60
     stepper, mac, args = _build_stepper(device, plan=plan, B=B, episode_limit=TL, seed=3)
     out = {}
