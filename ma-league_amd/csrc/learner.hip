@@ -265,7 +265,6 @@ __device__ __forceinline__ floatx4 tile_mm_lds(const float* __restrict__ W, int6
     return acc;
 }
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 // ================================================================================================
 // forward, split into the parallel (non-recurrent) and the recurrent part:
@@ -394,9 +393,9 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
         floatx4 rg, zg, ng, hn;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            rg[q] = sigm(ar[q]);
-            zg[q] = sigm(az[q]);
-            ng[q] = tanhf(gc[2][q] + rg[q] * ahn[q]);
+            rg[q] = fast_sigmoid(ar[q]);
+            zg[q] = fast_sigmoid(az[q]);
+            ng[q] = fast_tanh(gc[2][q] + rg[q] * ahn[q]);
             hn[q] = ng[q] + zg[q] * (hp[q] - ng[q]);
         }
         *reinterpret_cast<floatx4*>(hs[cur ^ 1] + col * LDA + f0) = hn;
@@ -505,9 +504,9 @@ __global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, 
         floatx4 rg, zg, ng, hn;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            rg[e] = sigm(acc[e]);
-            zg[e] = sigm(az[e]);
-            ng[e] = tanhf(in.gn[e] + rg[e] * ahn[e]);
+            rg[e] = fast_sigmoid(acc[e]);
+            zg[e] = fast_sigmoid(az[e]);
+            ng[e] = fast_tanh(in.gn[e] + rg[e] * ahn[e]);
             hn[e] = ng[e] + zg[e] * (hp[e] - ng[e]);
         }
         if (lead) *reinterpret_cast<floatx4*>(hs[cur ^ 1] + q * LDA + fD) = hn;

@@ -27,6 +27,12 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 
+// GRU gates on the hardware exp / reciprocal (v_exp_f32, v_rcp_f32; ~1 ulp each) instead of libm expf / tanhf and
+// IEEE division (~70 instructions with range branches): used by the v7 rollout and the learner recurrence, whose
+// parity bars are tolerance-based (Q 1e-4, learner stats rtol 1e-4); tanh(x) = 2 sigmoid(2x) - 1.
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float fast_tanh(float x) { return 2.f * fast_sigmoid(2.f * x) - 1.f; }
+
 // Branch-free predicated stores through a raw buffer resource: a dropped lane gets an out-of-range offset and
 // the hardware range check discards it. Inside sequential loops this keeps the VMEM stream straight-line, so
 // the compiler's waitcnt for a prefetched load counts the stores issued after it (an `if (valid)` store would

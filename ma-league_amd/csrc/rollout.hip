@@ -1171,11 +1171,6 @@ __device__ inline void load_gru_g8(GruG8& W, const float* __restrict__ P, const 
             asm volatile("" : "+v"(W.rzi[kk].p[q]), "+v"(W.rzh[kk].p[q]), "+v"(W.n[kk].p[q]));
 }
 
-// Gates of v7: hardware exp / reciprocal (v_exp_f32, v_rcp_f32; ~1 ulp each) -- v7 is fp32-class, not bit-equal
-// to v2, so the ~70-instruction libm expf / tanhf / IEEE division are not needed; tanh(x) = 2 sigmoid(2x) - 1.
-__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-__device__ __forceinline__ float fast_tanh(float x) { return 2.f * fast_sigmoid(2.f * x) - 1.f; }
-
 // B: GRU cell of every tile for the wave's 8 features -> h' (env-row hidden state). x comes as bf16 planes from
 // fc1 (split once), h is split here; the compact-row -> env-row map was stored by fc1.
 template <int H>
