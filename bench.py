@@ -193,8 +193,10 @@ def main():
     issued = fl / (sides * N) * rows_per_launch / avg_kernel_s if mode == "ai" else None
     traffic = None
     kc1 = (info.get("entity_shape", 0) + A + 15) // 16 if mode == "refil" else 0
-    kernel = {"ai": "rollout_v2_kernel<64, true>", "league": "rollout_sp_kernel<64>",
-              "refil": f"refil_rollout_kernel<{kc1}>"}[mode]
+    # the default rollout kernel: v7 (split-bf16 GRU), compile-time shape for the 5v5 / 3v3 plans
+    v7 = "rollout_v2_kernel<64, true, 5, 10>" if (N, info["n_actions"]) == (5, 15) else (
+        "rollout_v2_kernel<64, true, 3, 6>" if (N, info["n_actions"]) == (3, 11) else "rollout_v2_kernel<64, true>")
+    kernel = {"ai": v7, "league": "rollout_sp_kernel<64>", "refil": f"refil_rollout_kernel<{kc1}>"}[mode]
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
             traffic = json.load(f).get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
@@ -232,6 +234,9 @@ def main():
         if issued is not None:
             out["roofline"].update({"issued_tflops": issued / 1e12, "issued_frac": issued / FP32_MFMA_PEAK,
                                     "issued_rows_per_launch": rows_per_launch})
+        if mode == "ai" and kernel.startswith("rollout_v2_kernel<64, true"):
+            out["roofline"]["note"] = ("fp32 algorithmic FLOPs vs the fp32 MFMA peak; the GRU products run as "
+                                       "split-bf16 fp32 emulation (6 bf16 MFMA partial products each, DESIGN.md §4a)")
         if inst is not None:
             out["league"] = {"opponents_rank0": [h[1] for h in inst.history],
                              "historical_snapshots": len(inst.league.historical_meta)}

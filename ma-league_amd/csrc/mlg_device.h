@@ -27,6 +27,20 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 
+// bf16 operands of v_mfma_f32_16x16x32_bf16 (8 per lane) and round-to-nearest packing of two fp32 (low half = lo).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned int cvt_pk_bf16(float lo, float hi) {
+    unsigned int r;
+    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+    return r;
+}
+
+__device__ __forceinline__ floatx4 mfma_bf16(bf16x8 a, bf16x8 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // GRU gates on the hardware exp / reciprocal (v_exp_f32, v_rcp_f32; ~1 ulp each) instead of libm expf / tanhf and
 // IEEE division (~70 instructions with range branches): used by the v7 rollout and the learner recurrence, whose
 // parity bars are tolerance-based (Q 1e-4, learner stats rtol 1e-4); tanh(x) = 2 sigmoid(2x) - 1.

@@ -707,7 +707,7 @@ __device__ __forceinline__ int v2_avail(const UnitMasks& M, int G, int x, int y,
 __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec& spec, const SpecShared& SS,
                                            const int* pairtab, const int* avtab, const MlgBatch& bt, int slot, int t,
                                            int e, int hbase, int hl, const UnitLane& L, float* lobs, int ldo,
-                                           uint64_t* lavm, float inv_p, Stamps& sp) {
+                                           uint64_t* lavm, float inv_p, Stamps& sp, bool obf = false) {
     const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, G = spec.grid;
     const int64_t st_row = (int64_t)slot * bt.T1 + t;
     const int pk = pk_unit(L.x, L.y, L.hp);
@@ -730,9 +730,15 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
             float* dst = bt.obs + (st_row * N + a) * DO + j * 8;
             *reinterpret_cast<floatx4*>(dst) = lo;
             *reinterpret_cast<floatx4*>(dst + 4) = hi;
-            float* l = lobs + (e * N + a) * ldo + j * 8;
-            *reinterpret_cast<floatx4*>(l) = lo;
-            *reinterpret_cast<floatx4*>(l + 4) = hi;
+            if (obf) {  // v7: bf16 rows (every obs feature is exact in bf16: k/32, hp/max_hp, 0, 0.5, 1)
+                *reinterpret_cast<uint4*>(lobs + (e * N + a) * ldo + j * 4) =
+                    make_uint4(cvt_pk_bf16(lo.x, lo.y), cvt_pk_bf16(lo.z, lo.w), cvt_pk_bf16(hi.x, hi.y),
+                               cvt_pk_bf16(hi.z, hi.w));
+            } else {
+                float* l = lobs + (e * N + a) * ldo + j * 8;
+                *reinterpret_cast<floatx4*>(l) = lo;
+                *reinterpret_cast<floatx4*>(l + 4) = hi;
+            }
         }
     }
     sp.mark(9);
@@ -796,10 +802,13 @@ __host__ __device__ constexpr RolloutLds2 make_rollout_lds2(const AgentLayout& L
                                                             int xpl = 0) {
     RolloutLds2 r{};
     r.xpl = xpl;
-    r.ldo = L.Dob + 4;
+    // v7 (xpl): obs rows and W1 obs-column rows as bf16, K padded to a multiple of 32 (Kp); row stride Kp / 2 + 4
+    // words (an odd multiple of 4: the 16 rows of an MFMA operand read start on distinct bank quads); W1 held as
+    // three bf16 planes (W1 = p0 + p1 + p2 exactly). Else fp32 rows of Dob + 4 floats.
+    r.ldo = xpl ? ((L.Dob + 31) / 32 * 32) / 2 + 4 : L.Dob + 4;
     r.ldh = L.H + 4;
     int64_t o = 0;
-    r.w1o = ro_take(o, (int64_t)L.H * r.ldo);
+    r.w1o = ro_take(o, (int64_t)(xpl ? 3 : 1) * L.H * r.ldo);
     r.w1a = ro_take(o, L.last_action ? (int64_t)L.A * r.ldh : 0);
     r.w1n = ro_take(o, L.agent_id ? (int64_t)N * r.ldh : 0);
     r.b1 = ro_take(o, L.H);
@@ -827,6 +836,8 @@ __host__ __device__ constexpr RolloutLds2 make_rollout_lds2(const AgentLayout& L
     return r;
 }
 
+
+
 __device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
     for (int i = 0; i < k; ++i) m &= m - 1;
     return __builtin_ctz(m);
@@ -845,7 +856,22 @@ __device__ void v2_prologue(const MlgEnvSpec& spec, const AgentLayout& L, const 
     };
     for (int64_t i = tid; i < (int64_t)rows * lay.ldo; i += nthr) fm[lay.obs + i] = 0.f;
     for (int64_t i = tid; i < (int64_t)lay.nhb * lay.hsz; i += nthr) fm[lay.hb + i] = 0.f;
-    rows_cp(L.w1o, lay.w1o, H, L.Dob, lay.ldo);
+    if (lay.xpl) {  // v7: W1 obs columns as three bf16 planes [3][H][2 ldo], zero-padded to Kp
+        const int Kp = 2 * (lay.ldo - 4), pl = H * lay.ldo;
+        unsigned short* w = reinterpret_cast<unsigned short*>(fm + lay.w1o);
+        for (int i = tid; i < H * Kp; i += nthr) {
+            const int f = i / Kp, k = i % Kp;
+            float v = k < L.Dob ? P[L.w1o + (int64_t)f * L.Dob + k] : 0.f;
+#pragma unroll
+            for (int lvl = 0; lvl < 3; ++lvl) {
+                const unsigned int pk = cvt_pk_bf16(v, 0.f);
+                w[2 * (lvl * pl + f * lay.ldo) + k] = (unsigned short)(pk & 0xFFFFu);
+                v -= __uint_as_float(pk << 16);
+            }
+        }
+    } else {
+        rows_cp(L.w1o, lay.w1o, H, L.Dob, lay.ldo);
+    }
     if (L.last_action) rows_cp(L.w1a, lay.w1a, L.A, H, lay.ldh);
     if (L.agent_id) rows_cp(L.w1n, lay.w1n, N, H, lay.ldh);
     rows_cp(L.b1, lay.b1, 1, H, H);
@@ -935,11 +961,6 @@ __device__ inline StepRows make_rows(const uint32_t* amask, int ebase, int ne, i
 }
 
 // A: fc1 + ReLU for (tile, chunk j) over tiles ti0, ti0 + dt, ...  -> x (compact rows)
-__device__ __forceinline__ unsigned int cvt_pk_bf16(float lo, float hi) {
-    unsigned int r;
-    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-    return r;
-}
 
 template <int H>
 __device__ inline void ph_fc1(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* prev,
@@ -1038,7 +1059,7 @@ __device__ inline int make_rmap(const uint32_t* amask, int* wmap, int lane) {
 template <int H>
 __device__ inline void ph_fc1_g8(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* rmap, const int* prev,
                                  int tiles, int j, int ti0, int dt, int t, int lane) {
-    const int col = lane & 15, g = lane >> 4, N = L.N, ldo = lay.ldo, ldh = lay.ldh, KO = L.Dob / 16;
+    const int col = lane & 15, g = lane >> 4, N = L.N, ldo = lay.ldo, ldh = lay.ldh, KK = (L.Dob + 31) / 32;
     const float* lobs = fm + lay.obs;
     for (int ti = ti0; ti < tiles; ti += dt) {
         int zero = 0;
@@ -1051,9 +1072,17 @@ __device__ inline void ph_fc1_g8(const AgentLayout& L, const RolloutLds2& lay, f
         const int pa = (valid && t > 0) ? prev[er] : -1;
         if (L.last_action && pa >= 0) acc += ld4(fm + lay.w1a + pa * ldh + j * 16 + 4 * g);
         if (L.agent_id) acc += ld4(fm + lay.w1n + n * ldh + j * 16 + 4 * g);
-        const float* orow = lobs + er * ldo + 4 * g;
-        const float* wrow = fm + lay.w1o + zero + (j * 16 + col) * ldo + 4 * g;
-        for (int kc = 0; kc < KO; ++kc) acc = mfma_chunk(ld4(wrow + kc * 16), ld4(orow + kc * 16), acc);
+        // bf16 obs row (exact) x W1 as three bf16 planes: 3 partial products per 32-wide K step, all exact, fp32
+        // accumulation (the same fp32-class arithmetic as the GRU, §4a)
+        const bf16x8* orow = reinterpret_cast<const bf16x8*>(lobs + er * ldo) + g;
+        const bf16x8* wrow = reinterpret_cast<const bf16x8*>(fm + lay.w1o + zero + (j * 16 + col) * ldo) + g;
+        const int pl = L.H * ldo / 4;  // plane stride in bf16x8 units
+        for (int kk = 0; kk < KK; ++kk) {
+            const bf16x8 b = orow[4 * kk];
+            acc = mfma_bf16(wrow[2 * pl + 4 * kk], b, acc);
+            acc = mfma_bf16(wrow[pl + 4 * kk], b, acc);
+            acc = mfma_bf16(wrow[4 * kk], b, acc);
+        }
         unsigned int* xr = reinterpret_cast<unsigned int*>(fm + lay.xb + cr * XPL_STRIDE) + (j * 16 + 4 * g) / 2;
         float v[4] = {fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f), fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f)};
 #pragma unroll
@@ -1079,8 +1108,6 @@ __device__ inline void ph_fc1_g8(const AgentLayout& L, const RolloutLds2& lay, f
 // instead of 8 x 32 = 256 for v_mfma_f32_16x16x4_f32 (MI355X_MICROARCH.md cycle table). Accumulation is fp32
 // inside the MFMA, in a different order than the v1/v2 fmaf chains: v7 results equal v2's to fp32 rounding,
 // not bit for bit.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct Split3 {
     bf16x8 p[3];
@@ -1116,9 +1143,6 @@ __device__ __forceinline__ Split3 split3(floatx4 a, floatx4 b) {
     return s;
 }
 
-__device__ __forceinline__ floatx4 mfma_bf16(bf16x8 a, bf16x8 b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 
 // acc += A . B over one 32-wide K step with the six partial products (small terms first).
 __device__ __forceinline__ floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 c) {
@@ -1403,6 +1427,7 @@ struct EnvCtx {
     float* lobs;
     uint64_t* lavm;  // [16 envs * N] avail bit masks of the agents' current step
     int ldo, B;
+    bool obf;  // v7: obs rows in LDS are bf16
     float inv_p;
 };
 
@@ -1445,7 +1470,7 @@ __device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, En
         Stamps none;
         v2_pair_pass(C.M, spec.U, hl, E.u, C.pk + e * 32);
         v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, 0, e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
-                   C.inv_p, none);
+                   C.inv_p, none, C.obf);
     }
 }
 
@@ -1463,6 +1488,9 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
         if (!C.bt.full_write) C.bt.actions_onehot[off * A] = 1.0f;
     }
     if (hl < N) C.R.prev[E.e * N + hl] = pact[hl];
+#ifdef MLG_DUP_ONEHOT
+    for (int rep = 0; rep < 2; ++rep)
+#endif
     if (C.bt.full_write) {  // whole one-hot rows of the recorded actions
         const int64_t oh = ((int64_t)E.slot * T1 + t) * N * A;
         // rolled: the unrolled copy's rounded trip count was the v2 kernel's last VGPR spill, and its in-loop
@@ -1503,6 +1531,10 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     sact[hl] = act;
     int dmg = 0, heal = 0;
     const int me = MLG_ACT_BASE + hl;
+#ifdef MLG_DUP_E2  // timing ablation: the resolution loop twice (same result)
+    for (int rep = 0; rep < 2; ++rep) {
+    dmg = 0; heal = 0;
+#endif
     for (int i0 = 0; i0 < U; i0 += 4) {
         const int4 q4 = *reinterpret_cast<const int4*>(spk + i0);
         const int4 a4 = *reinterpret_cast<const int4*>(sact + i0);
@@ -1516,6 +1548,10 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
             dmg += (hit && !hl_i) ? role_power(mask_role(C.M, i)) : 0;
         }
     }
+#ifdef MLG_DUP_E2
+    asm volatile("" : "+v"(dmg), "+v"(heal));
+    }
+#endif
     E.h0 = E.u.hp;
     if (uvalid && E.h0 > 0) {
         const int v = E.h0 - dmg + heal, mx = role_maxhp(mask_role(C.M, hl));
@@ -1581,10 +1617,10 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
 #endif
     sp.mark(7);
     v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
-               C.inv_p, sp);
+               C.inv_p, sp, C.obf);
 #ifdef MLG_DUP_OBS
     v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
-               C.inv_p, sp);
+               C.inv_p, sp, C.obf);
 #endif
 }
 
@@ -1632,6 +1668,7 @@ __device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2&
     C.lobs = fm + lay.obs;
     C.lavm = reinterpret_cast<uint64_t*>(smem + lay.avail);
     C.ldo = lay.ldo;
+    C.obf = lay.xpl != 0;
     C.B = bt.B;
     C.inv_p = 1.0f / (float)pow2_at_least(spec.grid);
     return C;
@@ -1730,6 +1767,9 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         env_lane_step1(C, E, t, hl);
         sp.mark(4);
         env_lane_step2(C, E, t, hl, sp);
+#ifdef MLG_DUP_TAIL  // timing ablation: the tail zeroing twice over the same steps
+        if (!E.stepped && (t & 1)) { const int z0 = E.zcur; env_lane_tail(C, E, 8, hl); E.zcur = z0; }
+#endif
         if (!E.stepped && (t & 1)) env_lane_tail(C, E, 8, hl);
         sp.mark(8);
         __syncthreads();

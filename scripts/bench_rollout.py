@@ -1,5 +1,6 @@
 """Deterministic rollout-kernel microbenchmark: fixed random policy, the same episodes every repetition
-(env episode counters reset), 4096 envs, medium_1h_4t, episode_limit 100, epsilon 0.05.
+(env episode counters reset), 4096 envs, medium_1h_4t, episode_limit 100, epsilon 0.05. RING=1: train-mode runs
+write into a 5000-episode replay ring in full-write mode (the bench's path); each run is inserted.
 Prints mean kernel ms (HIP events) per kernel variant given in MLG_BENCH_KERNELS (default "v2")."""
 import json
 import os
@@ -28,6 +29,11 @@ proto = EpisodeBatch(scheme, groups, 1, 2, preprocess=preprocess, device="cuda")
 torch.manual_seed(0)
 mac = BasicMAC(proto.scheme, groups, args)
 stepper.initialize(scheme, groups, preprocess, mac)
+ring = None
+if int(os.environ.get("RING", "0")):
+    from maleague.components.replay_buffer import ReplayBuffer
+    ring = ReplayBuffer(scheme, groups, 5000, 101, preprocess=preprocess, device="cuda")
+    assert stepper.attach_replay(ring)
 out = {}
 for k in os.environ.get("MLG_BENCH_KERNELS", "v7").split(","):
     os.environ["MLG_ROLLOUT_KERNEL"] = k
@@ -37,6 +43,8 @@ for k in os.environ.get("MLG_BENCH_KERNELS", "v7").split(","):
         stepper.t_env = 10 ** 6
         stepper.timing = []
         stepper.run(test_mode=bool(int(os.environ.get("TEST_MODE", "0"))))
+        if ring is not None:
+            ring.insert_episode_batch(stepper.home_batch)
         torch.cuda.synchronize()
         if r >= 2:
             ms.append(stepper.timing[0][0].elapsed_time(stepper.timing[0][1]))
