@@ -707,14 +707,17 @@ __device__ __forceinline__ int v2_avail(const UnitMasks& M, int G, int x, int y,
 __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec& spec, const SpecShared& SS,
                                            const int* pairtab, const int* avtab, const MlgBatch& bt, int slot, int t,
                                            int e, int hbase, int hl, const UnitLane& L, float* lobs, int ldo,
-                                           uint64_t* lavm, float inv_p, Stamps& sp, bool obf = false) {
-    const int U = spec.U, N = spec.n_agents, A = spec.n_actions, S = 6 * U, DO = 8 * U, G = spec.grid;
+                                           uint64_t* lavm, float inv_p, Stamps& sp, bool obf, int U, int N, int A,
+                                           bool sd) {
+    const int S = 6 * U, DO = 8 * U, G = spec.grid;
     const int64_t st_row = (int64_t)slot * bt.T1 + t;
     const int pk = pk_unit(L.x, L.y, L.hp);
+#pragma unroll 1  // rolled: unrolled (static dims) it pushes the v7 kernel past 256 VGPRs
     for (int k0 = 0; k0 < N * U; k0 += 32) {
         const int k = k0 + hl;
         const bool valid = k < N * U;
-        const int pt = pairtab[valid ? k : 0];
+        const int kk = valid ? k : 0;
+        const int pt = sd ? ((kk / U) << 8) | (kk % U) : pairtab[kk];
         const int a = pt >> 8, j = pt & 255, i = SS.aunit[a];
         const int qi = __shfl(pk, hbase + i, 64), qj = __shfl(pk, hbase + j, 64);
         const uint32_t ti = __shfl((int)L.tgt, hbase + i, 64), si = __shfl((int)L.sight, hbase + i, 64);
@@ -757,7 +760,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
     for (int k0 = 0; k0 < N * A; k0 += 32) {
         const int k = k0 + hl;
         if (k < N * A) {
-            const int pt = avtab[k];
+            const int pt = sd ? ((k / A) << 8) | (k % A) : avtab[k];
             bt.avail[st_row * N * A + k] = (int)((lavm[e * N + (pt >> 8)] >> (pt & 255)) & 1ull);
         }
     }
@@ -1428,8 +1431,16 @@ struct EnvCtx {
     uint64_t* lavm;  // [16 envs * N] avail bit masks of the agents' current step
     int ldo, B;
     bool obf;  // v7: obs rows in LDS are bf16
+    int U, N, A;  // env dims (compile-time constants in the static-shape v7 instantiations)
+    bool sd;      // static dims: index tables replaced by arithmetic
     float inv_p;
 };
+
+__device__ __forceinline__ void env_observe(const EnvCtx& C, const MlgEnvSpec& spec, int slot, int t, int e, int hbase,
+                                            int hl, const UnitLane& L, Stamps& sp) {
+    v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, slot, t, e, hbase, hl, L, C.lobs, C.ldo, C.lavm, C.inv_p, sp,
+               C.obf, C.U, C.N, C.A, C.sd);
+}
 
 __device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, EnvLane& E, int e, int e0, int hl) {
     const MlgEnvSpec& spec = *C.spec;
@@ -1450,7 +1461,7 @@ __device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, En
         E.ep = st.episode[E.b];
         E.st = 0;
         E.slot = C.bt.ring_size > 0 ? (C.bt.ring_slot0 + E.b) % C.bt.ring_size : E.b;
-        if (hl < spec.U) {
+        if (hl < C.U) {
             const int tm = C.SS->team[hl];
             env_spawn_xyh(make_tables(spec, *C.SS), mlg_env_key(spec.seed, E.b), E.ep, hl, C.SS->team_first[tm],
                           C.SS->team_size[tm], E.u.x, E.u.y, E.u.hp);
@@ -1464,13 +1475,12 @@ __device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, En
         C.R.status[e] = E.st;
         C.R.slot[e] = E.slot;
         C.R.episode[e] = E.ep;
-        C.amask[e] = E.b < C.B ? (spec.n_agents >= 32 ? 0xFFFFFFFFu : (1u << spec.n_agents) - 1u) : 0u;
+        C.amask[e] = E.b < C.B ? (C.N >= 32 ? 0xFFFFFFFFu : (1u << C.N) - 1u) : 0u;
     }
     if (E.b < C.B) {
         Stamps none;
-        v2_pair_pass(C.M, spec.U, hl, E.u, C.pk + e * 32);
-        v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, 0, e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
-                   C.inv_p, none, C.obf);
+        v2_pair_pass(C.M, C.U, hl, E.u, C.pk + e * 32);
+        env_observe(C, spec, E.slot, 0, e, hbase, hl, E.u, none);
     }
 }
 
@@ -1479,7 +1489,7 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     E.stepped = false;
     if (E.st == 2) return;
     const MlgEnvSpec& spec = *C.spec;
-    const int N = spec.n_agents, A = spec.n_actions, U = spec.U, T1 = C.bt.T1;
+    const int N = C.N, A = C.A, U = C.U, T1 = C.bt.T1;
     int* pact = C.R.pact + E.e * N;
     if (hl < N && !((C.amask[E.e] >> hl) & 1u)) {  // dead agent: no cell was run; its action is the no-op
         pact[hl] = 0;
@@ -1497,7 +1507,7 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
         // scratch reload (vmcnt being in order) waited for every store of the step issued so far
 #pragma unroll 1
         for (int k = hl; k < N * A; k += 32) {
-            const int pt = C.avtab[k];
+            const int pt = C.sd ? ((k / A) << 8) | (k % A) : C.avtab[k];
             C.bt.actions_onehot[oh + k] = (pt & 255) == pact[pt >> 8] ? 1.0f : 0.0f;
         }
     }
@@ -1568,7 +1578,7 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
 __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl, Stamps& sp) {
     if (!E.stepped) return;
     const MlgEnvSpec& spec = *C.spec;
-    const int U = spec.U, T1 = C.bt.T1;
+    const int U = C.U, T1 = C.bt.T1;
     const int hbase = (threadIdx.x & 63) & 32;
     const bool uvalid = hl < U;
     const int h0 = E.h0, h1 = E.u.hp;
@@ -1605,7 +1615,7 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
     }
     if (hl == 0) C.R.status[E.e] = E.st;
     {  // agents alive after the step need a Q for the next action (incl. the final one after termination)
-        const int N = spec.n_agents;
+        const int N = C.N;
         const uint32_t am = (uint32_t)(__ballot(hl < N && ((alive_m >> C.SS->aunit[hl < N ? hl : 0]) & 1u)) >> hbase);
         if (hl == 0) C.amask[E.e] = am;
     }
@@ -1616,11 +1626,9 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
     v2_pair_pass(C.M, U, hl, E.u, C.pk + E.e * 32);
 #endif
     sp.mark(7);
-    v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
-               C.inv_p, sp, C.obf);
+    env_observe(C, spec, E.slot, t + 1, E.e, hbase, hl, E.u, sp);
 #ifdef MLG_DUP_OBS
-    v2_observe(C.M, spec, *C.SS, C.pairtab, C.avtab, C.bt, E.slot, t + 1, E.e, hbase, hl, E.u, C.lobs, C.ldo, C.lavm,
-               C.inv_p, sp, C.obf);
+    env_observe(C, spec, E.slot, t + 1, E.e, hbase, hl, E.u, sp);
 #endif
 }
 
@@ -1629,14 +1637,14 @@ __device__ inline void env_lane_tail(const EnvCtx& C, EnvLane& E, int steps, int
     if (!C.bt.full_write || E.st != 2 || E.zcur >= C.bt.T1 || E.b >= C.B) return;
     const MlgEnvSpec& spec = *C.spec;
     const int z1 = E.zcur + steps < C.bt.T1 ? E.zcur + steps : C.bt.T1;
-    zero_slot_steps(C.bt, E.slot, E.zcur, z1, spec.n_agents, spec.n_actions, 6 * spec.U, 8 * spec.U, hl, 32);
+    zero_slot_steps(C.bt, E.slot, E.zcur, z1, C.N, C.A, 6 * C.U, 8 * C.U, hl, 32);
     E.zcur = z1;
 }
 
 // Per-env summary + env state write-back (+ the rest of the tail in full-write mode).
 __device__ inline void env_lane_finish(const EnvCtx& C, const MlgEnvState& st, EnvLane& E, int hl) {
     if (E.b >= C.B) return;
-    const int U = C.spec->U;
+    const int U = C.U;
     if (C.bt.full_write) env_lane_tail(C, E, C.bt.T1, hl);
     if (hl == 0) {
         C.info.ep_len[E.b] = E.len;
@@ -1651,12 +1659,16 @@ __device__ inline void env_lane_finish(const EnvCtx& C, const MlgEnvState& st, E
 }
 
 __device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2& lay, int* smem, const MlgBatch& bt,
-                                      const MlgRunInfo& info) {
+                                      const MlgRunInfo& info, int U, int N, int A, bool sd) {
     EnvCtx C;
+    C.U = U;
+    C.N = N;
+    C.A = A;
+    C.sd = sd;
     float* fm = reinterpret_cast<float*>(smem);
     C.spec = &spec;
     C.SS = reinterpret_cast<const SpecShared*>(smem + lay.env.spec);
-    C.M = make_unit_masks(*C.SS, spec.U);
+    C.M = make_unit_masks(*C.SS, U);
     C.R = env_view(smem, lay.env);
     C.bt = bt;
     C.info = info;
@@ -1691,14 +1703,15 @@ struct StaticShape {
 template <int H, bool G8>
 __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
                                                 const float* __restrict__ P, const MlgBatch& bt, const MlgRunInfo& info,
-                                                float eps, int test_mode, const RolloutLds2& lay) {
+                                                float eps, int test_mode, const RolloutLds2& lay, int DU, int DN,
+                                                int DA, bool SD) {
     constexpr int HC = H / 16, NW = 8, REW = 16, G = NW / HC;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     float* fm = reinterpret_cast<float*>(smem);
     const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
     const int e0 = blockIdx.x * REW, T1 = bt.T1;
     v2_prologue(spec, L, P, lay, smem, REW * N);
-    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info);
+    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info, DU, DN, DA, SD);
     EnvLane E;
     env_lane_reset(C, st, E, wave * 2 + (lane >> 5), e0, hl);
     const int j = wave % HC, gi = wave / HC;
@@ -1786,9 +1799,10 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
                                                            float eps, int test_mode, RolloutLds2 lay) {
     using S = StaticShape<H, G8, SN, SU>;
     if constexpr (S::on)
-        rollout_v2_body<H, G8>(spec, st, S::L, P, bt, info, eps, test_mode, S::lay);
+        rollout_v2_body<H, G8>(spec, st, S::L, P, bt, info, eps, test_mode, S::lay, SU, SN, 5 + SU, true);
     else
-        rollout_v2_body<H, G8>(spec, st, L, P, bt, info, eps, test_mode, lay);
+        rollout_v2_body<H, G8>(spec, st, L, P, bt, info, eps, test_mode, lay, spec.U, spec.n_agents, spec.n_actions,
+                               false);
 }
 
 // ================================================================================================
@@ -1809,7 +1823,7 @@ __global__ void __launch_bounds__(256, 2) rollout_v6_kernel(MlgEnvSpec spec, Mlg
     const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
     const int e0 = blockIdx.x * REW, T1 = bt.T1;
     v2_prologue(spec, L, P, lay, smem, REW * N);
-    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info);
+    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info, spec.U, spec.n_agents, spec.n_actions, false);
     EnvLane E;
     env_lane_reset(C, st, E, wave * 2 + (lane >> 5), e0, hl);
     const int j = wave % HC, gi = wave / HC;
@@ -1861,7 +1875,7 @@ __global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel
     const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
     const int e0 = blockIdx.x * REW, T1 = bt.T1;
     v2_prologue(spec, L, P, lay, smem, REW * N);
-    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info);
+    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info, spec.U, spec.n_agents, spec.n_actions, false);
     // The two roles run separate copies of the phase loop (same uniform control state, same barrier count),
     // so the agent waves' weight registers and the env waves' unit registers are allocated over each other.
     // Phase state: tg[g] = next agent step of group g, pend[g] = env step tg[g] - 1 still to run.
