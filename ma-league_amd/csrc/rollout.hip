@@ -1064,62 +1064,39 @@ __device__ inline void ph_fc1_g8(const AgentLayout& L, const RolloutLds2& lay, f
                                  int tiles, int j, int ti0, int dt, int t, int lane) {
     const int col = lane & 15, g = lane >> 4, N = L.N, ldo = lay.ldo, ldh = lay.ldh, KK = (L.Dob + 31) / 32;
     const float* lobs = fm + lay.obs;
-    // Two tiles in flight per pass (the second clamped onto the first when the count is odd and its stores
-    // dropped): the two dependent chains (row map -> gathers -> MFMAs -> split) overlap instead of running back
-    // to back.
-    for (int ti = ti0; ti < tiles; ti += 2 * dt) {
+    for (int ti = ti0; ti < tiles; ti += dt) {
         int zero = 0;
         asm volatile("" : "+s"(zero));
-        const bool has2 = ti + dt < tiles;
-        const int tis[2] = {ti, has2 ? ti + dt : ti};
-        floatx4 acc[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int cr = tis[u] * 16 + col;
-            const int rm = rmap[cr];
-            const bool valid = rm & 1;
-            const int n = (rm >> 1) & 127, er = rmap_er(rm, N);
-            acc[u] = ld4(fm + lay.b1 + zero + j * 16 + 4 * g);
-            const int pa = (valid && t > 0) ? prev[er] : -1;
-            if (L.last_action && pa >= 0) acc[u] += ld4(fm + lay.w1a + pa * ldh + j * 16 + 4 * g);
-            if (L.agent_id) acc[u] += ld4(fm + lay.w1n + n * ldh + j * 16 + 4 * g);
-        }
+        const int cr = ti * 16 + col;
+        const int rm = rmap[cr];
+        const bool valid = rm & 1;
+        const int n = (rm >> 1) & 127, er = rmap_er(rm, N);
+        floatx4 acc = ld4(fm + lay.b1 + zero + j * 16 + 4 * g);
+        const int pa = (valid && t > 0) ? prev[er] : -1;
+        if (L.last_action && pa >= 0) acc += ld4(fm + lay.w1a + pa * ldh + j * 16 + 4 * g);
+        if (L.agent_id) acc += ld4(fm + lay.w1n + n * ldh + j * 16 + 4 * g);
         // bf16 obs row (exact) x W1 as three bf16 planes: 3 partial products per 32-wide K step, all exact, fp32
         // accumulation (the same fp32-class arithmetic as the GRU, §4a)
+        const bf16x8* orow = reinterpret_cast<const bf16x8*>(lobs + er * ldo) + g;
         const bf16x8* wrow = reinterpret_cast<const bf16x8*>(fm + lay.w1o + zero + (j * 16 + col) * ldo) + g;
         const int pl = L.H * ldo / 4;  // plane stride in bf16x8 units
-        const bf16x8* orow[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int er = rmap_er(rmap[tis[u] * 16 + col], N);
-            orow[u] = reinterpret_cast<const bf16x8*>(lobs + er * ldo) + g;
-        }
         for (int kk = 0; kk < KK; ++kk) {
-            const bf16x8 w2 = wrow[2 * pl + 4 * kk], w1 = wrow[pl + 4 * kk], w0 = wrow[4 * kk];
-            const bf16x8 b0 = orow[0][4 * kk], b1 = orow[1][4 * kk];
-            acc[0] = mfma_bf16(w2, b0, acc[0]);
-            acc[1] = mfma_bf16(w2, b1, acc[1]);
-            acc[0] = mfma_bf16(w1, b0, acc[0]);
-            acc[1] = mfma_bf16(w1, b1, acc[1]);
-            acc[0] = mfma_bf16(w0, b0, acc[0]);
-            acc[1] = mfma_bf16(w0, b1, acc[1]);
+            const bf16x8 b = orow[4 * kk];
+            acc = mfma_bf16(wrow[2 * pl + 4 * kk], b, acc);
+            acc = mfma_bf16(wrow[pl + 4 * kk], b, acc);
+            acc = mfma_bf16(wrow[4 * kk], b, acc);
         }
+        unsigned int* xr = reinterpret_cast<unsigned int*>(fm + lay.xb + cr * XPL_STRIDE) + (j * 16 + 4 * g) / 2;
+        float v[4] = {fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f), fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f)};
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (u == 1 && !has2) break;
-            const int cr = tis[u] * 16 + col;
-            unsigned int* xr = reinterpret_cast<unsigned int*>(fm + lay.xb + cr * XPL_STRIDE) + (j * 16 + 4 * g) / 2;
-            float v[4] = {fmaxf(acc[u][0], 0.f), fmaxf(acc[u][1], 0.f), fmaxf(acc[u][2], 0.f), fmaxf(acc[u][3], 0.f)};
-#pragma unroll
-            for (int lvl = 0; lvl < 3; ++lvl) {
-                const unsigned int a = cvt_pk_bf16(v[0], v[1]), b = cvt_pk_bf16(v[2], v[3]);
-                *reinterpret_cast<uint2*>(xr + lvl * 32) = make_uint2(a, b);
-                if (lvl < 2) {
-                    v[0] -= __uint_as_float(a << 16);
-                    v[1] -= __uint_as_float(a & 0xFFFF0000u);
-                    v[2] -= __uint_as_float(b << 16);
-                    v[3] -= __uint_as_float(b & 0xFFFF0000u);
-                }
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            const unsigned int a = cvt_pk_bf16(v[0], v[1]), b = cvt_pk_bf16(v[2], v[3]);
+            *reinterpret_cast<uint2*>(xr + lvl * 32) = make_uint2(a, b);
+            if (lvl < 2) {
+                v[0] -= __uint_as_float(a << 16);
+                v[1] -= __uint_as_float(a & 0xFFFF0000u);
+                v[2] -= __uint_as_float(b << 16);
+                v[3] -= __uint_as_float(b & 0xFFFF0000u);
             }
         }
     }
