@@ -645,6 +645,96 @@ struct Mixer {
     }
 };
 
+// The same QMixer forward with every weight operand of a stage loaded up front (one L2 round trip per stage
+// instead of one per 16-wide K chunk: the mix_td waves are L2-latency-bound, one wave per SIMD, so registers are
+// plentiful). State rows of at most SPC * 16 features, at most NMAX agents; identical arithmetic to Mixer. w1p
+// keeps the pre-abs hyper_w_1 outputs for the backward.
+template <int HE, int E, int SPC, int NMAX>
+struct MixerPF {
+    using Mx = Mixer<HE, E>;
+    static constexpr int T1H = Mx::T1H, TE = Mx::TE, L1T = Mx::L1T;
+    static constexpr int OW1 = Mx::OW1, OWF = Mx::OWF, OB1 = Mx::OB1, OVH = Mx::OVH;
+
+    __device__ static float forward(const MixPtrs& M, const MixPack& mp, int S, int N, const float* s, const float* qrow,
+                                    floatx4 (&l1)[L1T], floatx4 (&pre)[TE], floatx4 (&hid)[TE], floatx4 (&wfp)[TE],
+                                    floatx4 (&w1p)[NMAX][TE], int lane) {
+        const int col = lane & 15, g = lane >> 4;
+        {  // layer 1
+            floatx4 sv[SPC], wl[L1T][SPC];
+#pragma unroll
+            for (int kc = 0; kc < SPC; ++kc) sv[kc] = load_chunk(s, kc * 16 + 4 * g, S);
+#pragma unroll
+            for (int mt = 0; mt < L1T; ++mt) {
+                l1[mt] = ld4(M.mb1 + mt * 16 + 4 * g);
+#pragma unroll
+                for (int kc = 0; kc < SPC; ++kc) wl[mt][kc] = ld4(M.m1 + (int64_t)(mt * 16 + col) * mp.Sp + kc * 16 + 4 * g);
+            }
+#pragma unroll
+            for (int kc = 0; kc < SPC; ++kc)
+#pragma unroll
+                for (int mt = 0; mt < L1T; ++mt) l1[mt] = mfma_chunk(wl[mt][kc], sv[kc], l1[mt]);
+#pragma unroll
+            for (int mt = 0; mt < L1T; ++mt) {
+                if (mt >= OB1 && mt < OVH) continue;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) l1[mt][q] = fmaxf(l1[mt][q], 0.f);
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) pre[cc] = l1[OB1 + cc];
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) {  // hyper_w_1 second layer for every agent: weights of all agents first
+            if (n >= N) break;
+            floatx4 wa[TE][T1H];
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc) {
+                w1p[n][cc] = ld4(M.ba2 + n * E + cc * 16 + 4 * g);
+#pragma unroll
+                for (int kc = 0; kc < T1H; ++kc)
+                    wa[cc][kc] = ld4(M.a2 + (int64_t)(n * E + cc * 16 + col) * HE + kc * 16 + 4 * g);
+            }
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc)
+#pragma unroll
+                for (int kc = 0; kc < T1H; ++kc) w1p[n][cc] = mfma_chunk(wa[cc][kc], l1[OW1 + kc], w1p[n][cc]);
+        }
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) {
+            if (n >= N) break;
+            const float qn = qrow[n];
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pre[cc][q] += qn * fabsf(w1p[n][cc][q]);
+        }
+        floatx4 wf[TE][T1H], wv[TE];
+        floatx4 bv = ld4(M.bv2p + 4 * g);
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) {
+            wfp[cc] = ld4(M.bf2 + cc * 16 + 4 * g);
+            wv[cc] = ld4(M.v2p + (int64_t)col * E + cc * 16 + 4 * g);
+#pragma unroll
+            for (int kc = 0; kc < T1H; ++kc) wf[cc][kc] = ld4(M.f2 + (int64_t)(cc * 16 + col) * HE + kc * 16 + 4 * g);
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) {
+#pragma unroll
+            for (int kc = 0; kc < T1H; ++kc) wfp[cc] = mfma_chunk(wf[cc][kc], l1[OWF + kc], wfp[cc]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                hid[cc][q] = pre[cc][q] > 0.f ? pre[cc][q] : expm1f(pre[cc][q]);
+                part += hid[cc][q] * fabsf(wfp[cc][q]);
+            }
+        }
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+#pragma unroll
+        for (int kc = 0; kc < TE; ++kc) bv = mfma_chunk(wv[kc], l1[OVH + kc], bv);
+        return part + __shfl(bv[0], col);
+    }
+};
+
 __device__ __forceinline__ float row_sum16(float v) {  // sum over the 16 lanes of lane group 0
     v += __shfl_xor(v, 1);
     v += __shfl_xor(v, 2);
@@ -683,17 +773,81 @@ __device__ __forceinline__ void gather_q(const LCfg& c, const MlgBatch& bt, cons
     }
 }
 
+constexpr int MIXPF_N = 8, MIXPF_A = 16;  // mix_td FAST path bounds (agents, actions)
+
+// gather_q with every load of an agent issued together (A <= AMAX): avail row, online next-step Q, target
+// next-step Q; same selection rule and order as gather_q.
+template <int AMAX>
+__device__ __forceinline__ void gather_q_pf(const LCfg& c, const MlgBatch& bt, const float* mac, const float* tmac, int b,
+                                            int t, float* cq, float* tq) {
+    const int N = c.N, A = c.A, R = c.R;
+    const int64_t row0 = (bslot(bt, b) * bt.T1 + t) * N;
+#pragma unroll
+    for (int n = 0; n < MIXPF_N; ++n) {  // unrolled: cq / tq stay in registers
+        if (n >= N) break;
+        const int r = b * N + n;
+        const int a = (int)bt.actions[row0 + n];
+        const int32_t* av = bt.avail + (bslot(bt, b) * bt.T1 + t + 1) * N * A + (int64_t)n * A;
+        const float* qn = mac + ((int64_t)(t + 1) * R + r) * A;
+        const float* tn = tmac + ((int64_t)(t + 1) * R + r) * A;
+        int avv[AMAX];
+        float qv[AMAX], tv[AMAX];
+#pragma unroll
+        for (int k = 0; k < AMAX; ++k) {
+            const bool in = k < A;
+            avv[k] = in ? av[k] : 0;
+            qv[k] = in ? qn[k] : 0.f;
+            tv[k] = in ? tn[k] : 0.f;
+        }
+        cq[n] = mac[((int64_t)t * R + r) * A + a];
+        if (c.double_q) {
+            float bv = 0.f;
+            int bi = 0;
+#pragma unroll
+            for (int k = 0; k < AMAX; ++k) {
+                if (k >= A) break;
+                const float v = avv[k] ? qv[k] : -9999999.f;
+                const bool take = k == 0 || v > bv;
+                bv = take ? v : bv;
+                bi = take ? k : bi;
+            }
+            float tb = 0.f;
+            int ab = 0;
+#pragma unroll
+            for (int k = 0; k < AMAX; ++k) {  // tv[bi], avv[bi] without dynamic register indexing
+                tb = k == bi ? tv[k] : tb;
+                ab = k == bi ? avv[k] : ab;
+            }
+            tq[n] = ab ? tb : -9999999.f;
+        } else {
+            float bv = 0.f;
+#pragma unroll
+            for (int k = 0; k < AMAX; ++k) {
+                if (k >= A) break;
+                const float v = avv[k] ? tv[k] : -9999999.f;
+                bv = (k == 0 || v > bv) ? v : bv;
+            }
+            tq[n] = bv;
+        }
+    }
+}
+
 constexpr int MAXN = 32;
 
 struct MixOut {
     float *srow, *l1act, *d1, *da2, *df2, *dv2, *dq, *d2, *part;
 };
 
-template <int HE, int E>
+// FAST (state rows of <= 64 features, <= 8 agents, <= 16 actions): the prefetching mixer forward (MixerPF), the
+// backward reusing its hyper_w_1 outputs with the W_a2^T / W_f2^T operands loaded up front, gather_q_pf.
+// Identical arithmetic either way.
+template <int HE, int E, bool FAST = false>
 __global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtrs Mon, MixPtrs Mtg, MixPack mp,
                                                     const float* __restrict__ mac, const float* __restrict__ tmac,
                                                     const float* __restrict__ msum_p, MixOut o) {
     using Mx = Mixer<HE, E>;
+    using MP = MixerPF<HE, E, 4, MIXPF_N>;
+    floatx4 w1c[MIXPF_N][Mx::TE];  // FAST: the online forward's pre-abs hyper_w_1 outputs
     // two waves per 16-row tile: wave 0 runs the target mixer forward and hands y's target to wave 1 through LDS,
     // wave 1 runs the online forward, TD and the mixer backward (VDN: wave 1 alone)
     __shared__ float tgt_sh[16];
@@ -706,7 +860,12 @@ __global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtr
     const int N = c.N, S = c.S, L1 = 2 * HE + 2 * E, NE = N * E;
     float cq[MAXN], tq[MAXN];
     for (int n = 0; n < N; ++n) cq[n] = tq[n] = 0.f;
-    if (valid) gather_q(c, bt, mac, tmac, b, t, cq, tq);
+    if (valid) {
+        if constexpr (FAST)
+            gather_q_pf<MIXPF_A>(c, bt, mac, tmac, b, t, cq, tq);
+        else
+            gather_q(c, bt, mac, tmac, b, t, cq, tq);
+    }
     const float m = (valid && t < t_eff(msum_p) - 1) ? mask_at(bt, b, t) : 0.f;  // reference truncation
     const float rwd = valid ? bt.reward[bslot(bt, b) * bt.T1 + t] : 0.f;
     const float term = valid ? (float)bt.terminated[bslot(bt, b) * bt.T1 + t] : 0.f;
@@ -718,11 +877,20 @@ __global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtr
     if (c.mixer == 2) {
         if (wv == 0) {
             floatx4 tl1[Mx::L1T], tpre[Mx::TE], thid[Mx::TE], twfp[Mx::TE];
-            const float tv = Mx::forward(Mtg, mp, S, N, s1, tq, tl1, tpre, thid, twfp, lane);
+            float tv;
+            if constexpr (FAST) {
+                floatx4 tw1c[MIXPF_N][Mx::TE];
+                tv = MP::forward(Mtg, mp, S, N, s1, tq, tl1, tpre, thid, twfp, tw1c, lane);
+            } else {
+                tv = Mx::forward(Mtg, mp, S, N, s1, tq, tl1, tpre, thid, twfp, lane);
+            }
             if (g == 0) tgt_sh[col] = tv;
             qtot = 0.f;
         } else {
-            qtot = Mx::forward(Mon, mp, S, N, s0, cq, l1, pre, hid, wfp, lane);
+            if constexpr (FAST)
+                qtot = MP::forward(Mon, mp, S, N, s0, cq, l1, pre, hid, wfp, w1c, lane);
+            else
+                qtot = Mx::forward(Mon, mp, S, N, s0, cq, l1, pre, hid, wfp, lane);
         }
         __syncthreads();
         if (wv == 0) return;
@@ -773,9 +941,26 @@ __global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtr
         for (int mt = 0; mt < Mx::T1H; ++mt) dw1h[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
         for (int n = 0; n < N; ++n) {
             float part = 0.f;
+            floatx4 aT[Mx::TE][Mx::T1H];  // FAST: this agent's W_a2^T operands, loaded before its MFMAs
+            if constexpr (FAST) {
+#pragma unroll
+                for (int cc = 0; cc < Mx::TE; ++cc)
+#pragma unroll
+                    for (int mt = 0; mt < Mx::T1H; ++mt)
+                        aT[cc][mt] = ld4(Mon.a2T + (int64_t)(mt * 16 + col) * NE + n * E + cc * 16 + 4 * g);
+            }
 #pragma unroll
             for (int cc = 0; cc < Mx::TE; ++cc) {
-                const floatx4 wp = Mx::w1pre(Mon, n, cc, l1, lane);
+                floatx4 wp;
+                if constexpr (FAST) {
+                    floatx4 wsel = w1c[0][cc];  // w1c[n][cc] without dynamic register indexing
+#pragma unroll
+                    for (int k = 1; k < MIXPF_N; ++k)
+                        if (k == n) wsel = w1c[k][cc];
+                    wp = wsel;
+                } else {
+                    wp = Mx::w1pre(Mon, n, cc, l1, lane);
+                }
                 floatx4 dlt;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -786,8 +971,14 @@ __global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtr
                 if (valid) *reinterpret_cast<floatx4*>(o.da2 + (int64_t)rm * NE + n * E + cc * 16 + 4 * g) = dlt;
                 // dw1h += W_a2^T[:, n*E + cc*16 ..] . dlt   (a2T is [HE][NE])
 #pragma unroll
-                for (int mt = 0; mt < Mx::T1H; ++mt)
-                    dw1h[mt] = mfma_chunk(ld4(Mon.a2T + (int64_t)(mt * 16 + col) * NE + n * E + cc * 16 + 4 * g), dlt, dw1h[mt]);
+                for (int mt = 0; mt < Mx::T1H; ++mt) {
+                    floatx4 wa;
+                    if constexpr (FAST)
+                        wa = aT[cc][mt];
+                    else
+                        wa = ld4(Mon.a2T + (int64_t)(mt * 16 + col) * NE + n * E + cc * 16 + 4 * g);
+                    dw1h[mt] = mfma_chunk(wa, dlt, dw1h[mt]);
+                }
             }
             part += __shfl_xor(part, 16);
             part += __shfl_xor(part, 32);
@@ -1370,8 +1561,12 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
                        ws + p.w.p_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum);
     MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
               ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
-    hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, Mtg, p.mp,
-                       ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
+    if (p.mp.Sp <= 64 && c.N <= MIXPF_N && c.A <= MIXPF_A && !getenv("MLG_MIX_GENERIC"))
+        hipLaunchKernelGGL((mix_td_kernel<64, 32, true>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, Mtg, p.mp,
+                           ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
+    else
+        hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, Mtg, p.mp,
+                           ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
     if (rec16)
         hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                            ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi,
