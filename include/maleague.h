@@ -295,6 +295,8 @@ int mlg_refil_train(const MlgRefilLearnerCfg *c, const MlgRefilLearnerBufs *b, v
 /* Diagnostic builds only (-DMLG_STAMPS): device buffer [grid][8 waves][16] u64 of per-phase cycle counts
  * of mlg_rollout. Returns nonzero in normal builds. */
 int mlg_debug_set_stamps(void *ptr);
+/* Diagnostic builds only (-DMLG_STAMPS): per-wave phase cycle counters of the learner recurrences. */
+int mlg_debug_set_learner_stamps(void *ptr);
 int mlg_refil_debug_set_stamps(void *ptr); /* same for mlg_refil_rollout: [grid][16] u64 */
 
 const char *mlg_last_error(void);

@@ -251,7 +251,54 @@ __global__ void __launch_bounds__(1024) prep_kernel(PrepJob J) {
     }
 }
 
+
+#ifdef MLG_STAMPS
+// Diagnostic build only (-DMLG_STAMPS): per-wave cycle counts of the recurrences' step phases, written to
+// g_mlg_lstamps[kernel][block][wave][8] (slots 0..5 phases, 6 = steps, 7 = whole kernel).
+__device__ unsigned long long* g_mlg_lstamps = nullptr;
+struct LStamps {
+    unsigned long long acc[6], last, begin, steps;
+    __device__ void init() {
+        for (int k = 0; k < 6; ++k) acc[k] = 0;
+        steps = 0;
+        last = begin = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void mark(int k) {
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - last;
+        last = now;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __device__ void flush(int kid) {
+        if ((threadIdx.x & 63) || !g_mlg_lstamps) return;
+        unsigned long long* o = g_mlg_lstamps + (((int64_t)kid * 1024 + blockIdx.x) * 8 + (threadIdx.x >> 6)) * 8;
+        for (int k = 0; k < 6; ++k) o[k] = acc[k];
+        o[6] = steps;
+        o[7] = __builtin_amdgcn_s_memtime() - begin;
+    }
+};
+#else
+struct LStamps {
+    unsigned long long steps;
+    __device__ void init() {}
+    __device__ void mark(int) {}
+    __device__ void flush(int) {}
+};
+#endif
+#ifdef MLG_TE_CAP  // timing variant builds only (wrong results): cap the recurrences' step count
+__device__ __forceinline__ int t_eff(const float* msum) { return min((int)msum[1], MLG_TE_CAP); }
+#else
 __device__ __forceinline__ int t_eff(const float* msum) { return (int)msum[1]; }
+#endif
+
+// prefetch depth (steps) of the recurrences' per-step operand rings (even: the LDS double buffer alternates)
+#ifndef MLG_REC_PD
+#define MLG_REC_PD 4
+#endif
+#ifndef MLG_BWD_PD
+#define MLG_BWD_PD 4
+#endif
 
 // ================================================================================================
 // 16-row x 16-feature tile product with the activation operand in LDS, row-major [16][lda]:
@@ -425,7 +472,8 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
 // per CU is MFMA-bound at 48 16x16x4 MFMAs per SIMD per step; 4-row tiles put 4x as many CUs on the
 // sequential T loop. Wave w owns hidden features 16w..16w+15: block b = 4g + fg computes gate g (r, z, W_hn h;
 // g = 3 idle) of features 16w + 4fg + i for the tile's 4 rows, W_hh rows of the block in VGPRs (H per lane).
-// Lanes 0..15 then gather z and W_hn h from lanes +16 / +32 and finish the GRU cell for (feature, row).
+// A row / register transpose across the wave's four 16-lane rows (rows_transpose4, four VALU lane swaps) then
+// gives every lane the three gates of one (feature 16w + 4fg + g, row): all 64 lanes finish one GRU cell each.
 // grid (2 * ntiles4): blockIdx < ntiles4 online (saves gates), else target. H/16 waves.
 template <int H>
 __global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
@@ -436,6 +484,8 @@ __global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, 
                                                          float* __restrict__ ws_ghn, const float* __restrict__ msum) {
     constexpr int LDA = H + 4;
     __shared__ __attribute__((aligned(16))) float hs[2][4 * LDA];
+    LStamps lst;
+    lst.init();
     const int Te = t_eff(msum);
     const int nt4 = (c.R + 3) / 4;
     const bool online = blockIdx.x < nt4;
@@ -452,6 +502,7 @@ __global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, 
     const int rr = valid ? r : 0;
     const int fA = 16 * w + 4 * fg + q;  // A operand: feature row of W_hh for this lane (i = q)
     const int fD = 16 * w + 4 * fg;      // D: features fD..fD+3 of gate g at row r
+    const int f = fD + g;                // after the transpose: the lane's cell is (feature f, row r)
     float wa[H];
 #pragma unroll
     for (int k4 = 0; k4 < H / 4; ++k4) {
@@ -463,22 +514,24 @@ __global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, 
     }
     const floatx4 bhn = ld4(P + L.bhh + 2 * H + fD);
     for (int i = tid; i < 4 * LDA; i += blockDim.x) hs[0][i] = 0.f;
-    const bool lead = g == 0;  // lanes 0..15: finish the cell for (features fD.., row r)
-    st4_if(mlg_rsrc(hsg), (int64_t)rr * H + fD, floatx4{0.f, 0.f, 0.f, 0.f}, lead && valid);  // HS[0]
-    // per-step inputs: this lane's gate part of GI (r for g = 0, z for g = 1) and the n part (used by g = 0)
+    const __amdgpu_buffer_rsrc_t rs_gi = mlg_rsrc(gi), rs_h = mlg_rsrc(hsg), rs_r = mlg_rsrc(ws_gr),
+                                 rs_z = mlg_rsrc(ws_gz), rs_n = mlg_rsrc(ws_gn), rs_hn = mlg_rsrc(ws_ghn);
+    st1_rs(rs_h, valid ? (rr * H + f) * 4 : (int)0x80000000u, 0, 0.f);  // HS[0]
+    // per-step inputs: the MFMA init of rows 0 / 1 (GI r / z part of features fD..) and the lane's GI n element
     const int gq = g == 1 ? 1 : 0;
-    auto gi_at = [&](int t, int part) { return ld4(gi + ((int64_t)t * R + rr) * 3 * H + part * H + fD); };
-    const __amdgpu_buffer_rsrc_t rs_h = mlg_rsrc(hsg), rs_r = mlg_rsrc(ws_gr), rs_z = mlg_rsrc(ws_gz),
-                                 rs_n = mlg_rsrc(ws_gn), rs_hn = mlg_rsrc(ws_ghn);
+    const int vo_gp = (rr * 3 * H + gq * H + fD) * 4, vo_gn = (rr * 3 * H + 2 * H + f) * 4;
     struct In {
-        floatx4 gp, gn;
+        floatx4 gp;
+        float gn;
     };
     auto load_in = [&](int t, In& d) {
-        d.gp = gi_at(t, gq);
-        d.gn = gi_at(t, 2);
+        const int so = t * R * 3 * H * 4;
+        d.gp = ld4_rs(rs_gi, vo_gp, so);
+        d.gn = ld1_rs(rs_gi, vo_gn, so);
     };
-    auto step = [&](int t, const In& in, In& nx, int cur) {
-        load_in(t + 1 < Te ? t + 1 : t, nx);  // unconditional (clamped) prefetch
+    const int vo_st = valid ? (rr * H + f) * 4 : (int)0x80000000u;
+    float hprev = 0.f;  // h_{t-1} of the lane's cell: its own previous output
+    auto step = [&](int t, const In& in, int cur) {
         const float* hrow = hs[cur] + q * LDA;
         floatx4 hv[H / 4];  // the whole h row first: the MFMA chain then never waits on LDS
 #pragma unroll
@@ -494,39 +547,48 @@ __global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, 
             }
         }
         const floatx4 acc = acc0 + acc1;
-        floatx4 az, ahn;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            az[e] = __shfl(acc[e], lane + 16, 64);
-            ahn[e] = __shfl(acc[e], lane + 32, 64);
-        }
-        const floatx4 hp = ld4(hs[cur] + q * LDA + fD);
-        floatx4 rg, zg, ng, hn;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            rg[e] = fast_sigmoid(acc[e]);
-            zg[e] = fast_sigmoid(az[e]);
-            ng[e] = fast_tanh(in.gn[e] + rg[e] * ahn[e]);
-            hn[e] = ng[e] + zg[e] * (hp[e] - ng[e]);
-        }
-        if (lead) *reinterpret_cast<floatx4*>(hs[cur ^ 1] + q * LDA + fD) = hn;
-        const int64_t o = ((int64_t)t * R + r) * H + fD;
-        const bool keep = lead && valid;
-        st4_if(rs_h, o + (int64_t)R * H, hn, keep);  // HS[t + 1]
-        st4_if(rs_r, o, rg, keep && online);
-        st4_if(rs_z, o, zg, keep && online);
-        st4_if(rs_n, o, ng, keep && online);
-        st4_if(rs_hn, o, ahn, keep && online);
+        float ar = acc[0], az = acc[1], ahn = acc[2], a3 = acc[3];
+        rows_transpose4(ar, az, ahn, a3);  // gate g of (feature f, row r) now in register g
+        lst.mark(0);
+        const float rg = fast_sigmoid(ar), zg = fast_sigmoid(az);
+        const float ng = fast_tanh(in.gn + rg * ahn);
+        const float hn = ng + zg * (hprev - ng);
+        hs[cur ^ 1][q * LDA + f] = hn;
+        hprev = hn;
+        lst.mark(2);
+        const int vo = t < Te ? vo_st : (int)0x80000000u;  // t >= Te: padding step (see below)
+        const int vg = online ? vo : (int)0x80000000u;
+        const int so = (t < Te ? t : 0) * R * H * 4;
+        st1_rs(rs_h, vo, so + R * H * 4, hn);  // HS[t + 1]
+        st1_rs(rs_r, vg, so, rg);
+        st1_rs(rs_z, vg, so, zg);
+        st1_rs(rs_n, vg, so, ng);
+        st1_rs(rs_hn, vg, so, ahn);
+        lst.mark(3);
         __syncthreads();
+        lst.mark(4);
+        ++lst.steps;
     };
-    In ia, ib;
-    load_in(0, ia);
+    // GI rows are prefetched MLG_REC_PD steps ahead (clamped, unconditional loads) into a register ring. The step
+    // count is padded to a multiple of MLG_REC_PD (padding steps store nothing): no control flow inside the
+    // unrolled body, so every ring slot keeps its registers and the loads are waited for only where consumed.
+    In ring[MLG_REC_PD];
+#pragma unroll
+    for (int i = 0; i < MLG_REC_PD; ++i) load_in(i < Te ? i : Te - 1, ring[i]);
     __syncthreads();
-    step(0, ia, ib, 0);  // peeled (see agent_rec_kernel)
-    for (int t = 1; t < Te; t += 2) {
-        step(t, ib, ia, 1);
-        if (t + 1 < Te) step(t + 1, ia, ib, 0);
+    lst.mark(5);
+    for (int t0 = 0; t0 < Te; t0 += MLG_REC_PD) {
+#pragma unroll
+        for (int i = 0; i < MLG_REC_PD; ++i) {
+            const int t = t0 + i;
+            step(t, ring[i], i & 1);
+            // refill the slot only once the step has consumed it: the load then targets the slot's own registers
+            // (no register rotation at the loop back-edge, which would wait for every load in flight)
+            load_in(t + MLG_REC_PD < Te ? t + MLG_REC_PD : Te - 1, ring[i]);
+            lst.mark(1);
+        }
     }
+    lst.flush(0);
 }
 
 // grid (ntiles, T, 2), Ap/16 waves: wave = action tile. q = b2 + W2 . h_t (h_t = HS[t + 1]).
@@ -1149,8 +1211,9 @@ __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, Age
 
 // The backward recurrence on 4-row tiles (v_mfma_f32_4x4x1_16b_f32, as agent_rec4_kernel). Wave w owns hidden
 // features 16w..16w+15; block b = 4kq + fg accumulates W_hh^T dGH for features 16w + 4fg + i over the K quarter
-// kq (48 of the 3H gate rows, W_hh columns in VGPRs); the four quarter partials are summed across lanes
-// (+16, +32, +48) into lanes 0..15, which own (features 16w + 4fg.., row) for the elementwise GRU backward.
+// kq (48 of the 3H gate rows, W_hh columns in VGPRs). The four quarter partials are summed across the wave's
+// 16-lane rows with a transposing reduction (rows_sum_transpose4): lane (row kq, fg, j) ends up owning feature
+// 16w + 4fg + kq of row j, so all 64 lanes run the elementwise GRU backward, one (feature, row) each.
 // grid (ntiles4), H/16 waves.
 template <int H>
 __global__ void __launch_bounds__(512) agent_bwd4_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ P,
@@ -1167,79 +1230,101 @@ __global__ void __launch_bounds__(512) agent_bwd4_kernel(LCfg c, MlgBatch bt, Ag
     const int blk = lane >> 2, q = lane & 3, kq = blk >> 2, fg = blk & 3;
     const int r = blockIdx.x * 4 + q;
     const bool valid = r < c.R;
-    const bool lead = kq == 0;  // lanes 0..15 own (features fD.., row r) after the cross-lane K reduction
     const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
     const int R = c.R, N = c.N;
     const int fD = 16 * w + 4 * fg;
+    const int f = fD + kq;  // the lane's (feature, row) after the reduction
+    LStamps lst;
+    lst.init();
+    const int Te = t_eff(msum);
+    const int rr = valid ? r : 0;
+    const int64_t abase = bslot(bt, b) * bt.T1 * N + n;
+    struct Raw {  // per-step operands as stored by the forward, for (feature f, row r)
+        float rg, zg, ng, ghn, hp, dq;
+        int a;
+    };
+    // Buffer loads: the lane part of every offset is fixed, the step part is a wave-uniform SGPR offset, so a
+    // step's loads cost no VALU address arithmetic.
+    const __amdgpu_buffer_rsrc_t rs_r = mlg_rsrc(ws_gr), rs_z = mlg_rsrc(ws_gz), rs_n = mlg_rsrc(ws_gn),
+                                 rs_hn = mlg_rsrc(ws_ghn), rs_hs = mlg_rsrc(ws_hs), rs_dq = mlg_rsrc(dqv),
+                                 rs_act = mlg_rsrc(reinterpret_cast<const float*>(bt.actions));
+    const int vo_g = (rr * H + f) * 4, vo_dq = rr * 4, vo_act = (int)(abase * 8);
+    auto load_raw = [&](int t, Raw& s) {
+        const int so = t * R * H * 4;
+        s.rg = ld1_rs(rs_r, vo_g, so);
+        s.zg = ld1_rs(rs_z, vo_g, so);
+        s.ng = ld1_rs(rs_n, vo_g, so);
+        s.ghn = ld1_rs(rs_hn, vo_g, so);
+        s.hp = ld1_rs(rs_hs, vo_g, so);  // HS[t] = h_{t-1}
+        const int tq = t < c.T - 1 ? t : c.T - 2;
+        s.dq = ld1_rs(rs_dq, vo_dq, tq * R * 4);
+        // 32-bit load of the action's low word (little-endian int64), unconditional: no branch around it, and no
+        // dead high half whose pending load would block the reuse of its register
+        const int act = __float_as_int(ld1_rs(rs_act, vo_act, tq * N * 8));
+        s.a = t < c.T - 1 ? act : -1;
+    };
+    // the first steps' operands are requested before anything else is queued on the vector memory path
+    Raw ring[MLG_BWD_PD];
+#pragma unroll
+    for (int i = 0; i < MLG_BWD_PD; ++i) load_raw(Te - 1 - i > 0 ? Te - 1 - i : 0, ring[i]);
     float wt[KQ];  // A operand: W_hh[kq * KQ + kk][fD + i] (i = q)
 #pragma unroll
     for (int kk = 0; kk < KQ; ++kk) wt[kk] = P[L.whh + (int64_t)(kq * KQ + kk) * H + fD + q];
-    const int rr = valid ? r : 0;
     for (int i = tid; i < c.A * H; i += blockDim.x) w2s[i] = P[L.w2 + i];  // fc2 rows for dh += dq W2[a]
-    const int64_t abase = bslot(bt, b) * bt.T1 * N + n;
-    struct Step {
-        floatx4 rg, zg, ng, ghn, hp;
-        float dq;
-        int a;
-    };
-    auto load_step = [&](int t, Step& s) {
-        const int64_t o = ((int64_t)t * R + rr) * H + fD;
-        s.rg = ld4(ws_gr + o);
-        s.zg = ld4(ws_gz + o);
-        s.ng = ld4(ws_gn + o);
-        s.ghn = ld4(ws_ghn + o);
-        s.hp = ld4(ws_hs + o);  // HS[t] = h_{t-1}
-        const int tq = t < c.T - 1 ? t : c.T - 2;
-        s.dq = dqv[(int64_t)tq * R + rr];
-        s.a = t < c.T - 1 ? (int)bt.actions[abase + (int64_t)tq * N] : -1;
-    };
-    const int Te = t_eff(msum);
-    if (valid && lead) {  // steps past max_t_filled: zero deltas (wgrad rows)
+    {  // steps past max_t_filled: zero deltas (wgrad rows); the tile's rows are contiguous per step
+        const int nv = min(4, R - (int)blockIdx.x * 4) * 3 * H / 4;  // float4s per step and array
         for (int t = Te; t < c.T; ++t) {
-            const int64_t o3 = ((int64_t)t * R + r) * 3 * H + fD;
-#pragma unroll
-            for (int gq = 0; gq < 3; ++gq) {
-                *reinterpret_cast<floatx4*>(dgi + o3 + gq * H) = floatx4{0.f, 0.f, 0.f, 0.f};
-                *reinterpret_cast<floatx4*>(dgh + o3 + gq * H) = floatx4{0.f, 0.f, 0.f, 0.f};
+            float* zi = dgi + ((int64_t)t * R + blockIdx.x * 4) * 3 * H;
+            float* zh = dgh + ((int64_t)t * R + blockIdx.x * 4) * 3 * H;
+            for (int i = tid; i < nv; i += blockDim.x) {
+                reinterpret_cast<floatx4*>(zi)[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+                reinterpret_cast<floatx4*>(zh)[i] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
         }
     }
-    floatx4 dh = {0.f, 0.f, 0.f, 0.f};
+    // Every gate delta is dh times a factor of the saved activations (the GRU backward is linear in dh), and the
+    // fc2 term dq W2[a] does not depend on dh either: both are formed one step ahead, off the dh -> dh chain.
+    struct Coef {
+        float cr, cz, cn, chn, ch, dw;
+    };
+    auto coef = [&](const Raw& s, Coef& k) {
+        const bool take = valid && s.a >= 0;
+        const float w2 = w2s[(take ? s.a : 0) * H + f];
+        const float cn = (1.f - s.zg) * (1.f - s.ng * s.ng);  // dn' = dh (1 - z)(1 - n^2)
+        k.cn = cn;
+        k.cr = cn * s.ghn * (s.rg * (1.f - s.rg));      // dr' = dn' (W_hn h + b_hn) r (1 - r)
+        k.cz = (s.hp - s.ng) * (s.zg * (1.f - s.zg));  // dz' = dh (h_{t-1} - n) z (1 - z)
+        k.chn = cn * s.rg;                              // d(W_hn h + b_hn) = dn' r
+        k.ch = s.zg;                                    // direct path dh_{t-1} += dh z
+        k.dw = (take ? s.dq : 0.f) * w2;
+    };
+    float dh = 0.f;
     const __amdgpu_buffer_rsrc_t rs_gi = mlg_rsrc(dgi), rs_gh = mlg_rsrc(dgh);
-    auto step = [&](int t, const Step& s, Step& nx, int cur) {
-        load_step(t > 0 ? t - 1 : 0, nx);
-        if (valid && s.a >= 0) dh += s.dq * ld4(w2s + s.a * H + fD);
-        floatx4 drp, dzp, dnp, dghn, dhd;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float dn = dh[e] * (1.f - s.zg[e]);
-            const float dz = dh[e] * (s.hp[e] - s.ng[e]);
-            dhd[e] = dh[e] * s.zg[e];
-            dnp[e] = dn * (1.f - s.ng[e] * s.ng[e]);
-            const float dr = dnp[e] * s.ghn[e];
-            drp[e] = dr * s.rg[e] * (1.f - s.rg[e]);
-            dzp[e] = dz * s.zg[e] * (1.f - s.zg[e]);
-            dghn[e] = dnp[e] * s.rg[e];
-        }
-        if (lead) {
-            float* gh = sgh[cur] + q * LDG;
-            *reinterpret_cast<floatx4*>(gh + fD) = drp;
-            *reinterpret_cast<floatx4*>(gh + H + fD) = dzp;
-            *reinterpret_cast<floatx4*>(gh + 2 * H + fD) = dghn;
-        }
-        const int64_t o3 = ((int64_t)t * R + r) * 3 * H + fD;
-        const bool keep = valid && lead;
-        st4_if(rs_gi, o3, drp, keep);
-        st4_if(rs_gi, o3 + H, dzp, keep);
-        st4_if(rs_gi, o3 + 2 * H, dnp, keep);
-        st4_if(rs_gh, o3, drp, keep);
-        st4_if(rs_gh, o3 + H, dzp, keep);
-        st4_if(rs_gh, o3 + 2 * H, dghn, keep);
+    const int vo_st = valid ? (r * 3 * H + f) * 4 : (int)0x80000000u;
+    auto step = [&](int t, const Coef& k, int cur) {
+        dh += k.dw;
+        const float drp = dh * k.cr, dzp = dh * k.cz, dnp = dh * k.cn, dghn = dh * k.chn, dhd = dh * k.ch;
+        float* gh = sgh[cur] + q * LDG + f;
+        gh[0] = drp;
+        gh[H] = dzp;
+        gh[2 * H] = dghn;
+        lst.mark(2);
         __syncthreads();
+        lst.mark(4);
         const float* ghr = sgh[cur] + q * LDG + kq * KQ;
         floatx4 gv[KQ / 4];
 #pragma unroll
         for (int k4 = 0; k4 < KQ / 4; ++k4) gv[k4] = ld4(ghr + 4 * k4);
+        // the step's global stores go out behind the barrier, in the shadow of the MFMA chain
+        const int vo = t >= 0 ? vo_st : (int)0x80000000u;  // t < 0: padding step, every lane dropped
+        const int so = (t >= 0 ? t : 0) * R * 3 * H * 4;
+        st1_rs(rs_gi, vo, so, drp);
+        st1_rs(rs_gi, vo, so + H * 4, dzp);
+        st1_rs(rs_gi, vo, so + 2 * H * 4, dnp);
+        st1_rs(rs_gh, vo, so, drp);
+        st1_rs(rs_gh, vo, so + H * 4, dzp);
+        st1_rs(rs_gh, vo, so + 2 * H * 4, dghn);
+        lst.mark(3);
         floatx4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k4 = 0; k4 < KQ / 4; k4 += 2) {
@@ -1249,20 +1334,29 @@ __global__ void __launch_bounds__(512) agent_bwd4_kernel(LCfg c, MlgBatch bt, Ag
                 p1 = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[4 * k4 + 4 + e], gv[k4 + 1][e], p1, 0, 0, 0);
             }
         }
-        floatx4 part = p0 + p1, dprev = dhd;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            dprev[e] += (part[e] + __shfl(part[e], lane + 16, 64)) +
-                        (__shfl(part[e], lane + 32, 64) + __shfl(part[e], lane + 48, 64));
-        dh = dprev;
+        const floatx4 part = p0 + p1;
+        dh = dhd + rows_sum_transpose4(part[0], part[1], part[2], part[3]);  // (q0 + q1) + (q2 + q3)
+        lst.mark(0);
+        ++lst.steps;
     };
-    Step sa, sb;
-    load_step(Te - 1, sa);
-    step(Te - 1, sa, sb, 0);  // peeled (see agent_rec_kernel)
-    for (int t = Te - 2; t >= 0; t -= 2) {
-        step(t, sb, sa, 1);
-        if (t > 0) step(t - 1, sa, sb, 0);
+    __syncthreads();  // w2s staged
+    Coef kc;
+    coef(ring[0], kc);
+    lst.mark(5);
+    // step count padded to a multiple of MLG_BWD_PD (padding steps t < 0 store nothing; see agent_rec4_kernel)
+    for (int t0 = Te - 1; t0 >= 0; t0 -= MLG_BWD_PD) {
+#pragma unroll
+        for (int i = 0; i < MLG_BWD_PD; ++i) {
+            const int t = t0 - i;
+            load_raw(t - MLG_BWD_PD > 0 ? t - MLG_BWD_PD : 0, ring[i]);  // slot i (step t) is consumed
+            Coef kn;
+            coef(ring[(i + 1) % MLG_BWD_PD], kn);  // step t - 1
+            lst.mark(1);
+            step(t, kc, i & 1);
+            kc = kn;
+        }
     }
+    lst.flush(1);
 }
 
 // dA = (W_ih^T dGI) * (x > 0) for every (t, row): grid (ntiles, T), HC waves (wave = feature chunk).
@@ -1594,6 +1688,17 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
 }
 
 }  // namespace
+
+extern "C" int mlg_debug_set_learner_stamps(void* ptr) {
+#ifdef MLG_STAMPS
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_mlg_lstamps), &ptr, sizeof(ptr));
+    if (e != hipSuccess) return mlg::fail("set learner stamps: %s", hipGetErrorString(e));
+    return 0;
+#else
+    (void)ptr;
+    return mlg::fail("not a stamps build (-DMLG_STAMPS)");
+#endif
+}
 
 extern "C" int64_t mlg_qlearner_param_counts(const MlgLearnerCfg* c, int64_t* n_agent, int64_t* n_mixer) {
     if (check_cfg(c)) return -1;

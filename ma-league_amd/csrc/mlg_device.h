@@ -47,6 +47,18 @@ __device__ __forceinline__ floatx4 mfma_bf16(bf16x8 a, bf16x8 b, floatx4 c) {
 __device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float fast_tanh(float x) { return 2.f * fast_sigmoid(2.f * x) - 1.f; }
 
+// Cross-lane reads without LDS (v_permlane16/32_swap, VALU): lane_plus16 returns lane l + 16's value in lanes of
+// the even 16-lane rows (0..15, 32..47); lane_plus32 returns lane l + 32's value in lanes 0..31. Other lanes get
+// unspecified values.
+__device__ __forceinline__ float lane_plus16(float x) {
+    const unsigned u = __float_as_uint(x);
+    return __uint_as_float(__builtin_amdgcn_permlane16_swap(u, u, false, false)[1]);
+}
+__device__ __forceinline__ float lane_plus32(float x) {
+    const unsigned u = __float_as_uint(x);
+    return __uint_as_float(__builtin_amdgcn_permlane32_swap(u, u, false, false)[1]);
+}
+
 // Branch-free predicated stores through a raw buffer resource: a dropped lane gets an out-of-range offset and
 // the hardware range check discards it. Inside sequential loops this keeps the VMEM stream straight-line, so
 // the compiler's waitcnt for a prefetched load counts the stores issued after it (an `if (valid)` store would
@@ -58,6 +70,43 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlg_rsrc(const float* base) {
 __device__ __forceinline__ void st4_if(__amdgpu_buffer_rsrc_t rs, int64_t off, floatx4 v, bool keep) {
     const int byte = keep ? (int)(off * 4) : (int)0x80000000u;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(mlg_u32x4, v), rs, byte, 0, 0);
+}
+
+// 4x4 transpose across the four 16-lane rows of a wave (same lane within the row): on return x[g] in row p holds
+// the input x[p] of row g. Two v_permlane16_swap + two v_permlane32_swap.
+__device__ __forceinline__ void rows_transpose4(float& x0, float& x1, float& x2, float& x3) {
+    const auto s01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
+    const auto s23 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2), __float_as_uint(x3), false, false);
+    const auto s02 = __builtin_amdgcn_permlane32_swap(s01[0], s23[0], false, false);
+    const auto s13 = __builtin_amdgcn_permlane32_swap(s01[1], s23[1], false, false);
+    x0 = __uint_as_float(s02[0]);
+    x1 = __uint_as_float(s13[0]);
+    x2 = __uint_as_float(s02[1]);
+    x3 = __uint_as_float(s13[1]);
+}
+// Register-wise sum over the four 16-lane rows, transposed: row p receives (x[p]_row0 + x[p]_row1) +
+// (x[p]_row2 + x[p]_row3). Three lane swaps and three adds.
+__device__ __forceinline__ float rows_sum_transpose4(float x0, float x1, float x2, float x3) {
+    const auto s01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
+    const auto s23 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2), __float_as_uint(x3), false, false);
+    const float a = __uint_as_float(s01[0]) + __uint_as_float(s01[1]);  // rows: x0 0+1, x1 0+1, x0 2+3, x1 2+3
+    const float b = __uint_as_float(s23[0]) + __uint_as_float(s23[1]);  // same for x2, x3
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+
+// Raw buffer access with a per-lane byte offset vo and a wave-uniform (SGPR) byte offset so.
+__device__ __forceinline__ floatx4 ld4_rs(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+}
+__device__ __forceinline__ float ld1_rs(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0));
+}
+__device__ __forceinline__ void st1_rs(__amdgpu_buffer_rsrc_t rs, int vo, int so, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, vo, so, 0);
+}
+__device__ __forceinline__ void st4_rs(__amdgpu_buffer_rsrc_t rs, int vo, int so, floatx4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(mlg_u32x4, v), rs, vo, so, 0);
 }
 
 __device__ __forceinline__ floatx4 mfma_chunk(const floatx4 w, const floatx4 x, floatx4 acc) {

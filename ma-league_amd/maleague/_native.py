@@ -136,6 +136,7 @@ SIGNATURES = {
     "mlg_refil_workspace_floats": (ctypes.c_int64, [_P]),
     "mlg_refil_train": (ctypes.c_int, [_P, _P, _P]),
     "mlg_debug_set_stamps": (ctypes.c_int, [_P]),
+    "mlg_debug_set_learner_stamps": (ctypes.c_int, [_P]),
     "mlg_refil_debug_set_stamps": (ctypes.c_int, [_P]),
     "mlg_last_error": (ctypes.c_char_p, []),
     "mlg_version": (ctypes.c_char_p, []),

@@ -1,4 +1,5 @@
-"""Sum rocprofv3 --pmc counter CSVs per kernel (rollout kernels only) and print per-dispatch averages."""
+"""Sum rocprofv3 --pmc counter CSVs per kernel (kernels whose name contains argv[2], default "rollout") and print
+per-dispatch averages."""
 import csv
 import glob
 import os
@@ -6,13 +7,14 @@ import sys
 from collections import defaultdict
 
 out = sys.argv[1]
+filt = sys.argv[2].split(",") if len(sys.argv) > 2 else ["rollout"]
 tot = defaultdict(float)
 disp = defaultdict(set)
 for f in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for row in csv.DictReader(fh):
             k = row.get("Kernel_Name", "")
-            if "rollout" not in k:
+            if not any(f in k for f in filt):
                 continue
             name = row.get("Counter_Name")
             tot[(k[:75], name)] += float(row.get("Counter_Value", 0))
