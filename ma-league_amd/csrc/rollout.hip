@@ -24,14 +24,34 @@
 // written to g_mlg_stamps[block][wave][16] (slots 0..13 phases, 14 total, 15 = 1).
 __device__ unsigned long long* g_mlg_stamps = nullptr;
 struct Stamps {
-    unsigned long long acc[14], last, begin;
+    unsigned long long acc[14], last, begin, tstep;
     __device__ void init() {
         for (int k = 0; k < 14; ++k) acc[k] = 0;
-        last = begin = __builtin_amdgcn_s_memtime();
+        last = begin = tstep = __builtin_amdgcn_s_memtime();
     }
+    // step trace (wave 0): cycles of step t-1 and running envs of step t, after the phase slots of the grid
+    __device__ void step(int t, int nrun) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if (g_mlg_stamps && threadIdx.x == 0 && t < 128)
+            g_mlg_stamps[(int64_t)gridDim.x * 8 * 16 + (int64_t)blockIdx.x * 128 + t] = ((now - tstep) << 8) | (unsigned)nrun;
+        tstep = now;
+#ifdef MLG_STAMPS_LOWRUN
+        on = nrun <= MLG_STAMPS_LOWRUN;
+#endif
+#ifdef MLG_STAMPS_TIMELINE
+        on = nrun == 1 && !seen;
+        seen = seen || on;
+#endif
+    }
+    bool on = true;  // -DMLG_STAMPS_LOWRUN=k: phase slots count only the steps with <= k running envs
+    bool seen = false;
     __device__ void mark(int k) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
-        acc[k] += now - last;
+#ifdef MLG_STAMPS_TIMELINE  // slot k = cycles from the start of the first one-env step to mark k
+        if (on) acc[k] = now - tstep;
+#else
+        if (on) acc[k] += now - last;
+#endif
         last = now;
     }
     __device__ void flush() {
@@ -46,6 +66,7 @@ struct Stamps {
 struct Stamps {
     __device__ void init() {}
     __device__ void mark(int) {}
+    __device__ void step(int, int) {}
     __device__ void flush() {}
 };
 #endif
@@ -1686,6 +1707,21 @@ __device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2&
     return C;
 }
 
+// Per-step copy of the env context for the env phase with the unit masks and the batch pointers moved into VGPRs
+// behind an opaque asm: values derived from them (per-unit role / team predicates of the unrolled unit loops, store
+// addresses) can then not be hoisted out of the step loop as loop invariants. Hoisted, they held ~40 SGPRs (64-bit
+// lane masks per unit) across the loop and spilled, and every batch store reloaded the whole 16-SGPR pointer tuple
+// from the spill lanes.
+__device__ __forceinline__ EnvCtx env_ctx_step(const EnvCtx& C) {
+    EnvCtx c = C;
+#ifndef MLG_ENV_SGPR_CTX  // A/B: the loop-invariant (SGPR) context
+    asm volatile("" : "+v"(c.M.team1), "+v"(c.M.healer), "+v"(c.M.tank), "+v"(c.M.melee));
+    asm volatile("" : "+v"(c.bt.obs), "+v"(c.bt.state), "+v"(c.bt.avail), "+v"(c.bt.actions));
+    asm volatile("" : "+v"(c.bt.actions_onehot), "+v"(c.bt.reward), "+v"(c.bt.terminated), "+v"(c.bt.filled));
+#endif
+    return c;
+}
+
 // ================================================================================================
 // v2 kernel: 8 waves, 16 envs; every wave does agent work (chunk j = w % HC of tiles w / HC, ...) and then
 // the env step of envs 2w, 2w + 1. Barriers per step: A|B, B|C, C|env, env|A.
@@ -1700,11 +1736,22 @@ struct StaticShape {
     static constexpr RolloutLds2 lay = on ? make_rollout_lds2(L, SU, SN, 16, 2, G8 ? 1 : 0) : RolloutLds2{};
 };
 
+// The batch pointers as eight independent SGPR pairs: loaded as one 16-SGPR tuple (s_load_dwordx16), a spilled
+// tuple is reloaded whole (16 v_readlane) wherever any one pointer is used.
+__device__ __forceinline__ MlgBatch split_batch_sgprs(MlgBatch b) {
+#ifndef MLG_ENV_SGPR_CTX
+    asm volatile("" : "+s"(b.obs), "+s"(b.state), "+s"(b.avail), "+s"(b.actions));
+    asm volatile("" : "+s"(b.actions_onehot), "+s"(b.reward), "+s"(b.terminated), "+s"(b.filled));
+#endif
+    return b;
+}
+
 template <int H, bool G8>
 __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
-                                                const float* __restrict__ P, const MlgBatch& bt, const MlgRunInfo& info,
+                                                const float* __restrict__ P, const MlgBatch& bt_arg, const MlgRunInfo& info,
                                                 float eps, int test_mode, const RolloutLds2& lay, int DU, int DN,
                                                 int DA, bool SD) {
+    const MlgBatch bt = split_batch_sgprs(bt_arg);
     constexpr int HC = H / 16, NW = 8, REW = 16, G = NW / HC;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     float* fm = reinterpret_cast<float*>(smem);
@@ -1727,6 +1774,7 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
     uint64_t rows_issued = 0;  // agent rows issued to the MFMA cell (incl. tile padding)
     for (int t = 0; t < T1; ++t) {
         const uint32_t run = (uint32_t)__ballot(lane < REW && C.R.status[lane & (REW - 1)] < 2);
+        sp.step(t, __popc(run));
         if (run == 0) break;
         const float* hc = fm + lay.hb + (t & 1) * lay.hsz;
         float* hn = fm + lay.hb + ((t & 1) ^ 1) * lay.hsz;
@@ -1777,13 +1825,14 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         sp.mark(2);
         __syncthreads();
         sp.mark(3);
-        env_lane_step1(C, E, t, hl);
+        const EnvCtx Ce = env_ctx_step(C);
+        env_lane_step1(Ce, E, t, hl);
         sp.mark(4);
-        env_lane_step2(C, E, t, hl, sp);
+        env_lane_step2(Ce, E, t, hl, sp);
 #ifdef MLG_DUP_TAIL  // timing ablation: the tail zeroing twice over the same steps
-        if (!E.stepped && (t & 1)) { const int z0 = E.zcur; env_lane_tail(C, E, 8, hl); E.zcur = z0; }
+        if (!E.stepped && (t & 1)) { const int z0 = E.zcur; env_lane_tail(Ce, E, 8, hl); E.zcur = z0; }
 #endif
-        if (!E.stepped && (t & 1)) env_lane_tail(C, E, 8, hl);
+        if (!E.stepped && (t & 1)) env_lane_tail(Ce, E, 8, hl);
         sp.mark(8);
         __syncthreads();
         sp.mark(10);

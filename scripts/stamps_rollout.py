@@ -20,13 +20,15 @@ exp._init_stepper()
 st = exp.stepper
 st.t_env = 10 ** 6
 grid = (B + 15) // 16
-buf = torch.zeros(grid * 8 * 16, dtype=torch.int64, device="cuda")
+buf = torch.zeros(grid * 8 * 16 + grid * 128, dtype=torch.int64, device="cuda")  # phase slots + step trace
 _native.call("mlg_debug_set_stamps", _native.ptr(buf))
 for it in range(3):
     buf.zero_()
     exp._train_episode(it * B)
 torch.cuda.synchronize()
-a = buf.view(grid, 8, 16).cpu().numpy().astype(np.float64)
+allb = buf.cpu().numpy()
+a = allb[:grid * 128].reshape(grid, 8, 16).astype(np.float64)
+tr = allb[grid * 128:].reshape(grid, 128)
 valid = a[:, :, 15] == 1
 if os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v1":
     names = ["agent", "barrier_after_agent", "-", "-"]
@@ -62,3 +64,37 @@ print("active env-steps per WG (sum len): p50 %d max %d" % (np.median([lens[i:i+
       max(lens[i:i+16].sum() for i in range(0, B, 16))))
 print("episode len mean", lens.mean(), "max", lens.max(), "iterations per WG (mean of max)",
       np.mean([lens[i:i + 16].max() + 1 for i in range(0, B, 16)]))
+
+# step trace: entry t = (cycles of step t-1) << 8 | running envs at step t
+cyc = (tr >> 8).astype(np.float64)
+nrun = (tr & 255).astype(np.int64)
+by = {}
+for g in range(grid):
+    for t in range(127):
+        if nrun[g, t] == 0 or cyc[g, t + 1] == 0:
+            continue
+        by.setdefault(int(nrun[g, t]), []).append(cyc[g, t + 1])
+print("step cycles by running envs in the WG (mean, count):")
+for k in sorted(by):
+    print(f"  nrun={k:2d} mean={np.mean(by[k]):8.0f} n={len(by[k])}")
+tot_wg = cyc[:, 1:].sum(1)
+slow = int(np.argmax(tot_wg))
+print("slowest WG", slow, "total", tot_wg[slow], "mean WG", tot_wg.mean())
+prof = [(int(nrun[slow, t]), int(cyc[slow, t + 1])) for t in range(127) if nrun[slow, t] > 0]
+print("slowest WG steps (nrun, cycles):", prof)
+if int(os.environ.get("TIMELINE", "0")):
+    # -DMLG_STAMPS_TIMELINE build: slot k = cycles from the start of the WG's first one-env step to mark k
+    order = [(0, "fc1"), (5, "barrier_A"), (1, "gru"), (13, "barrier_B"), (2, "fc2"), (3, "barrier_C"),
+             (4, "E1E2"), (6, "E3"), (7, "pair"), (9, "obs"), (11, "avail"), (12, "state"), (8, "tail"), (10, "end")]
+    envw, oth = [], []
+    for g in range(grid):
+        for w in range(8):
+            if a[g, w, 15] != 1 or a[g, w, 10] == 0:
+                continue
+            (envw if a[g, w, 7] > 0 else oth).append(a[g, w, :14])
+    for nm, rows in (("env wave", envw), ("other waves", oth)):
+        if not rows:
+            continue
+        r = np.array(rows)
+        print(f"timeline of the first one-env step, {nm} (n={len(r)}): " +
+              ", ".join(f"{n}@{r[:, k].mean():.0f}" for k, n in order))
