@@ -2435,11 +2435,22 @@ extern "C" int mlg_rollout_selfplay(const MlgEnvSpec* spec, MlgEnvState* st, con
     sd.eps[1] = test_mode ? 0.f : eps_away;
     sd.ns = 2;
     sd.nh = nh;
-    // self-play kernel (v2 structure, two policies) when the shape allows it, else the generic v1 kernel
+    // self-play kernels (two policies): sp7 (v7 agent phases) for H = 64, else sp2 (v2 structure) when the shape
+    // allows it, else the generic v1 kernel. MLG_ROLLOUT_KERNEL=v1 | sp2 forces one.
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
+    const bool force_v1 = k && k[0] == 'v' && k[1] == '1', force_sp2 = k && !strcmp(k, "sp2");
+    const RolloutLdsSP l7 = make_rollout_lds_sp(L, spec->U, spec->n_agents, true);
+    if (!force_v1 && !force_sp2 && L.H == 64 && spec->U <= 32 && l7.total * 4 <= LDS_LIMIT_BYTES) {
+        const size_t bytes = (size_t)l7.total * 4;
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rollout_sp7_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return mlg::fail("rollout_selfplay: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
+        hipLaunchKernelGGL(rollout_sp7_kernel, dim3((st->B + RS - 1) / RS), dim3(512), bytes, (hipStream_t)stream, *spec,
+                           *st, L, home_packed, away_packed, *home, *away, *info, sd.eps[0], sd.eps[1], test_mode, l7);
+        return mlg::check_launch("rollout_sp7_kernel");
+    }
     const RolloutLdsSP lsp = make_rollout_lds_sp(L, spec->U, spec->n_agents);
-    if (!(k && k[0] == 'v' && k[1] == '1') && (L.H == 64 || L.H == 32) && spec->U <= 32 &&
-        lsp.total * 4 <= LDS_LIMIT_BYTES) {
+    if (!force_v1 && (L.H == 64 || L.H == 32) && spec->U <= 32 && lsp.total * 4 <= LDS_LIMIT_BYTES) {
         const size_t bytes = (size_t)lsp.total * 4;
         auto kern = L.H == 64 ? rollout_sp_kernel<64> : rollout_sp_kernel<32>;
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),

@@ -1,7 +1,7 @@
 """ISA stats of the static 5v5 v7 rollout kernel (analysis aid; see isa_stats.sh)."""
 import re, sys
 lines = open(sys.argv[1]).read().split("\n")
-name = "_ZN12_GLOBAL__N_117rollout_v2_kernelILi64ELb1ELi5ELi10EEEv10MlgEnvSpec"
+name = sys.argv[2] if len(sys.argv) > 2 else "_ZN12_GLOBAL__N_117rollout_v2_kernelILi64ELb1ELi5ELi10EEEv10MlgEnvSpec"
 st = next(i for i, l in enumerate(lines) if l.startswith(name) and ":" in l)
 en = next(i for i in range(st, len(lines)) if lines[i].startswith("\t.size\t" + name))
 k = lines[st:en]

@@ -263,16 +263,14 @@ def test_league_instance_single_rank(device, mode):
 
 @pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium"])
 def test_selfplay_kernel_equals_v1(device, plan, monkeypatch):
-    """The compacted two-policy kernel (rollout_sp_kernel) and the generic per-tile kernel (v1) compute in the
-    same arithmetic order: both batches and the run summary must be bit-identical (train mode, epsilon on)."""
+    """The compacted two-policy kernel of the v2 structure (rollout_sp_kernel, MLG_ROLLOUT_KERNEL=sp2) and the
+    generic per-tile kernel (v1) compute in the same arithmetic order: both batches and the run summary must be
+    bit-identical (train mode, epsilon on)."""
     from maleague.envs.teams_env import VecEnvState
     stepper, home, away, args = _build(device, plan=plan, B=100, episode_limit=60, seed=3)
     out = {}
     for kern in ("v1", "sp"):
-        if kern == "v1":
-            monkeypatch.setenv("MLG_ROLLOUT_KERNEL", "v1")
-        else:
-            monkeypatch.delenv("MLG_ROLLOUT_KERNEL", raising=False)
+        monkeypatch.setenv("MLG_ROLLOUT_KERNEL", "v1" if kern == "v1" else "sp2")
         stepper.envs = VecEnvState(stepper.spec, 100, device)
         stepper.t_env = 30000
         hb, ab, _ = stepper.run(test_mode=False)
@@ -285,3 +283,43 @@ def test_selfplay_kernel_equals_v1(device, plan, monkeypatch):
             assert torch.equal(out["v1"][side][k], out["sp"][side][k]), (side, k)
     for i in (2, 3, 4):
         assert torch.equal(out["v1"][i], out["sp"][i])
+
+
+@pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium"])
+def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, monkeypatch):
+    """sp7 (default for H = 64): the v7 agent phases with two policies -- GRU products as split-bf16 fp32 emulation,
+    each wave swapping between the home and away weights. Along sp7's own trajectory (test mode) the fp32 oracle
+    MAC of each side must rate every recorded action as an available argmax up to a 1e-5 tie, and sp7 must
+    reproduce sp2's episodes bit for bit except where a near-tie flips an argmax (the env code is sp2's)."""
+    from maleague.envs.teams_env import VecEnvState
+    B, TL = 100, 60
+    stepper, home, away, args = _build(device, plan=plan, B=B, episode_limit=TL, seed=3)
+    out = {}
+    for k in ("sp2", "sp7"):
+        if k == "sp2":
+            monkeypatch.setenv("MLG_ROLLOUT_KERNEL", "sp2")
+        else:
+            monkeypatch.delenv("MLG_ROLLOUT_KERNEL", raising=False)
+        stepper.envs = VecEnvState(stepper.spec, B, device)
+        hb, ab, _ = stepper.run(test_mode=True)
+        out[k] = ([np_batch(hb), np_batch(ab)], stepper.last_run["ep_len"].numpy().copy())
+    nbs, L = out["sp7"]
+    N = args.n_agents
+    worst = 0.0
+    for mac, nb in zip((home, away), nbs):
+        tb = {kk: torch.from_numpy(v) for kk, v in nb.items()}
+        p = {kk: v.detach().cpu() for kk, v in mac.agent.state_dict().items()}
+        with torch.no_grad():
+            q, _ = LR.mac_unroll(p, tb, N, T=TL + 1)
+        q = q.numpy()
+        av = nb["avail_actions"].astype(bool)
+        for b_ in range(B):
+            for t in range(int(L[b_]) + 1):
+                qm = np.where(av[b_, t], q[b_, t], -np.inf)
+                chosen = np.take_along_axis(qm, nb["actions"][b_, t], axis=-1)[:, 0]
+                assert np.isfinite(chosen).all(), (b_, t)
+                worst = max(worst, float((qm.max(axis=-1) - chosen).max()))
+    assert worst <= 1e-5, worst
+    ref = out["sp2"][0]
+    same = [all(np.array_equal(ref[s][kk][b_], nbs[s][kk][b_]) for s in (0, 1) for kk in nbs[s]) for b_ in range(B)]
+    assert np.mean(same) >= 0.9, np.mean(same)
