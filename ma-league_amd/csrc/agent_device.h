@@ -14,12 +14,17 @@
 //   brz [2H]      b_ih + b_hh for the r,z gates (pre-summed)
 //   w2  [Ap][H]   fc2.weight zero padded to Ap = A rounded up to 16 rows
 //   b2  [Ap]
+//   gsp [8 waves][18 regs][64 lanes][4]  (H = 64 only) the GRU weights as split-bf16 pieces in the register
+//                 layout of the self-play kernel's waves (GruG8: per K step kk, {W_ir;W_iz}, {W_hr;W_hz},
+//                 {W_in;W_hn} rows, pieces 0..2; a u32 = two bf16), so a weight swap is 18 straight loads
+//   w1s [H/16 chunks][KK][3 pieces][64 lanes][4]  (H = 64 only) fc1 obs columns as split-bf16 A operands
+//                 (K steps of 32, zero padded past d_obs)
 #pragma once
 #include "mlg_device.h"
 
 struct AgentLayout {
     int H, A, Ap, N, d_obs, Dob, d_in, Dip, last_action, agent_id;
-    int32_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, total;  // 32-bit: fewer SGPRs in kernels
+    int32_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, gsp, w1s, total;  // 32-bit: fewer SGPRs
 };
 
 __host__ __device__ constexpr int64_t mlg_align4(int64_t v) { return (v + 3) & ~int64_t(3); }
@@ -49,8 +54,23 @@ __host__ __device__ constexpr AgentLayout make_agent_layout(const MlgAgentDims& 
     L.brz = o; o += 2 * L.H;
     L.w2 = o; o += (int64_t)L.Ap * L.H;
     L.b2 = o; o += L.Ap;
+    o = mlg_align4(o);
+    L.gsp = o; o += L.H == 64 ? 8 * 18 * 64 * 4 : 0;
+    L.w1s = o; o += L.H == 64 ? (int64_t)(L.H / 16) * ((L.Dob + 31) / 32) * 3 * 64 * 4 : 0;
     L.total = mlg_align4(o);
     return L;
+}
+
+// Piece `piece` (0..2) of the split-bf16 representation of the pair (a, b) as one u32 (bf16 of a low, of b high),
+// bit-identical to split3() in rollout.hip: a = a0 + a1 + a2 exactly, round to nearest per piece.
+__device__ __forceinline__ float split_bf16_pair(float a, float b, int piece) {
+    unsigned int pk = 0u;
+    for (int lvl = 0; lvl <= piece; ++lvl) {
+        pk = cvt_pk_bf16(a, b);
+        a -= __uint_as_float(pk << 16);
+        b -= __uint_as_float(pk & 0xFFFF0000u);
+    }
+    return __uint_as_float(pk);
 }
 
 // Packed float i of the kernel weight layout from the canonical nn.Module tensors (pack_agent_kernel and the
@@ -86,9 +106,29 @@ __device__ __forceinline__ float pack_agent_elem(const AgentLayout& L, const Mlg
     } else if (i < L.b2) {
         const int64_t k = i - L.w2, r = k / H, c = k % H;
         v = r < L.A ? p.fc2_w[r * H + c] : 0.f;
-    } else {
+    } else if (i < L.gsp) {
         const int64_t k = i - L.b2;
         v = k < L.Ap && k < L.A ? p.fc2_b[k] : 0.f;
+    } else if (i < L.w1s) {  // split GRU pieces (H = 64): k = ((w * 18 + kk * 9 + mat * 3 + piece) * 64 + lane) * 4 + q
+        const int64_t k = i - L.gsp;
+        const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), r = (int)((k >> 8) % 18), w = (int)((k >> 8) / 18);
+        const int kk = r / 9, mat = (r / 3) % 3, piece = r % 3;
+        const int row = lane & 15, g = lane >> 4, f = 8 * w + (row & 7), hi = row >> 3;
+        const float* src = mat == 0 ? p.w_ih + (int64_t)(hi * H + f) * H
+                                    : (mat == 1 ? p.w_hh + (int64_t)(hi * H + f) * H
+                                                : (hi ? p.w_hh : p.w_ih) + (int64_t)(2 * H + f) * H);
+        const int kb = 32 * kk + 8 * g + 2 * q;
+        v = split_bf16_pair(src[kb], src[kb + 1], piece);
+    } else {  // split fc1 obs columns: k = (((j * KK + kk) * 3 + piece) * 64 + lane) * 4 + q
+        const int64_t k = i - L.w1s;
+        const int KK = (L.Dob + 31) / 32;
+        const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), r = (int)(k >> 8);
+        const int piece = r % 3, kk = (r / 3) % KK, j = r / (3 * KK);
+        const int64_t row = j * 16 + (lane & 15);
+        const int kb = 32 * kk + 8 * (lane >> 4) + 2 * q;
+        const float a = kb < L.d_obs ? p.fc1_w[row * L.d_in + kb] : 0.f;
+        const float b = kb + 1 < L.d_obs ? p.fc1_w[row * L.d_in + kb + 1] : 0.f;
+        v = split_bf16_pair(a, b, piece);
     }
     return v;
 }

@@ -2440,13 +2440,18 @@ extern "C" int mlg_rollout_selfplay(const MlgEnvSpec* spec, MlgEnvState* st, con
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
     const bool force_v1 = k && k[0] == 'v' && k[1] == '1', force_sp2 = k && !strcmp(k, "sp2");
     const RolloutLdsSP l7 = make_rollout_lds_sp(L, spec->U, spec->n_agents, true);
-    if (!force_v1 && !force_sp2 && L.H == 64 && spec->U <= 32 && l7.total * 4 <= LDS_LIMIT_BYTES) {
+    if (!force_v1 && !force_sp2 && L.H == 64 && L.Dob <= 32 * SP7_MAXKK && l7.total * 4 <= LDS_LIMIT_BYTES) {
         const size_t bytes = (size_t)l7.total * 4;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rollout_sp7_kernel),
+        auto kern = rollout_sp7_kernel<0, 0>;  // runtime shapes; the 5v5 / 3v3 self-play plans as constants
+        if (!getenv("MLG_ROLLOUT_GENERIC")) {
+            if (static_shape_matches_sp<10, 10>(L, l7)) kern = rollout_sp7_kernel<10, 10>;
+            else if (static_shape_matches_sp<6, 6>(L, l7)) kern = rollout_sp7_kernel<6, 6>;
+        }
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return mlg::fail("rollout_selfplay: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
-        hipLaunchKernelGGL(rollout_sp7_kernel, dim3((st->B + RS - 1) / RS), dim3(512), bytes, (hipStream_t)stream, *spec,
-                           *st, L, home_packed, away_packed, *home, *away, *info, sd.eps[0], sd.eps[1], test_mode, l7);
+        hipLaunchKernelGGL(kern, dim3((st->B + RS - 1) / RS), dim3(512), bytes, (hipStream_t)stream, *spec, *st, L,
+                           home_packed, away_packed, *home, *away, *info, sd.eps[0], sd.eps[1], test_mode, l7);
         return mlg::check_launch("rollout_sp7_kernel");
     }
     const RolloutLdsSP lsp = make_rollout_lds_sp(L, spec->U, spec->n_agents);
