@@ -226,7 +226,8 @@ __global__ void __launch_bounds__(1024) prep_kernel(PrepJob J) {
         mask_sum_block(J.bt, J.B, J.T, J.msum, red);
         return;
     }
-    const int64_t na = J.L.total, nt = (int64_t)J.rows3 * J.cols, nm = J.mixer == 2 ? J.mp.total : 0;
+    const int64_t na = J.L.gsp,  // the learner reads no pre-split rollout sections (gsp, w1s)
+                   nt = (int64_t)J.rows3 * J.cols, nm = J.mixer == 2 ? J.mp.total : 0;
     const int64_t total = 2 * na + nt + 2 * nm + J.n_d2 + J.n_dq;
     for (int64_t i = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)(gridDim.x - 1) * blockDim.x) {
