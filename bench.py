@@ -196,7 +196,10 @@ def main():
     # the default rollout kernel: v7 (split-bf16 GRU), compile-time shape for the 5v5 / 3v3 plans
     v7 = "rollout_v2_kernel<64, true, 5, 10>" if (N, info["n_actions"]) == (5, 15) else (
         "rollout_v2_kernel<64, true, 3, 6>" if (N, info["n_actions"]) == (3, 11) else "rollout_v2_kernel<64, true>")
-    kernel = {"ai": v7, "league": "rollout_sp_kernel<64>", "refil": f"refil_rollout_kernel<{kc1}>"}[mode]
+    sp7 = "rollout_sp7_kernel<10, 10>" if (N, info["n_actions"]) == (5, 15) else (
+        "rollout_sp7_kernel<6, 6>" if (N, info["n_actions"]) == (3, 11) else "rollout_sp7_kernel<0, 0>")
+    kernel = {"ai": v7, "league": sp7,  # the bench runs H = 64 (rnn_hidden_dim below)
+              "refil": f"refil_rollout_kernel<{kc1}>"}[mode]
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
             traffic = json.load(f).get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
