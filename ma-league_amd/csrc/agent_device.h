@@ -350,11 +350,27 @@ __device__ __forceinline__ void argmax_accumulate(ArgmaxState& s, const floatx4 
     }
 }
 
+// Reduction over the four 16-lane rows (lane l with l ^ 16, then l ^ 32) by v_permlane16/32_swap (VALU) instead of
+// LDS permutes: the same exchanged values, ~10x less latency on the action-selection path. All 64 lanes must be
+// active (callers: wave-uniform tile loops).
 __device__ __forceinline__ int argmax_reduce(ArgmaxState s) {
+    const bool odd16 = (threadIdx.x & 16) != 0, hi32 = (threadIdx.x & 32) != 0;
 #pragma unroll
-    for (int m = 16; m <= 32; m <<= 1) {
-        const float ov = __shfl_xor(s.bv, m);
-        const int oi = __shfl_xor(s.bi, m);
+    for (int r = 0; r < 2; ++r) {
+        const unsigned uv = __float_as_uint(s.bv), ui = (unsigned)s.bi;
+        float ov;
+        int oi;
+        if (r == 0) {  // lane ^ 16: even rows read the second result, odd rows the first
+            const auto xv = __builtin_amdgcn_permlane16_swap(uv, uv, false, false);
+            const auto xi = __builtin_amdgcn_permlane16_swap(ui, ui, false, false);
+            ov = __uint_as_float(odd16 ? xv[0] : xv[1]);
+            oi = (int)(odd16 ? xi[0] : xi[1]);
+        } else {       // lane ^ 32
+            const auto xv = __builtin_amdgcn_permlane32_swap(uv, uv, false, false);
+            const auto xi = __builtin_amdgcn_permlane32_swap(ui, ui, false, false);
+            ov = __uint_as_float(hi32 ? xv[0] : xv[1]);
+            oi = (int)(hi32 ? xi[0] : xi[1]);
+        }
         const bool take = amax_better(ov, oi, s.bv, s.bi);
         s.bv = take ? ov : s.bv;
         s.bi = take ? oi : s.bi;

@@ -47,6 +47,17 @@ __device__ __forceinline__ floatx4 mfma_bf16(bf16x8 a, bf16x8 b, floatx4 c) {
 __device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float fast_tanh(float x) { return 2.f * fast_sigmoid(2.f * x) - 1.f; }
 
+// Workgroup barrier that orders LDS only: the release fence waits for this wave's LDS operations (lgkmcnt) but not
+// for its outstanding global stores, which __syncthreads() (a release fence over all address spaces) waits for --
+// on the rollout's per-step barriers that was the HBM write latency of the step's action / batch-row stores. Only
+// for kernels whose waves never read, within the kernel, global data another wave of the workgroup wrote (the
+// rollout kernels: batch rows and actions are write-only there, cross-wave data goes through LDS).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Cross-lane reads without LDS (v_permlane16/32_swap, VALU): lane_plus16 returns lane l + 16's value in lanes of
 // the even 16-lane rows (0..15, 32..47); lane_plus32 returns lane l + 32's value in lanes 0..31. Other lanes get
 // unspecified values.

@@ -1349,13 +1349,25 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
     }
 }
 
+// Epsilon coin of this lane's row of compact tile ti (action_selectors.py:56, spec §3.7 counter RNG; the agent index
+// field of the row-map entry: agent within the env, or the global agent index in the self-play map), drawn ahead of
+// the fc2 phase.
+__device__ __forceinline__ int eps_coin(const MlgEnvSpec& spec, const RoEnv& R, const int* rmap, int ti, int e0, int t,
+                                        float eps, int test_mode, int lane) {
+    const int rm = rmap[ti * 16 + (lane & 15)];
+    const int e = rm >> 8, n = (rm >> 1) & 127;
+    const uint64_t key = mlg_env_key(spec.seed, e0 + e);
+    return !test_mode && eps > 0.f &&
+           mlg_u01(mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n))) < eps;
+}
+
 // v7 C: fc2 + masked argmax + epsilon-greedy per tile, rows from the fc1 row map. The epsilon draws do not depend
 // on Q, so they are made before the fc2 chain (their latency overlaps the MFMAs), and fc2 accumulates the four
 // 16-wide K chunks in separate chains (fp32-class like the rest of v7; same selection rule as ph_fc2).
 template <int H>
 __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, const RolloutLds2& lay, float* fm,
                                  const int* rmap, const RoEnv& R, const MlgBatch& bt, const float* hn, int tiles, int ti0,
-                                 int dt, int e0, int t, float eps, int test_mode, int lane) {
+                                 int dt, int e0, int t, float eps, int test_mode, int lane, int pre = -1) {
     constexpr int HC = H / 16;
     const int col = lane & 15, g = lane >> 4, N = L.N, ldh = lay.ldh, A = spec.n_actions, n_at = L.Ap / 16;
     const uint64_t* lavm = reinterpret_cast<const uint64_t*>(fm + lay.avail);
@@ -1373,8 +1385,12 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
         // branch, so it issues between the fc2 MFMAs; only the rare exploring lanes take the branch below
         const uint64_t key = mlg_env_key(spec.seed, e0 + e);
         const uint32_t ep = R.episode[e];
-        const bool explore = !test_mode && eps > 0.f &&
-                             mlg_u01(mlg_rng(key, mlg_ctr(ep, (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n))) < eps;
+        bool explore;  // the wave's first tile: coin drawn during the GRU phase (eps_coin), off this phase's path
+        if (ti == ti0 && pre >= 0)
+            explore = pre;
+        else
+            explore = !test_mode && eps > 0.f &&
+                      mlg_u01(mlg_rng(key, mlg_ctr(ep, (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n))) < eps;
         auto q_block = [&](int at) {  // Q rows at*16 .. at*16+15 of this lane's agent row; all operands loaded first
             const float* w2r = fm + lay.w2 + zero + (at * 16 + col) * ldh + 4 * g;
             floatx4 wk[HC], hk[HC], qk[HC];
@@ -1797,8 +1813,11 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         }
         rows_issued += tiles * 16;
         sp.mark(0);
-        __syncthreads();
+        lds_barrier();
         if constexpr (G8) sp.mark(5);  // v7 stamps: barrier A wait in slot 5, barrier B wait in slot 13
+        int pre = -1;  // v7: epsilon coin of the wave's fc2 tile, drawn here (VALU next to the GRU's MFMAs)
+        if constexpr (G8)
+            if (wave < tiles) pre = eps_coin(spec, C.R, wmap, wave, e0, t, eps, test_mode, lane);
         if constexpr (G8)
             ph_gru_g8<H>(W8, lay, fm, wmap, hc, hn, tiles, N, wave, lane);
         else
@@ -1810,10 +1829,10 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
             ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
 #endif
         sp.mark(1);
-        __syncthreads();
+        lds_barrier();
         if constexpr (G8) sp.mark(13);
         if constexpr (G8)
-            ph_fc2_g8<H>(spec, L, lay, fm, wmap, C.R, bt, hn, tiles, wave, NW, e0, t, eps, test_mode, lane);
+            ph_fc2_g8<H>(spec, L, lay, fm, wmap, C.R, bt, hn, tiles, wave, NW, e0, t, eps, test_mode, lane, pre);
         else
             ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
 #ifdef MLG_DUP_FC2
@@ -1823,7 +1842,7 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
             ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
 #endif
         sp.mark(2);
-        __syncthreads();
+        lds_barrier();
         sp.mark(3);
         const EnvCtx Ce = env_ctx_step(C);
         env_lane_step1(Ce, E, t, hl);
@@ -1834,7 +1853,7 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
 #endif
         if (!E.stepped && (t & 1)) env_lane_tail(Ce, E, 8, hl);
         sp.mark(8);
-        __syncthreads();
+        lds_barrier();
         sp.mark(10);
     }
     sp.flush();
