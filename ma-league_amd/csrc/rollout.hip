@@ -653,31 +653,43 @@ struct UnitLane {
     int ai;              // scripted action decided on the current state (spec §3.3)
 };
 
-// One pass over all units j of the env for unit u (every lane of the half-wave runs all U iterations):
-// attack/heal availability, sight, and the scripted AI choice (lowest-hp target in range, else nearest
-// ally for a healer when one is alive, else nearest enemy) -- spec §3.2-3.3 in mask form.
+// One pass over all units j of the env for unit u: attack/heal availability, sight, and the scripted AI choice
+// (lowest-hp target in range, else nearest ally for a healer when one is alive, else nearest enemy) -- spec
+// §3.2-3.3 in mask form. U <= 16 (the latency path of every env step): the two 16-lane rows of the half-wave split
+// the units j -- row 1 mirrors row 0's unit (one v_permlane16_swap), visits the upper half of j, and the partial
+// masks / min-keys are combined across the rows (min and OR: exact, order-free, so the result is bit-identical to
+// visiting all j in one lane).
 __device__ __forceinline__ void v2_pair_pass(const UnitMasks& M, int U, int u, UnitLane& L, int* spk) {
     const uint32_t all = U >= 32 ? 0xFFFFFFFFu : ((1u << U) - 1u);
-    const int my_team = (M.team1 >> u) & 1;
-    const bool healer = (M.healer >> u) & 1;
-    const int r2 = ((M.melee >> u) & 1) ? 2 : 9;
-    const bool alive = L.hp > 0;
     const int hbase = (threadIdx.x & 63) & 32;
-    // alive units of the env (bit j) and this unit's ally / enemy candidate sets (spec §3.2-3.3)
+    // alive units of the env (bit j): the unit lanes of row 0 (u < U)
     const uint32_t alive_m = (uint32_t)(__ballot(u < U && L.hp > 0) >> hbase) & all;
+    const int pk_own = pk_unit(L.x, L.y, L.hp);
+    // packed unit states of the env through LDS (written and read by this half-wave only: in-order LDS
+    // queue of one wave, no barrier)
+    spk[u] = pk_own;
+    const bool split = U <= 16, odd = split && (threadIdx.x & 16) != 0;
+    int pkm = pk_own, uu = u;  // the unit this lane visits for: its own, or (row 1 of a split pass) row 0's
+    if (split) {
+        const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)pk_own, (unsigned)pk_own, false, false);
+        pkm = odd ? (int)sw[0] : pk_own;
+        uu = u & 15;
+    }
+    const int X = pk_x(pkm), Y = pk_y(pkm), HP = pk_hp(pkm);
+    const int my_team = (M.team1 >> uu) & 1;
+    const bool healer = (M.healer >> uu) & 1;
+    const int r2 = ((M.melee >> uu) & 1) ? 2 : 9;
+    const bool alive = HP > 0;
     const uint32_t mates = (my_team ? M.team1 : ~M.team1) & all;
-    const uint32_t cand_a = alive ? (mates & alive_m & ~(1u << u)) : 0u;
+    const uint32_t cand_a = alive ? (mates & alive_m & ~(1u << uu)) : 0u;
     const uint32_t cand_e = alive ? (~mates & alive_m & all) : 0u;
     const uint32_t seen = alive ? alive_m : 0u;
-    // packed unit states of the env through LDS (written and read by this half-wave only: in-order LDS
-    // queue of one wave, no barrier), read back four units per 16-byte broadcast load
-    spk[u] = pk_unit(L.x, L.y, L.hp);
     // min-keys (value << 5 | j) give "smallest value, then lowest j" -- the spec's tie rule -- without branches
     constexpr uint32_t NONE = 0xFFFFFFFFu;
     uint32_t kbest = NONE, kally = NONE, kenemy = NONE, tgt = 0, sight = 0;
-    auto visit = [&](int j, int q) {
+    auto visit = [&](int j, int q) {  // j may differ per lane; bits of j >= U are clear in every candidate mask
         const int hj = pk_hp(q);
-        const int dx = pk_x(q) - L.x, dy = pk_y(q) - L.y;
+        const int dx = pk_x(q) - X, dy = pk_y(q) - Y;
         const uint32_t d2 = (uint32_t)(__mul24(dx, dx) + __mul24(dy, dy));
         const uint32_t bit = 1u << j;
         const bool vis = (seen & bit) && d2 <= MLG_SIGHT2;
@@ -690,12 +702,31 @@ __device__ __forceinline__ void v2_pair_pass(const UnitMasks& M, int U, int u, U
         kally = min(kally, (cand_a & bit) ? (d2 << 5 | j) : NONE);
         kenemy = min(kenemy, (cand_e & bit) ? (d2 << 5 | j) : NONE);
     };
-    for (int j0 = 0; j0 < U; j0 += 4) {
-        const int4 q4 = *reinterpret_cast<const int4*>(spk + j0);
-        visit(j0, q4.x);
-        if (j0 + 1 < U) visit(j0 + 1, q4.y);
-        if (j0 + 2 < U) visit(j0 + 2, q4.z);
-        if (j0 + 3 < U) visit(j0 + 3, q4.w);
+    if (split) {
+        const int JH = (U + 1) >> 1, base = odd ? JH : 0;
+        int q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = k < JH ? spk[(base + k) & 31] : 0;  // all reads issued together
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (k < JH) visit((base + k) & 31, q[k]);
+        auto other = [&](uint32_t v) {  // the value of lane l ^ 16
+            const auto s2 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            return (threadIdx.x & 16) ? s2[0] : s2[1];
+        };
+        kbest = min(kbest, other(kbest));
+        kally = min(kally, other(kally));
+        kenemy = min(kenemy, other(kenemy));
+        tgt |= other(tgt);
+        sight |= other(sight);
+    } else {
+        for (int j0 = 0; j0 < U; j0 += 4) {  // four units per 16-byte broadcast load
+            const int4 q4 = *reinterpret_cast<const int4*>(spk + j0);
+            visit(j0, q4.x);
+            if (j0 + 1 < U) visit(j0 + 1, q4.y);
+            if (j0 + 2 < U) visit(j0 + 2, q4.z);
+            if (j0 + 3 < U) visit(j0 + 3, q4.w);
+        }
     }
     int ai = 0;
     if (alive) {
@@ -705,10 +736,10 @@ __device__ __forceinline__ void v2_pair_pass(const UnitMasks& M, int U, int u, U
         else k = kenemy;
         if (ai == 0 && k != NONE) {
             const int q = spk[k & 31];
-            ai = move_toward_d(pk_x(q) - L.x, pk_y(q) - L.y);
+            ai = move_toward_d(pk_x(q) - X, pk_y(q) - Y);
         }
     }
-    L.tgt = tgt;
+    L.tgt = tgt;  // row 1 of a split pass: lanes u >= U (no unit), whose fields no reader uses
     L.sight = sight;
     L.ai = ai;
 }
