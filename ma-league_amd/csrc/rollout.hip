@@ -744,6 +744,52 @@ __device__ __forceinline__ void v2_pair_pass(const UnitMasks& M, int U, int u, U
     L.ai = ai;
 }
 
+// Damage and heal received by unit hl from the executed actions of all units (spec §3.4 resolution on the
+// pre-step state: pk = packed pre-step units, act = executed actions, both per env in LDS). U <= 16: split across
+// the two 16-lane rows (as v2_pair_pass): row 1 sums the upper half of the attackers i for row 0's unit, the
+// integer partial sums are combined by one permlane16 swap each (exact).
+__device__ __forceinline__ void resolve_hits(const UnitMasks& M, int U, int hl, const int* spk, const int* sact, int& dmg,
+                                             int& heal) {
+    if (U <= 16) {
+        const bool odd = (hl & 16) != 0;
+        const int me = MLG_ACT_BASE + (hl & 15), JH = (U + 1) >> 1, base = odd ? JH : 0;
+        int qs[8], as[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // all reads issued together
+            qs[k] = k < JH ? spk[(base + k) & 31] : 0;
+            as[k] = k < JH ? sact[(base + k) & 31] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= JH) break;
+            const int i = base + k;
+            const bool hit = i < U && pk_hp(qs[k]) > 0 && as[k] == me;
+            const bool hl_i = (M.healer >> i) & 1;
+            heal += (hit && hl_i) ? role_power(1) : 0;
+            dmg += (hit && !hl_i) ? role_power(mask_role(M, i)) : 0;
+        }
+        const auto sd = __builtin_amdgcn_permlane16_swap((unsigned)dmg, (unsigned)dmg, false, false);
+        const auto sh = __builtin_amdgcn_permlane16_swap((unsigned)heal, (unsigned)heal, false, false);
+        dmg += (int)(odd ? sd[0] : sd[1]);
+        heal += (int)(odd ? sh[0] : sh[1]);
+        return;
+    }
+    const int me = MLG_ACT_BASE + hl;
+    for (int i0 = 0; i0 < U; i0 += 4) {  // four units per 16-byte broadcast load
+        const int4 q4 = *reinterpret_cast<const int4*>(spk + i0);
+        const int4 a4 = *reinterpret_cast<const int4*>(sact + i0);
+        const int qs[4] = {q4.x, q4.y, q4.z, q4.w}, as[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + r;
+            const bool hit = i < U && pk_hp(qs[r]) > 0 && as[r] == me;
+            const bool hl_i = (M.healer >> i) & 1;
+            heal += (hit && hl_i) ? role_power(1) : 0;
+            dmg += (hit && !hl_i) ? role_power(mask_role(M, i)) : 0;
+        }
+    }
+}
+
 __device__ __forceinline__ int v2_avail(const UnitMasks& M, int G, int x, int y, int hp, uint32_t tgt, int k) {
     const bool alive = hp > 0;
     if (k == 0) return !alive;
@@ -1608,28 +1654,7 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     const int* spk = C.pk + E.e * 32;
     sact[hl] = act;
     int dmg = 0, heal = 0;
-    const int me = MLG_ACT_BASE + hl;
-#ifdef MLG_DUP_E2  // timing ablation: the resolution loop twice (same result)
-    for (int rep = 0; rep < 2; ++rep) {
-    dmg = 0; heal = 0;
-#endif
-    for (int i0 = 0; i0 < U; i0 += 4) {
-        const int4 q4 = *reinterpret_cast<const int4*>(spk + i0);
-        const int4 a4 = *reinterpret_cast<const int4*>(sact + i0);
-        const int qs[4] = {q4.x, q4.y, q4.z, q4.w}, as[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = i0 + r;
-            const bool hit = i < U && pk_hp(qs[r]) > 0 && as[r] == me;
-            const bool hl_i = (C.M.healer >> i) & 1;
-            heal += (hit && hl_i) ? role_power(1) : 0;
-            dmg += (hit && !hl_i) ? role_power(mask_role(C.M, i)) : 0;
-        }
-    }
-#ifdef MLG_DUP_E2
-    asm volatile("" : "+v"(dmg), "+v"(heal));
-    }
-#endif
+    resolve_hits(C.M, U, hl, spk, sact, dmg, heal);
     E.h0 = E.u.hp;
     if (uvalid && E.h0 > 0) {
         const int v = E.h0 - dmg + heal, mx = role_maxhp(mask_role(C.M, hl));
