@@ -790,6 +790,19 @@ __device__ __forceinline__ void resolve_hits(const UnitMasks& M, int U, int hl, 
     }
 }
 
+// Hit points lost per team over the step, summed over the half-wave's unit lanes without cross-lane permutes: one
+// ballot per bit of the per-unit loss (0..64, 7 bits) and scalar popcounts by team (exact integer sums; the
+// shuffle-tree reduction it replaces cost five LDS permute round trips on the env step's latency path).
+__device__ __forceinline__ void team_losses(const UnitMasks& M, int loss, int hbase, int& lost0, int& lost1) {
+    lost0 = lost1 = 0;
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+        const uint32_t m = (uint32_t)(__ballot((loss >> b) & 1) >> hbase);
+        lost0 += __builtin_popcount(m & ~M.team1) << b;
+        lost1 += __builtin_popcount(m & M.team1) << b;
+    }
+}
+
 __device__ __forceinline__ int v2_avail(const UnitMasks& M, int G, int x, int y, int hp, uint32_t tgt, int k) {
     const bool alive = hp > 0;
     if (k == 0) return !alive;
@@ -1675,15 +1688,12 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
     const int hbase = (threadIdx.x & 63) & 32;
     const bool uvalid = hl < U;
     const int h0 = E.h0, h1 = E.u.hp;
-    const int my_team = (C.M.team1 >> hl) & 1;
     const uint32_t alive_m = (uint32_t)(__ballot(uvalid && h1 > 0) >> hbase);
     const uint32_t kill_m = (uint32_t)(__ballot(uvalid && h0 > 0 && h1 == 0) >> hbase);
-    int lostv = (uvalid && h0 > 0 && h0 > h1) ? (h0 - h1) << (16 * my_team) : 0;
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) lostv += __shfl_xor(lostv, m, 64);
+    int lost0, lost1;
+    team_losses(C.M, uvalid && h0 > h1 ? h0 - h1 : 0, hbase, lost0, lost1);
     const int alive0 = __builtin_popcount(alive_m & ~C.M.team1), alive1 = __builtin_popcount(alive_m & C.M.team1);
     const int kills0 = __builtin_popcount(kill_m & C.M.team1), kills1 = __builtin_popcount(kill_m & ~C.M.team1);
-    const int lost0 = lostv & 0xFFFF, lost1 = lostv >> 16;
     const int done = alive0 == 0 || alive1 == 0 || t + 1 >= spec.episode_limit;
     const int won0 = alive1 == 0 && alive0 > 0, won1 = alive0 == 0 && alive1 > 0;
     const int pt = spec.policy_team;
