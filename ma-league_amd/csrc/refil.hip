@@ -492,15 +492,33 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
         int pk[16];
         load16(S.pk[e], pk);
         const int pu = S.pk[e][u];
-        if (stepping && u < a.U) {  // executed action: validated policy action or scripted AI (spec §3.4)
-            int ac;
-            if (u < a.NA) {
-                const int pa = S.pact[e][u];
-                ac = (pa >= 0 && pa < MLG_ACT_BASE + a.U && ((avail_bits(M, pk, u, pu) >> pa) & 1u)) ? pa : 0;
-            } else {
-                ac = ai_action_reg(M, pk, u, pu);
+        {  // executed action: validated policy action or scripted AI (spec §3.4). Lanes 32-63 (no env of their
+           // own) mirror unit u of env e and scan the upper half of the units j; partials combine by permlane32
+            uint32_t tb, kb, ka, ke;
+            unit_scan<8>(M, pk, u, pu, lane >= 32, tb, kb, ka, ke);
+            auto other = [](uint32_t v) {  // lane l ^ 32
+                const auto s2 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+                return (threadIdx.x & 32) ? s2[0] : s2[1];
+            };
+            tb |= other(tb);
+            kb = min(kb, other(kb));
+            ka = min(ka, other(ka));
+            ke = min(ke, other(ke));
+            if (stepping && u < a.U) {
+                int ac;
+                if (u < a.NA) {
+                    const int pa = S.pact[e][u];
+                    const uint32_t av = pkh(pu) <= 0 ? 1u
+                                                     : (((uint32_t)(pky(pu) + 1 < M.grid) << 1) |
+                                                        ((uint32_t)(pky(pu) - 1 >= 0) << 2) |
+                                                        ((uint32_t)(pkx(pu) + 1 < M.grid) << 3) |
+                                                        ((uint32_t)(pkx(pu) - 1 >= 0) << 4) | (tb << MLG_ACT_BASE));
+                    ac = (pa >= 0 && pa < MLG_ACT_BASE + a.U && ((av >> pa) & 1u)) ? pa : 0;
+                } else {
+                    ac = ai_from_scan(M, u, pu, kb, ka, ke, [&](int j) { return S.pk[e][j]; });
+                }
+                S.act[e][u] = ac;
             }
-            S.act[e][u] = ac;
         }
         wave_sync();
         stp.mark(4);
@@ -512,6 +530,18 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
         wave_sync();
         stp.mark(5);
         if (stepping && u < a.U && S.hp[e][u] > 0) env_apply_move(S.act[e][u], &S.x[e][u], &S.y[e][u]);
+        // per-unit step results as lane ballots (bit 16 e + u): alive after, killed, bits of the hp lost (<= 64);
+        // the reward below counts them per team instead of a serial loop over the units in one lane
+        uint64_t rw_alive, rw_kill, rw_loss[7];
+        {
+            const bool v = stepping && u < a.U;
+            const int h0 = v ? S.hp[e][u] : 0, h1 = v ? S.nhp[e][u] : 0;
+            const int loss = (h0 > 0 && h0 > h1) ? h0 - h1 : 0;
+            rw_alive = __ballot(v && h1 > 0);
+            rw_kill = __ballot(v && h0 > 0 && h1 == 0);
+#pragma unroll
+            for (int bb = 0; bb < 7; ++bb) rw_loss[bb] = __ballot((loss >> bb) & 1);
+        }
         if (env_lane && u == 0) {
             const int stt = S.status[e];
             S.stepped[e] = 0;
@@ -524,14 +554,17 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
                 }
             } else if (stt == 0) {
                 int alive[2] = {0, 0}, lost[2] = {0, 0}, kills[2] = {0, 0};
-                for (int j = 0; j < a.U; ++j) {
-                    const int tm = S.team[j];
-                    const int h0 = S.hp[e][j], h1 = S.nhp[e][j];
-                    if (h0 > 0) {
-                        lost[tm] += h0 - h1 > 0 ? h0 - h1 : 0;
-                        if (h1 == 0) kills[1 - tm] += 1;
-                    }
-                    if (h1 > 0) alive[tm] += 1;
+                const uint32_t t1 = M.team1 & ((1u << a.U) - 1u);
+                const uint32_t am = (uint32_t)(rw_alive >> (16 * e)) & 0xFFFFu, km = (uint32_t)(rw_kill >> (16 * e)) & 0xFFFFu;
+                alive[0] = __builtin_popcount(am & ~t1);
+                alive[1] = __builtin_popcount(am & t1);
+                kills[0] = __builtin_popcount(km & t1);  // team-1 units killed: credited to team 0
+                kills[1] = __builtin_popcount(km & ~t1);
+#pragma unroll
+                for (int bb = 0; bb < 7; ++bb) {
+                    const uint32_t lm = (uint32_t)(rw_loss[bb] >> (16 * e)) & 0xFFFFu;
+                    lost[0] += __builtin_popcount(lm & ~t1) << bb;
+                    lost[1] += __builtin_popcount(lm & t1) << bb;
                 }
                 const int done = alive[0] == 0 || alive[1] == 0 || t + 1 >= sp.episode_limit;
                 const int w0 = alive[1] == 0 && alive[0] > 0, w1 = alive[0] == 0 && alive[1] > 0;

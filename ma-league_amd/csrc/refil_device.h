@@ -689,6 +689,57 @@ __device__ __forceinline__ int resolve_hp_reg(const EnvMasks& M, const int (&pk)
     return v < 0 ? 0 : (v > mx ? mx : v);
 }
 
+// One scan over the units j of [j0, j0 + NJ) for unit i (alive or not): target bits (as target_bits) and the scripted
+// AI's min-keys -- lowest-hp target (hp << 5 | j), nearest living ally != i and nearest living enemy (d2 << 5 | j);
+// "smallest value, then lowest j" is the rule of ai_action_reg's strict-< scans. The keys and bits of two scans
+// over disjoint j ranges combine by min / OR, so the scan can be split across lanes (bit-identical).
+template <int NJ>
+__device__ __forceinline__ void unit_scan(const EnvMasks& M, const int (&pk)[16], int i, int pi, bool upper,
+                                          uint32_t& tb, uint32_t& kbest, uint32_t& kally, uint32_t& kenemy) {
+    const int xi = pkx(pi), yi = pky(pi);
+    const int r2 = ((M.melee >> i) & 1u) ? 2 : 9;
+    const bool heal = (M.healer >> i) & 1u;
+    const uint32_t mt = (M.team1 >> i) & 1u;
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    tb = 0u;
+    kbest = kally = kenemy = NONE;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+        const int j = (upper ? 16 - NJ : 0) + k;
+        const int p = upper ? pk[16 - NJ + k] : pk[k];  // compile-time register indices (see target_bits)
+        const int hj = pkh(p);
+        const int dx = pkx(p) - xi, dy = pky(p) - yi;
+        const uint32_t d2 = (uint32_t)(dx * dx + dy * dy);
+        const uint32_t tj = (M.team1 >> j) & 1u;
+        const bool live = j < M.U && hj > 0;
+        const bool ok = heal ? (j != i && tj == mt && hj < (((M.tank >> j) & 1u) ? 64 : 32)) : (tj != mt);
+        const bool tg = live && d2 <= (uint32_t)r2 && ok;
+        tb |= (uint32_t)tg << j;
+        kbest = min(kbest, tg ? ((uint32_t)hj << 5 | (uint32_t)j) : NONE);
+        kally = min(kally, (live && j != i && tj == mt) ? (d2 << 5 | (uint32_t)j) : NONE);
+        kenemy = min(kenemy, (live && tj != mt) ? (d2 << 5 | (uint32_t)j) : NONE);
+    }
+}
+
+// The scripted AI action (ai_action_reg) from unit_scan's combined results; pkj(j) = packed state of unit j.
+template <typename PK>
+__device__ __forceinline__ int ai_from_scan(const EnvMasks& M, int i, int pi, uint32_t kbest, uint32_t kally,
+                                            uint32_t kenemy, PK pkj) {
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    if (pkh(pi) <= 0) return 0;
+    if (kbest != NONE) return MLG_ACT_BASE + (int)(kbest & 31u);
+    uint32_t k = kenemy;
+    if ((M.healer >> i) & 1u) {
+        if (kally != NONE) {
+            if ((kally >> 5) <= 2u) return 0;
+            k = kally;
+        }
+    }
+    if (k == NONE) return 0;
+    const int p = pkj((int)(k & 31u));
+    return move_toward_d(pkx(p) - pkx(pi), pky(p) - pky(pi));
+}
+
 // obs-mask row of unit u: bit j = u dead, j dead or out of sight
 __device__ __forceinline__ uint32_t om_bits(const EnvMasks& M, const int (&pk)[16], int u, int pu) {
     (void)u;
