@@ -258,9 +258,31 @@ __device__ __forceinline__ int64_t ro_slot(const MlgEntityBatch& bt, int b) {
 RO_PHASE void ro_observe(RoLds& S, const EnvTables& T, const EnvMasks& M, const RoArgs& a, const MlgEntityBatch& bt,
                          int e, int u, bool active, int t) {
     const bool me = active && u < a.U;
-    if (me) {
+    // obs-mask and target bits of unit u, the units j split between the two half-waves (lanes 32-63 mirror unit u
+    // of env e and scan j = 8..15) and ORed together by a permlane32 swap (all 64 lanes take part)
+    uint32_t om_all, tb_all;
+    {
         int pk[16];
         load16(S.pk[e], pk);
+        const int pu = S.pk[e][u];
+        const bool upper = (threadIdx.x & 32) != 0;
+        const int xu = pkx(pu), yu = pky(pu);
+        uint32_t om = 0u, tb, kb, ka, ke;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = (upper ? 8 : 0) + k;
+            const int p = upper ? pk[8 + k] : pk[k];
+            const int dx = pkx(p) - xu, dy = pky(p) - yu;
+            om |= (uint32_t)(j < M.U && (pkh(p) <= 0 || dx * dx + dy * dy > MLG_SIGHT2)) << j;
+        }
+        unit_scan<8>(M, pk, u, pu, upper, tb, kb, ka, ke);
+        const auto so = __builtin_amdgcn_permlane32_swap(om, om, false, false);
+        const auto st = __builtin_amdgcn_permlane32_swap(tb, tb, false, false);
+        om_all = om | (upper ? so[0] : so[1]);
+        tb_all = tb | (upper ? st[0] : st[1]);
+        if (pkh(pu) <= 0) om_all = (1u << M.U) - 1u;  // om_bits: a dead unit sees nothing
+    }
+    if (me) {
         const int pu = S.pk[e][u];
         const int64_t row = (S.slot[e] * (int64_t)bt.T1 + t);
         float f[8];
@@ -270,13 +292,25 @@ RO_PHASE void ro_observe(RoLds& S, const EnvTables& T, const EnvMasks& M, const 
             S.feat[e][u][k] = f[k];
             if (k < a.ED) eg[k] = f[k];
         }
-        const uint32_t bits = om_bits(M, pk, u, pu);
+        const uint32_t bits = om_all;
         uint8_t* omg = bt.obs_mask + (row * a.U + u) * a.U;
-        for (int j = 0; j < a.U; ++j) omg[j] = (uint8_t)((bits >> j) & 1u);
+        if (a.U == 16) {  // one 16-byte row (rows of U bytes: 16-byte aligned when U == 16)
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                w[q] = ((bits >> (4 * q)) & 1u) | (((bits >> (4 * q + 1)) & 1u) << 8) |
+                       (((bits >> (4 * q + 2)) & 1u) << 16) | (((bits >> (4 * q + 3)) & 1u) << 24);
+            *reinterpret_cast<uint4*>(omg) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            for (int j = 0; j < a.U; ++j) omg[j] = (uint8_t)((bits >> j) & 1u);
+        }
         S.om[e][u] = bits;
         bt.entity_mask[row * a.U + u] = (uint8_t)(pkh(pu) <= 0);
         if (u < a.NA) {
-            const uint32_t av = avail_bits(M, pk, u, pu);
+            const uint32_t av = pkh(pu) <= 0 ? 1u
+                                             : (((uint32_t)(pky(pu) + 1 < M.grid) << 1) | ((uint32_t)(pky(pu) - 1 >= 0) << 2) |
+                                                ((uint32_t)(pkx(pu) + 1 < M.grid) << 3) | ((uint32_t)(pkx(pu) - 1 >= 0) << 4) |
+                                                (tb_all << MLG_ACT_BASE));
             int32_t* ag = bt.avail + (row * a.NA + u) * a.A;
             for (int k = 0; k < a.A; ++k) ag[k] = (int)((av >> k) & 1u);
             S.av[e][u] = av;
