@@ -61,18 +61,6 @@ __host__ __device__ constexpr AgentLayout make_agent_layout(const MlgAgentDims& 
     return L;
 }
 
-// Piece `piece` (0..2) of the split-bf16 representation of the pair (a, b) as one u32 (bf16 of a low, of b high),
-// bit-identical to split3() in rollout.hip: a = a0 + a1 + a2 exactly, round to nearest per piece.
-__device__ __forceinline__ float split_bf16_pair(float a, float b, int piece) {
-    unsigned int pk = 0u;
-    for (int lvl = 0; lvl <= piece; ++lvl) {
-        pk = cvt_pk_bf16(a, b);
-        a -= __uint_as_float(pk << 16);
-        b -= __uint_as_float(pk & 0xFFFF0000u);
-    }
-    return __uint_as_float(pk);
-}
-
 // Packed float i of the kernel weight layout from the canonical nn.Module tensors (pack_agent_kernel and the
 // learner's fused prologue).
 __device__ __forceinline__ float pack_agent_elem(const AgentLayout& L, const MlgAgentParams& p, int64_t i) {

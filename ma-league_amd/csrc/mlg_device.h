@@ -47,6 +47,68 @@ __device__ __forceinline__ floatx4 mfma_bf16(bf16x8 a, bf16x8 b, floatx4 c) {
 __device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float fast_tanh(float x) { return 2.f * fast_sigmoid(2.f * x) - 1.f; }
 
+// ---- split-bf16 fp32 emulation pieces (shared by the rollout kernels) ----
+struct Split3 {
+    bf16x8 p[3];
+};
+
+// 8 fp32 -> three bf16x8 pieces (element j of every piece belongs to input j).
+__device__ __forceinline__ Split3 split3(floatx4 a, floatx4 b) {
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    Split3 s;
+#ifdef MLG_G8_NOSPLIT  // timing ablation only: one conversion, copied to all pieces
+    {
+        u32x4 w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
+        s.p[0] = s.p[1] = s.p[2] = __builtin_bit_cast(bf16x8, w);
+        return s;
+    }
+#endif
+#pragma unroll
+    for (int lvl = 0; lvl < 3; ++lvl) {
+        u32x4 w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned int pk = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
+            w[q] = pk;
+            if (lvl < 2) {  // remainders (exact in fp32)
+                v[2 * q] -= __uint_as_float(pk << 16);
+                v[2 * q + 1] -= __uint_as_float(pk & 0xFFFF0000u);
+            }
+        }
+        s.p[lvl] = __builtin_bit_cast(bf16x8, w);
+    }
+    return s;
+}
+
+
+// acc += A . B over one 32-wide K step with the six partial products (small terms first).
+__device__ __forceinline__ floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 c) {
+#ifdef MLG_G8_P1  // timing ablation only: the leading product alone
+    return mfma_bf16(a.p[0], b.p[0], c);
+#endif
+    c = mfma_bf16(a.p[2], b.p[0], c);
+    c = mfma_bf16(a.p[1], b.p[1], c);
+    c = mfma_bf16(a.p[0], b.p[2], c);
+    c = mfma_bf16(a.p[1], b.p[0], c);
+    c = mfma_bf16(a.p[0], b.p[1], c);
+    c = mfma_bf16(a.p[0], b.p[0], c);
+    return c;
+}
+
+// Piece `piece` (0..2) of the split-bf16 representation of the pair (a, b) as one u32 (bf16 of a low, of b high),
+// bit-identical to split3() in rollout.hip: a = a0 + a1 + a2 exactly, round to nearest per piece.
+__device__ __forceinline__ float split_bf16_pair(float a, float b, int piece) {
+    unsigned int pk = 0u;
+    for (int lvl = 0; lvl <= piece; ++lvl) {
+        pk = cvt_pk_bf16(a, b);
+        a -= __uint_as_float(pk << 16);
+        b -= __uint_as_float(pk & 0xFFFF0000u);
+    }
+    return __uint_as_float(pk);
+}
+
 // Workgroup barrier that orders LDS only: the release fence waits for this wave's LDS operations (lgkmcnt) but not
 // for its outstanding global stores, which __syncthreads() (a release fence over all address spaces) waits for --
 // on the rollout's per-step barriers that was the HBM write latency of the step's action / batch-row stores. Only

@@ -89,6 +89,20 @@ __global__ void copy_jobs_kernel(CopyJobs J, const float* __restrict__ src, floa
     dst[i] = v;
 }
 
+// gsp section of the packed agent (refil_device.h gru_tile_b16): element ((reg * 64 + lane) * 4 + q) = bf16 pair
+// (2q, 2q + 1) of piece `pc` of the A operand of (mat, mt, gate, kk): row gate * 64 + mt * 16 + (lane & 15), K slots
+// 2q, 2q + 1 of lane group g = lane >> 4, feature (2kk + i / 4) * 16 + 4g + i % 4 for slot i.
+__global__ void refil_pack_gsp_kernel(RAgent L, const float* __restrict__ flat, float* __restrict__ packed) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= REFIL_GSP) return;
+    const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
+    const int pc = reg % 3, kk = (reg / 3) % 2, gate = (reg / 6) % 3, mt = (reg / 18) % 4, mat = reg / 72;
+    const int row = gate * EMB + mt * 16 + (lane & 15), g = lane >> 4;
+    const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * g + i0 % 4;
+    const float* W = flat + (mat ? L.c_whh : L.c_wih) + (int64_t)row * EMB;
+    packed[L.gsp + k] = split_bf16_pair(W[f0], W[f0 + 1], pc);
+}
+
 CopyJob cj(int64_t src, int64_t dst, int rd, int cd, int rs, int cs, int64_t src2 = -1) {
     return CopyJob{src, src2, dst, rd, cd, rs, cs};
 }
@@ -205,10 +219,12 @@ __device__ inline void agent_tile_post_w(const float* __restrict__ P, const RAge
     mm_reg<4, 4>(x3, w2, ld2, 0, x2, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x3[i] = relu4(x3[i]);
-#ifdef MLG_REFIL_GRU_PLAIN
+#if defined(MLG_REFIL_GRU_PLAIN)
     gru_tile(P + L.wih, P + L.whh, P + L.bih, P + L.bhh, P + L.brz, x3, h, lane);
-#else
+#elif defined(MLG_REFIL_GRU_F32)  // A/B: f32 MFMA products (round 1)
     gru_tile_pipe(P + L.wih, P + L.whh, P + L.bih, P + L.bhh, P + L.brz, x3, h, lane);
+#else
+    gru_tile_b16(P, L, x3, h, lane);
 #endif
 }
 
@@ -742,7 +758,11 @@ extern "C" int64_t mlg_refil_packed_agent_size(const MlgRefilDims* d) {
 extern "C" int mlg_refil_pack_agent(const MlgRefilDims* d, const float* flat, float* packed, void* stream) {
     if (check_dims(d)) return 1;
     MLG_REQUIRE(flat && packed, "refil_pack_agent: null pointer");
-    return launch_copy(agent_pack_jobs(agent_layout(d)), flat, packed, (hipStream_t)stream);
+    const RAgent L = agent_layout(d);
+    if (launch_copy(agent_pack_jobs(L), flat, packed, (hipStream_t)stream)) return 1;
+    hipLaunchKernelGGL(refil_pack_gsp_kernel, dim3((unsigned)((REFIL_GSP + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       L, flat, packed);
+    return mlg::check_launch("refil_pack_gsp_kernel");
 }
 
 extern "C" int mlg_refil_agent_forward(const MlgRefilDims* d, const float* packed, const float* entities,

@@ -38,9 +38,12 @@ __device__ __forceinline__ void wave_sync() {
 //   wih [192][64], whh [192][64], bih [192], bhh [192], brz [128] (= b_ih + b_hh of r, z), w3 [Ap][64], b3 [Ap]
 // Canonical flat order (named_parameters): fc1.w [64][D0], fc1.b, attn.in_trans.w [192][64], attn.out_trans.w,
 //   attn.out_trans.b, fc2.w, fc2.b, rnn.weight_ih, rnn.weight_hh, rnn.bias_ih, rnn.bias_hh, fc3.w [A][64], fc3.b [A]
+// gsp section: W_ih / W_hh as split-bf16 MFMA A operands, [mat 2][mt 4][gate 3][kk 2][piece 3][lane 64] x 16 B
+constexpr int64_t REFIL_GSP = 2 * 4 * 3 * 2 * 3 * 64 * 4;
+
 struct RAgent {
     int D0, K1, A, Ap;
-    int64_t w1, b1, win, wout, bout, w2, b2, wih, whh, bih, bhh, brz, w3, b3, total;
+    int64_t w1, b1, win, wout, bout, w2, b2, wih, whh, bih, bhh, brz, w3, b3, gsp, total;
     // canonical offsets
     int64_t c_w1, c_b1, c_win, c_wout, c_bout, c_w2, c_b2, c_wih, c_whh, c_bih, c_bhh, c_w3, c_b3, c_total;
 };
@@ -67,6 +70,7 @@ __host__ __device__ inline RAgent make_ragent(int D0, int A) {
     L.brz = take(2 * EMB);
     L.w3 = take((int64_t)L.Ap * EMB);
     L.b3 = take(L.Ap);
+    L.gsp = take(REFIL_GSP);  // rollout GRU weights pre-split (gru_tile_b16 layout), written by mlg_refil_pack_agent
     L.total = o;
     int64_t c = 0;
     L.c_w1 = c; c += (int64_t)EMB * D0;
@@ -531,6 +535,81 @@ __device__ inline void gru_tile_pipe(const float* __restrict__ wih, const float*
             ar = mfma_chunk(w[kc * 6 + 3], h[kc], ar);
             az = mfma_chunk(w[kc * 6 + 4], h[kc], az);
             ahn = mfma_chunk(w[kc * 6 + 5], h[kc], ahn);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float rg = sigm(ar[r]);
+            const float zg = sigm(az[r]);
+            const float ng = tanhf(ain[r] + rg * ahn[r]);
+            hn[mt][r] = ng + zg * (h[mt][r] - ng);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) h[mt] = hn[mt];
+}
+
+// GRUCell tile with the products as split-bf16 fp32 emulation on the bf16 matrix cores: x and h
+// (D layout) are split once into three bf16 pieces per 32-wide K step -- K slot (g, i) of step kk holds feature
+// (2kk + i / 4) * 16 + 4g + i % 4, i.e. the lane's own registers x[2kk], x[2kk + 1] -- and the weights come
+// pre-split in that K order from the packed block (section gsp, refil_pack_gsp_kernel), streamed per (mt, kk)
+// with the next stage's 18 loads issued before the current stage's MFMAs. 288 bf16 MFMAs (16 cycles) instead of
+// 384 f32 MFMAs (32 cycles) per tile; fp32-class results (six partial products, fp32 accumulation).
+__device__ __forceinline__ int refil_gsp_reg(int mat, int mt, int gate, int kk, int piece) {
+    return ((((mat * 4 + mt) * 3 + gate) * 2 + kk) * 3 + piece) * 64;
+}
+
+__device__ inline void gru_tile_b16(const float* __restrict__ P, const RAgent& L, const floatx4 (&x)[4], floatx4 (&h)[4],
+                                    int lane) {
+    const int g = lane >> 4;
+    const u32x4* gs = reinterpret_cast<const u32x4*>(P + L.gsp) + lane;
+    const float* brz = P + L.brz;
+    const float* bih = P + L.bih;
+    const float* bhh = P + L.bhh;
+    Split3 xs[2], hs[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        xs[kk] = split3(x[2 * kk], x[2 * kk + 1]);
+        hs[kk] = split3(h[2 * kk], h[2 * kk + 1]);
+    }
+    bf16x8 wb[2][18];  // [mat * 9 + gate * 3 + piece]
+    auto load = [&](int st, bf16x8 (&w)[18]) {
+        const int mt = st >> 1, kk = st & 1;
+#pragma unroll
+        for (int mat = 0; mat < 2; ++mat)
+#pragma unroll
+            for (int gate = 0; gate < 3; ++gate)
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc)
+                    w[mat * 9 + gate * 3 + pc] = __builtin_bit_cast(bf16x8, gs[refil_gsp_reg(mat, mt, gate, kk, pc)]);
+    };
+    auto piece3 = [](const bf16x8 (&w)[18], int b) {
+        Split3 s;
+        s.p[0] = w[b];
+        s.p[1] = w[b + 1];
+        s.p[2] = w[b + 2];
+        return s;
+    };
+    floatx4 hn[4];
+    load(0, wb[0]);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        floatx4 ar = ld4(brz + mt * 16 + 4 * g);
+        floatx4 az = ld4(brz + EMB + mt * 16 + 4 * g);
+        floatx4 ain = ld4(bih + 2 * EMB + mt * 16 + 4 * g);
+        floatx4 ahn = ld4(bhh + 2 * EMB + mt * 16 + 4 * g);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int st = mt * 2 + kk;
+            if (st + 1 < 8) load(st + 1, wb[(st + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const bf16x8(&w)[18] = wb[st & 1];
+            ar = mfma_x6(piece3(w, 0), xs[kk], ar);
+            az = mfma_x6(piece3(w, 3), xs[kk], az);
+            ain = mfma_x6(piece3(w, 6), xs[kk], ain);
+            ar = mfma_x6(piece3(w, 9), hs[kk], ar);
+            az = mfma_x6(piece3(w, 12), hs[kk], az);
+            ahn = mfma_x6(piece3(w, 15), hs[kk], ahn);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

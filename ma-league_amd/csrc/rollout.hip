@@ -1223,55 +1223,6 @@ __device__ inline void ph_fc1_g8(const AgentLayout& L, const RolloutLds2& lay, f
 // inside the MFMA, in a different order than the v1/v2 fmaf chains: v7 results equal v2's to fp32 rounding,
 // not bit for bit.
 
-struct Split3 {
-    bf16x8 p[3];
-};
-
-// 8 fp32 -> three bf16x8 pieces (element j of every piece belongs to input j).
-__device__ __forceinline__ Split3 split3(floatx4 a, floatx4 b) {
-    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    Split3 s;
-#ifdef MLG_G8_NOSPLIT  // timing ablation only: one conversion, copied to all pieces
-    {
-        u32x4 w;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
-        s.p[0] = s.p[1] = s.p[2] = __builtin_bit_cast(bf16x8, w);
-        return s;
-    }
-#endif
-#pragma unroll
-    for (int lvl = 0; lvl < 3; ++lvl) {
-        u32x4 w;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const unsigned int pk = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
-            w[q] = pk;
-            if (lvl < 2) {  // remainders (exact in fp32)
-                v[2 * q] -= __uint_as_float(pk << 16);
-                v[2 * q + 1] -= __uint_as_float(pk & 0xFFFF0000u);
-            }
-        }
-        s.p[lvl] = __builtin_bit_cast(bf16x8, w);
-    }
-    return s;
-}
-
-
-// acc += A . B over one 32-wide K step with the six partial products (small terms first).
-__device__ __forceinline__ floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 c) {
-#ifdef MLG_G8_P1  // timing ablation only: the leading product alone
-    return mfma_bf16(a.p[0], b.p[0], c);
-#endif
-    c = mfma_bf16(a.p[2], b.p[0], c);
-    c = mfma_bf16(a.p[1], b.p[1], c);
-    c = mfma_bf16(a.p[0], b.p[2], c);
-    c = mfma_bf16(a.p[1], b.p[0], c);
-    c = mfma_bf16(a.p[0], b.p[1], c);
-    c = mfma_bf16(a.p[0], b.p[0], c);
-    return c;
-}
-
 // Wave w owns hidden features 8w .. 8w+7 (H = 64, 8 waves): three 16-row A blocks per 32-wide K step,
 //   rz_i = [W_ir ; W_iz] (rows 0-7 r, 8-15 z of its features)   with B = x
 //   rz_h = [W_hr ; W_hz]                                         with B = h   (same accumulator rows)
