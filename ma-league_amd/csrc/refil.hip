@@ -92,9 +92,23 @@ __global__ void copy_jobs_kernel(CopyJobs J, const float* __restrict__ src, floa
 // gsp section of the packed agent (refil_device.h gru_tile_b16): element ((reg * 64 + lane) * 4 + q) = bf16 pair
 // (2q, 2q + 1) of piece `pc` of the A operand of (mat, mt, gate, kk): row gate * 64 + mt * 16 + (lane & 15), K slots
 // 2q, 2q + 1 of lane group g = lane >> 4, feature (2kk + i / 4) * 16 + 4g + i % 4 for slot i.
+// wsp section (in_trans, out_trans, fc2 of the rollout): the same element order per (tile, kk, piece), row
+// (lane & 15) of the tile's 16 output features. One launch writes both sections.
 __global__ void refil_pack_gsp_kernel(RAgent L, const float* __restrict__ flat, float* __restrict__ packed) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= REFIL_GSP) return;
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= REFIL_GSP + REFIL_WSP) return;
+    if (k >= REFIL_GSP) {
+        k -= REFIL_GSP;
+        const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
+        const int pc = reg % 3, kk = (reg / 3) % 2, mt = reg / 6;
+        const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * (lane >> 4) + i0 % 4;
+        const int64_t src = mt < REFIL_WSP_WOUT ? L.c_win + (int64_t)mt * 16 * EMB
+                            : mt < REFIL_WSP_W2 ? L.c_wout + (int64_t)(mt - REFIL_WSP_WOUT) * 16 * EMB
+                                                : L.c_w2 + (int64_t)(mt - REFIL_WSP_W2) * 16 * EMB;
+        const float* W = flat + src + (int64_t)(lane & 15) * EMB;
+        packed[L.wsp + k] = split_bf16_pair(W[f0], W[f0 + 1], pc);
+        return;
+    }
     const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
     const int pc = reg % 3, kk = (reg / 3) % 2, gate = (reg / 6) % 3, mt = (reg / 18) % 4, mat = reg / 72;
     const int row = gate * EMB + mt * 16 + (lane & 15), g = lane >> 4;
@@ -177,6 +191,51 @@ __device__ inline void entity_block_reg(const float* __restrict__ P, const RAgen
     mm_reg<4, KC1>(x1, P + L.w1, L.K1, 0, xin, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[i] = relu4(x1[i]);
+#if !defined(MLG_REFIL_INTRANS_F32)
+    // in_trans as split-bf16 fp32 emulation (gru_tile_b16's scheme): x1 split once per 32-wide K step (K slot (g, i)
+    // of step kk = the lane's own registers x1[2kk], x1[2kk + 1]), the weights pre-split in that K order (packed
+    // section wsp), streamed in stages of 3 output tiles with the next stage's 18 loads issued before the current
+    // stage's MFMAs. Tiles 0-3 = q (agent rows only), 4-11 = k | v. 144 bf16 MFMAs instead of 192 f32 MFMAs.
+    (void)win;
+    (void)ldin;
+    {
+        Split3 xs[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) xs[kk] = split3(x1[2 * kk], x1[2 * kk + 1]);
+        const u32x4* ws = reinterpret_cast<const u32x4*>(P + L.wsp) + lane;
+        bf16x8 wb[2][18];  // [tile in stage * 6 + kk * 3 + piece]
+        auto load = [&](int stg, bf16x8 (&w)[18]) {
+#pragma unroll
+            for (int i = 0; i < 18; ++i) w[i] = __builtin_bit_cast(bf16x8, ws[(stg * 18 + i) * 64]);
+        };
+        load(0, wb[0]);
+#pragma unroll
+        for (int stg = 0; stg < 4; ++stg) {
+            if (stg + 1 < 4) load(stg + 1, wb[(stg + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const bf16x8(&w)[18] = wb[stg & 1];
+#pragma unroll
+            for (int ti = 0; ti < 3; ++ti) {
+                const int mt = stg * 3 + ti;
+                floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) {
+                    Split3 a;
+                    a.p[0] = w[ti * 6 + kk * 3 + 0];
+                    a.p[1] = w[ti * 6 + kk * 3 + 1];
+                    a.p[2] = w[ti * 6 + kk * 3 + 2];
+                    acc = mfma_x6(a, xs[kk], acc);
+                }
+                if (mt < 4) {
+                    if (col < NAS) st_row(qs, LDX, mt, acc, lane);
+                } else {
+                    st_row(kvs, LDKV, mt - 4, acc, lane);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#else
     {  // q: only the agent rows are queried
         floatx4 acc[4];
         bias_init<4>(acc, nullptr, 0, lane);
@@ -194,6 +253,7 @@ __device__ inline void entity_block_reg(const float* __restrict__ P, const RAgen
 #pragma unroll
         for (int i = 0; i < 4; ++i) st_row(kvs, LDKV, m0 - 4 + i, acc[i], lane);
     }
+#endif
     wave_sync();
     if (nq <= 8)
         attn_fwd_half(qs, LDX, kvs, kvs + EMB, LDKV, mrow, nq, ne, o, LDX, lane);
@@ -226,6 +286,52 @@ __device__ inline void agent_tile_post_w(const float* __restrict__ P, const RAge
 #else
     gru_tile_b16(P, L, x3, h, lane);
 #endif
+}
+
+// Rollout form of agent_tile_post_w with out_trans and fc2 as split-bf16 fp32 emulation: o (LDS rows) is split once
+// per 32-wide K step in the wsp K order (lane (col, g) reads features (2kk) * 16 + 4g .. + 3 and (2kk + 1) * 16 + 4g
+// .. + 3 of row col), x2 from its D-layout registers; weights from the wsp tiles 12-19, all 48 loads issued up front.
+__device__ inline void agent_tile_post_b16(const float* __restrict__ P, const RAgent& L, const float* o, uint32_t dead,
+                                           floatx4 (&h)[4], int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    const u32x4* ws = reinterpret_cast<const u32x4*>(P + L.wsp) + lane;
+    bf16x8 wo[24], w2[24];  // [tile * 6 + kk * 3 + piece]
+#pragma unroll
+    for (int i = 0; i < 24; ++i) wo[i] = __builtin_bit_cast(bf16x8, ws[(REFIL_WSP_WOUT * 6 + i) * 64]);
+    Split3 os[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+        os[kk] = split3(ld4(o + col * LDX + 2 * kk * 16 + 4 * g), ld4(o + col * LDX + (2 * kk + 1) * 16 + 4 * g));
+#pragma unroll
+    for (int i = 0; i < 24; ++i) w2[i] = __builtin_bit_cast(bf16x8, ws[(REFIL_WSP_W2 * 6 + i) * 64]);
+    auto piece3 = [](const bf16x8 (&w)[24], int b) {
+        Split3 s;
+        s.p[0] = w[b];
+        s.p[1] = w[b + 1];
+        s.p[2] = w[b + 2];
+        return s;
+    };
+    floatx4 x2[4], x3[4];
+    bias_init<4>(x2, P + L.bout, 0, lane);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) x2[mt] = mfma_x6(piece3(wo, mt * 6 + kk * 3), os[kk], x2[mt]);
+    if ((dead >> col) & 1u) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x2[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    Split3 xs[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) xs[kk] = split3(x2[2 * kk], x2[2 * kk + 1]);
+    bias_init<4>(x3, P + L.b2, 0, lane);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) x3[mt] = mfma_x6(piece3(w2, mt * 6 + kk * 3), xs[kk], x3[mt]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x3[i] = relu4(x3[i]);
+    gru_tile_b16(P, L, x3, h, lane);
 }
 
 RO_PHASE void agent_tile_post(const float* __restrict__ P, const RAgent& L, const float* o, uint32_t dead,
@@ -490,7 +596,11 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
             m |= ~((1u << a.NA) - 1u) & 0xFFu;  // padding rows >= n_agents
             dead |= (m & 0xFFu) << (8 * ee);
         }
+#if defined(MLG_REFIL_POST_F32) || defined(MLG_REFIL_GRU_PLAIN) || defined(MLG_REFIL_GRU_F32)
         agent_tile_post_w(Pw, L, SH.wout, LDW, SH.w2, LDW, S.o, dead, h, lane);
+#else
+        agent_tile_post_b16(Pw, L, S.o, dead, h, lane);
+#endif
         stp.mark(2);
         // fc3 + masked argmax + epsilon-greedy
         const int re = col >> 3, rn = col & 7;
@@ -760,7 +870,8 @@ extern "C" int mlg_refil_pack_agent(const MlgRefilDims* d, const float* flat, fl
     MLG_REQUIRE(flat && packed, "refil_pack_agent: null pointer");
     const RAgent L = agent_layout(d);
     if (launch_copy(agent_pack_jobs(L), flat, packed, (hipStream_t)stream)) return 1;
-    hipLaunchKernelGGL(refil_pack_gsp_kernel, dim3((unsigned)((REFIL_GSP + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(refil_pack_gsp_kernel, dim3((unsigned)((REFIL_GSP + REFIL_WSP + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream,
                        L, flat, packed);
     return mlg::check_launch("refil_pack_gsp_kernel");
 }

@@ -40,10 +40,14 @@ __device__ __forceinline__ void wave_sync() {
 //   attn.out_trans.b, fc2.w, fc2.b, rnn.weight_ih, rnn.weight_hh, rnn.bias_ih, rnn.bias_hh, fc3.w [A][64], fc3.b [A]
 // gsp section: W_ih / W_hh as split-bf16 MFMA A operands, [mat 2][mt 4][gate 3][kk 2][piece 3][lane 64] x 16 B
 constexpr int64_t REFIL_GSP = 2 * 4 * 3 * 2 * 3 * 64 * 4;
+// wsp section: in_trans [192][64] (tiles 0-11), out_trans [64][64] (12-15) and fc2 [64][64] (16-19) as split-bf16
+// MFMA A operands, [tile 20][kk 2][piece 3][lane 64] x 16 B
+constexpr int REFIL_WSP_WOUT = 12, REFIL_WSP_W2 = 16;
+constexpr int64_t REFIL_WSP = 20 * 2 * 3 * 64 * 4;
 
 struct RAgent {
     int D0, K1, A, Ap;
-    int64_t w1, b1, win, wout, bout, w2, b2, wih, whh, bih, bhh, brz, w3, b3, gsp, total;
+    int64_t w1, b1, win, wout, bout, w2, b2, wih, whh, bih, bhh, brz, w3, b3, gsp, wsp, total;
     // canonical offsets
     int64_t c_w1, c_b1, c_win, c_wout, c_bout, c_w2, c_b2, c_wih, c_whh, c_bih, c_bhh, c_w3, c_b3, c_total;
 };
@@ -71,6 +75,7 @@ __host__ __device__ inline RAgent make_ragent(int D0, int A) {
     L.w3 = take((int64_t)L.Ap * EMB);
     L.b3 = take(L.Ap);
     L.gsp = take(REFIL_GSP);  // rollout GRU weights pre-split (gru_tile_b16 layout), written by mlg_refil_pack_agent
+    L.wsp = take(REFIL_WSP);  // rollout in_trans / out_trans / fc2 weights pre-split, written by mlg_refil_pack_agent
     L.total = o;
     int64_t c = 0;
     L.c_w1 = c; c += (int64_t)EMB * D0;

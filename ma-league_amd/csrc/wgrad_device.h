@@ -177,6 +177,7 @@ struct BJob {
     float* db;
     int64_t ldd, ldx;
     int M, K, rows, mb, nb, chunks, ch_rows;
+    int va, vb;  // delta / x rows readable as 16-byte vectors (ld % 4 == 0, 16-byte aligned base)
     int task0;
     int64_t slab0;
 };
@@ -204,6 +205,8 @@ inline BJob bjob(const float* delta, int64_t ldd, const float* x, int64_t ldx, f
     int ch = rows / (256 / (j.mb * j.nb) + 1);
     ch = ch < 64 ? 64 : (ch > BCH ? BCH : ch);
     j.ch_rows = (ch + 3) & ~3;
+    j.va = (ldd % 4 == 0) && ((uintptr_t)delta % 16 == 0);
+    j.vb = (ldx % 4 == 0) && ((uintptr_t)x % 16 == 0);
     j.chunks = (rows + j.ch_rows - 1) / j.ch_rows;
     j.task0 = 0;
     j.slab0 = 0;
@@ -235,15 +238,11 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-    int mi[4], ki[4];
-    bool mv[4], kv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        mi[i] = mbi * 64 + i * 16 + col;
-        ki[i] = nbi * 64 + i * 16 + col;
-        mv[i] = mi[i] < jb.M;
-        kv[i] = ki[i] < jb.K;
-    }
+    // lane col reads the 4 consecutive delta columns m0 .. m0 + 3 and x columns k0 .. k0 + 3 of its row (one 16-byte
+    // load each when the row layout allows it): MFMA tile i holds m = m0 + i, tile j holds k = k0 + j. The row (K)
+    // order of every product is unchanged; only the block's output positions are permuted (undone at the store).
+    const int m0 = mbi * 64 + 4 * col, k0 = nbi * 64 + 4 * col;
+    const bool va = jb.va && m0 + 3 < jb.ldd, vb = jb.vb && k0 + 3 < jb.ldx;
     // two 4-row steps per iteration: both steps' loads are issued before the first step's MFMAs (same
     // accumulation order as one step per iteration)
     for (int rr = r0; rr < r1; rr += 8) {
@@ -252,12 +251,23 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
         for (int h = 0; h < 2; ++h) {
             const int row = rr + 4 * h + g;
             const bool rv = row < r1;
-            const float* dr = jb.delta + (int64_t)row * jb.ldd;
-            const float* xr = jb.x + (int64_t)row * jb.ldx;
+            const float* dr = jb.delta + (int64_t)row * jb.ldd + m0;
+            const float* xr = jb.x + (int64_t)row * jb.ldx + k0;
+            if (rv && va) {
+                const floatx4 v = ld4(dr);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                a[h][i] = (mv[i] && rv) ? dr[mi[i]] : 0.f;
-                b[h][i] = (kv[i] && rv) ? xr[ki[i]] : 0.f;
+                for (int i = 0; i < 4; ++i) a[h][i] = v[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[h][i] = (rv && m0 + i < jb.M) ? dr[i] : 0.f;
+            }
+            if (rv && vb) {
+                const floatx4 v = ld4(xr);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b[h][i] = v[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b[h][i] = (rv && k0 + i < jb.K) ? xr[i] : 0.f;
             }
         }
 #pragma unroll
@@ -272,19 +282,20 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
         }
     }
     float* out = slab + jb.slab0 + ((int64_t)blk * jb.chunks + ch) * BSLAB;
-    // D layout: acc[i][j] reg q -> (m = 16 i + 4 g + q, k = 16 j + col) within the block
+    // D layout: acc[i][j] reg q -> MFMA row 4g + q, i.e. the A values of lane col' = 4g + q (block row
+    // m = 4 col' + i), and MFMA column col (block column k = 4 col + j)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) out[(16 * i + 4 * g + q) * 64 + 16 * j + col] = acc[i][j][q];
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<floatx4*>(out + (4 * (4 * g + q) + i) * 64 + 4 * col) =
+                floatx4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         float s = bsum[i];
         s += __shfl_xor(s, 16);
         s += __shfl_xor(s, 32);
-        if (g == 0) out[4096 + 16 * i + col] = s;
+        if (g == 0) out[4096 + 4 * col + i] = s;
     }
 }
 
