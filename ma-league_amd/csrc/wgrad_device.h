@@ -204,7 +204,11 @@ inline BJob bjob(const float* delta, int64_t ldd, const float* x, int64_t ldx, f
     // chunk length: up to BCH rows, fewer when the job is small so that it still spreads over >= ~256 waves
     int ch = rows / (256 / (j.mb * j.nb) + 1);
     ch = ch < 64 ? 64 : (ch > BCH ? BCH : ch);
+#if defined(MLG_WGRAD_F32)
     j.ch_rows = (ch + 3) & ~3;
+#else
+    j.ch_rows = (ch + 31) & ~31;  // whole 32-row MFMA steps
+#endif
     j.va = (ldd % 4 == 0) && ((uintptr_t)delta % 16 == 0);
     j.vb = (ldx % 4 == 0) && ((uintptr_t)x % 16 == 0);
     j.chunks = (rows + j.ch_rows - 1) / j.ch_rows;
@@ -243,6 +247,50 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
     // order of every product is unchanged; only the block's output positions are permuted (undone at the store).
     const int m0 = mbi * 64 + 4 * col, k0 = nbi * 64 + 4 * col;
     const bool va = jb.va && m0 + 3 < jb.ldd, vb = jb.vb && k0 + 3 < jb.ldx;
+#if !defined(MLG_WGRAD_F32)
+    // 32-row steps on the bf16 matrix cores as split-bf16 fp32 emulation (six partial products, fp32 accumulation,
+    // mlg_device.h mfma_x6): lane (col, g) loads rows rr + 8g .. rr + 8g + 7; K slot t of its operands = row
+    // rr + 8g + t, so tile i's A operand is element i of the 8 delta vectors and tile j's B operand element j of
+    // the 8 x vectors. Same D layout (and output permutation) as the f32 form below.
+    for (int rr = r0; rr < r1; rr += 32) {
+        float a[8][4], b[8][4];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int row = rr + 8 * g + t;
+            const bool rv = row < r1;
+            const float* dr = jb.delta + (int64_t)row * jb.ldd + m0;
+            const float* xr = jb.x + (int64_t)row * jb.ldx + k0;
+            if (rv && va) {
+                const floatx4 v = ld4(dr);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[t][i] = v[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[t][i] = (rv && m0 + i < jb.M) ? dr[i] : 0.f;
+            }
+            if (rv && vb) {
+                const floatx4 v = ld4(xr);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b[t][i] = v[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b[t][i] = (rv && k0 + i < jb.K) ? xr[i] : 0.f;
+            }
+        }
+        Split3 as[4], bs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            as[i] = split3(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]});
+            bs[i] = split3(floatx4{b[0][i], b[1][i], b[2][i], b[3][i]}, floatx4{b[4][i], b[5][i], b[6][i], b[7][i]});
+#pragma unroll
+            for (int t = 0; t < 8; ++t) bsum[i] += a[t][i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_x6(as[i], bs[j], acc[i][j]);
+    }
+#else
     // two 4-row steps per iteration: both steps' loads are issued before the first step's MFMAs (same
     // accumulation order as one step per iteration)
     for (int rr = r0; rr < r1; rr += 8) {
@@ -281,6 +329,7 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
             }
         }
     }
+#endif
     float* out = slab + jb.slab0 + ((int64_t)blk * jb.chunks + ch) * BSLAB;
     // D layout: acc[i][j] reg q -> MFMA row 4g + q, i.e. the A values of lane col' = 4g + q (block row
     // m = 4 col' + i), and MFMA column col (block column k = 4 col + j)
