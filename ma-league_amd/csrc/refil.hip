@@ -467,25 +467,42 @@ __device__ inline void ro_zero_tail(const MlgEntityBatch& bt, const RoArgs& a, i
 // prologue); the waves share one LDS copy of in_trans / out_trans / fc2 (padded rows, conflict-free A reads).
 constexpr int RO_WAVES = 4;
 constexpr int LDW = EMB + 4;
+// fp32 in_trans / out_trans / fc2 copies in LDS only for the f32 A/B forms; the split-bf16 default streams the
+// pre-split weights from L2 (69 KB of LDS per workgroup instead of 156 KB)
+#if defined(MLG_REFIL_INTRANS_F32) || defined(MLG_REFIL_POST_F32) || defined(MLG_REFIL_GRU_PLAIN) || defined(MLG_REFIL_GRU_F32)
+#define RO_LDS_WEIGHTS 1
+#endif
 struct RoShared {
+#ifdef RO_LDS_WEIGHTS
     float win[3 * EMB * LDW];
     float wout[EMB * LDW];
     float w2[EMB * LDW];
+#endif
     RoLds S[RO_WAVES];
 };
 
 template <int KC1>
-__global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityEnvSpec spec, MlgEnvState st, RAgent L,
+#ifdef MLG_REFIL_W2  // experiment: two waves per SIMD (<= 256 VGPR + AGPR per lane)
+#define RO_OCC __attribute__((amdgpu_waves_per_eu(2, 2)))
+#else
+#define RO_OCC
+#endif
+__global__ void __launch_bounds__(64 * RO_WAVES) RO_OCC refil_rollout_kernel(MlgEntityEnvSpec spec, MlgEnvState st, RAgent L,
                                                                       const float* __restrict__ P, MlgEntityBatch bt,
                                                                       MlgRunInfo info, RoArgs a, float eps,
                                                                       int test_mode) {
     extern __shared__ __attribute__((aligned(16))) float ro_smem[];
     RoShared& SH = *reinterpret_cast<RoShared*>(ro_smem);
+#ifdef RO_LDS_WEIGHTS
     for (int i = threadIdx.x; i < 3 * EMB * EMB; i += blockDim.x) SH.win[(i / EMB) * LDW + i % EMB] = P[L.win + i];
     for (int i = threadIdx.x; i < EMB * EMB; i += blockDim.x) {
         SH.wout[(i / EMB) * LDW + i % EMB] = P[L.wout + i];
         SH.w2[(i / EMB) * LDW + i % EMB] = P[L.w2 + i];
     }
+    const float* sh_win = SH.win;
+#else
+    const float* sh_win = nullptr;
+#endif
     __syncthreads();
     const int wave = threadIdx.x >> 6;
     RoLds& S = SH.S[wave];
@@ -585,7 +602,7 @@ __global__ void __launch_bounds__(64 * RO_WAVES) refil_rollout_kernel(MlgEntityE
                     xin[kc][r] = v;
                 }
             stp.mark(0);
-            entity_block_reg<KC1>(Pw, L, SH.win, LDW, xin, S.q, S.kv, S.om[ee], a.NA, a.U, S.o + ee * NAS * LDX, lane);
+            entity_block_reg<KC1>(Pw, L, sh_win, LDW, xin, S.q, S.kv, S.om[ee], a.NA, a.U, S.o + ee * NAS * LDX, lane);
             stp.mark(1);
             rows += (uint64_t)a.NA;
         }
