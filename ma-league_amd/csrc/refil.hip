@@ -92,8 +92,9 @@ __global__ void copy_jobs_kernel(CopyJobs J, const float* __restrict__ src, floa
 // gsp section of the packed agent (refil_device.h gru_tile_b16): element ((reg * 64 + lane) * 4 + q) = bf16 pair
 // (2q, 2q + 1) of piece `pc` of the A operand of (mat, mt, gate, kk): row gate * 64 + mt * 16 + (lane & 15), K slots
 // 2q, 2q + 1 of lane group g = lane >> 4, feature (2kk + i / 4) * 16 + 4g + i % 4 for slot i.
-// wsp section (in_trans, out_trans, fc2 of the rollout): the same element order per (tile, kk, piece), row
-// (lane & 15) of the tile's 16 output features. One launch writes both sections.
+// wsp section (in_trans, out_trans, fc2, fc1, fc3 of the rollout): the same element order per (tile, kk, piece),
+// row (lane & 15) of the tile's 16 output features; fc1's K slots >= D0 and fc3's rows >= A are zero. One launch
+// writes both sections.
 __global__ void refil_pack_gsp_kernel(RAgent L, const float* __restrict__ flat, float* __restrict__ packed) {
     int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= REFIL_GSP + REFIL_WSP) return;
@@ -102,11 +103,26 @@ __global__ void refil_pack_gsp_kernel(RAgent L, const float* __restrict__ flat, 
         const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
         const int pc = reg % 3, kk = (reg / 3) % 2, mt = reg / 6;
         const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * (lane >> 4) + i0 % 4;
-        const int64_t src = mt < REFIL_WSP_WOUT ? L.c_win + (int64_t)mt * 16 * EMB
-                            : mt < REFIL_WSP_W2 ? L.c_wout + (int64_t)(mt - REFIL_WSP_WOUT) * 16 * EMB
-                                                : L.c_w2 + (int64_t)(mt - REFIL_WSP_W2) * 16 * EMB;
-        const float* W = flat + src + (int64_t)(lane & 15) * EMB;
-        packed[L.wsp + k] = split_bf16_pair(W[f0], W[f0 + 1], pc);
+        int64_t src;
+        int row = lane & 15, rows = EMB, cols = EMB;
+        if (mt < REFIL_WSP_WOUT) {
+            src = L.c_win + (int64_t)mt * 16 * EMB;
+        } else if (mt < REFIL_WSP_W2) {
+            src = L.c_wout + (int64_t)(mt - REFIL_WSP_WOUT) * 16 * EMB;
+        } else if (mt < REFIL_WSP_W1) {
+            src = L.c_w2 + (int64_t)(mt - REFIL_WSP_W2) * 16 * EMB;
+        } else if (mt < REFIL_WSP_W3) {
+            src = L.c_w1 + (int64_t)(mt - REFIL_WSP_W1) * 16 * L.D0;
+            cols = L.D0;
+        } else {
+            row += (mt - REFIL_WSP_W3) * 16;
+            src = L.c_w3;
+            rows = L.A;
+        }
+        const float* W = flat + src + (int64_t)row * cols;
+        const bool rv = row < rows;
+        const float w0 = rv && f0 < cols ? W[f0] : 0.f, w1 = rv && f0 + 1 < cols ? W[f0 + 1] : 0.f;
+        packed[L.wsp + k] = split_bf16_pair(w0, w1, pc);
         return;
     }
     const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
@@ -188,7 +204,30 @@ __device__ inline void entity_block_reg(const float* __restrict__ P, const RAgen
     const int col = lane & 15;
     floatx4 x1[4];
     bias_init<4>(x1, P + L.b1, 0, lane);
+#if !defined(MLG_REFIL_INTRANS_F32)
+    if constexpr (KC1 == 2) {  // K1 = 32: one split-bf16 K step over xin[0], xin[1] (wsp tiles 20-23, kk = 0)
+        const u32x4* ws = reinterpret_cast<const u32x4*>(P + L.wsp) + lane;
+        bf16x8 w[12];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                w[mt * 3 + pc] = __builtin_bit_cast(bf16x8, ws[((REFIL_WSP_W1 + mt) * 6 + pc) * 64]);
+        const Split3 xs = split3(xin[0], xin[1]);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            Split3 a;
+            a.p[0] = w[mt * 3];
+            a.p[1] = w[mt * 3 + 1];
+            a.p[2] = w[mt * 3 + 2];
+            x1[mt] = mfma_x6(a, xs, x1[mt]);
+        }
+    } else {
+        mm_reg<4, KC1>(x1, P + L.w1, L.K1, 0, xin, lane);
+    }
+#else
     mm_reg<4, KC1>(x1, P + L.w1, L.K1, 0, xin, lane);
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[i] = relu4(x1[i]);
 #if !defined(MLG_REFIL_INTRANS_F32)
@@ -302,8 +341,6 @@ __device__ inline void agent_tile_post_b16(const float* __restrict__ P, const RA
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
         os[kk] = split3(ld4(o + col * LDX + 2 * kk * 16 + 4 * g), ld4(o + col * LDX + (2 * kk + 1) * 16 + 4 * g));
-#pragma unroll
-    for (int i = 0; i < 24; ++i) w2[i] = __builtin_bit_cast(bf16x8, ws[(REFIL_WSP_W2 * 6 + i) * 64]);
     auto piece3 = [](const bf16x8 (&w)[24], int b) {
         Split3 s;
         s.p[0] = w[b];
@@ -317,6 +354,9 @@ __device__ inline void agent_tile_post_b16(const float* __restrict__ P, const RA
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) x2[mt] = mfma_x6(piece3(wo, mt * 6 + kk * 3), os[kk], x2[mt]);
+    // fc2's weights after out_trans' MFMAs are issued (wo's registers are free again: lower peak pressure)
+#pragma unroll
+    for (int i = 0; i < 24; ++i) w2[i] = __builtin_bit_cast(bf16x8, ws[(REFIL_WSP_W2 * 6 + i) * 64]);
     if ((dead >> col) & 1u) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) x2[i] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -623,8 +663,33 @@ __global__ void __launch_bounds__(64 * RO_WAVES) RO_OCC refil_rollout_kernel(Mlg
         const int re = col >> 3, rn = col & 7;
         const uint32_t avm = (rn < a.NA) ? S.av[re][rn] : 1u;
         ArgmaxState as{-INFINITY, 1 << 30};
+#if !defined(MLG_REFIL_POST_F32) && !defined(MLG_REFIL_GRU_PLAIN) && !defined(MLG_REFIL_GRU_F32)
+        Split3 hs3[2];  // fc3 as split-bf16 (wsp tiles 24-25; Ap <= 32 host-checked)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) hs3[kk] = split3(h[2 * kk], h[2 * kk + 1]);
+#endif
         for (int at = 0; at < L.Ap / 16; ++at) {
+#if !defined(MLG_REFIL_POST_F32) && !defined(MLG_REFIL_GRU_PLAIN) && !defined(MLG_REFIL_GRU_F32)
+            floatx4 q;
+            {
+                const u32x4* ws = reinterpret_cast<const u32x4*>(Pw + L.wsp) + lane;
+                bf16x8 w[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) w[i] = __builtin_bit_cast(bf16x8, ws[((REFIL_WSP_W3 + at) * 6 + i) * 64]);
+                q = ld4(Pw + L.b3 + at * 16 + 4 * g);
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) {
+                    Split3 a3;
+                    a3.p[0] = w[kk * 3];
+                    a3.p[1] = w[kk * 3 + 1];
+                    a3.p[2] = w[kk * 3 + 2];
+                    q = mfma_x6(a3, hs3[kk], q);
+                }
+                if ((dead >> (lane & 15)) & 1u) q = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+#else
             const floatx4 q = agent_q(Pw, L, h, at, dead, lane);
+#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int ac = at * 16 + 4 * g + r;

@@ -40,10 +40,11 @@ __device__ __forceinline__ void wave_sync() {
 //   attn.out_trans.b, fc2.w, fc2.b, rnn.weight_ih, rnn.weight_hh, rnn.bias_ih, rnn.bias_hh, fc3.w [A][64], fc3.b [A]
 // gsp section: W_ih / W_hh as split-bf16 MFMA A operands, [mat 2][mt 4][gate 3][kk 2][piece 3][lane 64] x 16 B
 constexpr int64_t REFIL_GSP = 2 * 4 * 3 * 2 * 3 * 64 * 4;
-// wsp section: in_trans [192][64] (tiles 0-11), out_trans [64][64] (12-15) and fc2 [64][64] (16-19) as split-bf16
-// MFMA A operands, [tile 20][kk 2][piece 3][lane 64] x 16 B
-constexpr int REFIL_WSP_WOUT = 12, REFIL_WSP_W2 = 16;
-constexpr int64_t REFIL_WSP = 20 * 2 * 3 * 64 * 4;
+// wsp section: in_trans [192][64] (tiles 0-11), out_trans [64][64] (12-15), fc2 [64][64] (16-19), fc1 [64][D0]
+// (20-23, K slots >= D0 zero) and fc3 [A][64] (24-25, rows >= A zero) as split-bf16 MFMA A operands,
+// [tile 26][kk 2][piece 3][lane 64] x 16 B
+constexpr int REFIL_WSP_WOUT = 12, REFIL_WSP_W2 = 16, REFIL_WSP_W1 = 20, REFIL_WSP_W3 = 24;
+constexpr int64_t REFIL_WSP = 26 * 2 * 3 * 64 * 4;
 
 struct RAgent {
     int D0, K1, A, Ap;
