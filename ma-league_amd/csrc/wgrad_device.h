@@ -3,6 +3,8 @@
 // per (job, 16x16 tile, chunk), MFMA with the row index as K) and summed over chunks in a fixed order
 // (deterministic). The reduce pass also emits per-block sums of squares for clip_grad_norm_.
 #pragma once
+#include <cstdlib>
+
 #include "mlg_device.h"
 
 namespace mlg {
@@ -202,7 +204,12 @@ inline BJob bjob(const float* delta, int64_t ldd, const float* x, int64_t ldx, f
     j.mb = (M + 63) / 64;
     j.nb = (K + 63) / 64;
     // chunk length: up to BCH rows, fewer when the job is small so that it still spreads over >= ~256 waves
-    int ch = rows / (256 / (j.mb * j.nb) + 1);
+    static const int target = [] {  // waves per job (MLG_WGRAD_WAVES overrides, for tuning runs)
+        const char* e = getenv("MLG_WGRAD_WAVES");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? v : 256;
+    }();
+    int ch = rows / (target / (j.mb * j.nb) + 1);
     ch = ch < 64 ? 64 : (ch > BCH ? BCH : ch);
 #if defined(MLG_WGRAD_F32)
     j.ch_rows = (ch + 3) & ~3;
