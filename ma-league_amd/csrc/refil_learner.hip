@@ -170,7 +170,14 @@ struct CopyJobs {
     int64_t total;
 };
 
-__global__ void copy_jobs_kernel(CopyJobs J, const float* __restrict__ src, float* __restrict__ dst) {
+// One launch packs several parameter blocks with the same layout: blockIdx.y selects the (src, dst) pair.
+struct CopyPairs {
+    const float* src[8];
+    float* dst[8];
+};
+__global__ void copy_jobs_kernel(CopyJobs J, CopyPairs pp) {
+    const float* __restrict__ src = pp.src[blockIdx.y];
+    float* __restrict__ dst = pp.dst[blockIdx.y];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= J.total) return;
     float v = 0.f;
@@ -211,7 +218,7 @@ CopyJobs agent_jobs(const RAgent& L) {
     J.j[J.n++] = cj(L.c_bih, L.brz, 1, 2 * EMB, 1, 2 * EMB, L.c_bhh);
     J.j[J.n++] = cj(L.c_w3, L.w3, L.Ap, EMB, L.A, EMB);
     J.j[J.n++] = cj(L.c_b3, L.b3, 1, L.Ap, 1, L.A);
-    J.total = L.total;
+    J.total = L.gsp;  // the rollout's pre-split sections (gsp, wsp) are not read by the learner
     return J;
 }
 
@@ -229,11 +236,22 @@ CopyJobs hyper_jobs(const RHyper& L) {
     return J;
 }
 
-__global__ void transpose_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols) {
+// All the prologue's weight transposes in one launch: blockIdx.y = job.
+struct TrJob {
+    const float* src;
+    float* dst;
+    int rows, cols;
+};
+struct TrJobs {
+    TrJob j[16];
+    int n;
+};
+__global__ void transpose_kernel(TrJobs J) {
+    const TrJob& t = J.j[blockIdx.y];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)rows * cols) return;
-    const int r = (int)(i / cols), c = (int)(i % cols);
-    dst[(int64_t)c * rows + r] = src[i];
+    if (i >= (int64_t)t.rows * t.cols) return;
+    const int r = (int)(i / t.cols), c = (int)(i % t.cols);
+    t.dst[(int64_t)c * t.rows + r] = t.src[i];
 }
 
 __device__ __forceinline__ int64_t eslot(const MlgEntityBatch& bt, int b) {
@@ -1235,30 +1253,34 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     const float* params = bufs->params;
     const float* tparams = bufs->target_params;
     const WsR& w = p.w;
-    auto copy = [&](const CopyJobs& J, const float* src, float* dst) {
-        hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((J.total + 255) / 256)), dim3(256), 0, s, J, src, dst);
-    };
-    auto tr = [&](const float* src, float* dst, int rows, int cols) {
-        hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((rows * cols + 255) / 256)), dim3(256), 0, s, src, dst, rows,
-                           cols);
-    };
-    // ---- pack ----
+    // ---- pack: three launches (agent blocks, hypernet blocks, all transposes) ----
     const CopyJobs aj = agent_jobs(p.La), hj = hyper_jobs(p.Lh);
-    copy(aj, params, ws + w.pa_on);
-    copy(aj, tparams, ws + w.pa_tg);
+    CopyPairs ap{}, hpp{};
+    ap.src[0] = params;
+    ap.dst[0] = ws + w.pa_on;
+    ap.src[1] = tparams;
+    ap.dst[1] = ws + w.pa_tg;
+    hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((aj.total + 255) / 256), 2), dim3(256), 0, s, aj, ap);
     const RAgent& La = p.La;
+    TrJobs tj{};
+    auto tr = [&](const float* src, float* dst, int rows, int cols) { tj.j[tj.n++] = TrJob{src, dst, rows, cols}; };
     tr(params + La.c_win, ws + w.a_winT, 3 * EMB, EMB);
     tr(params + La.c_wout, ws + w.a_woutT, EMB, EMB);
     tr(params + La.c_w2, ws + w.a_w2T, EMB, EMB);
     tr(params + La.c_wih, ws + w.a_wihT, 3 * EMB, EMB);
     for (int k = 0; k < 4; ++k) {
         const int64_t G0 = p.n_agent + (int64_t)k * p.Lh.c_total;
-        copy(hj, params + G0, ws + w.ph_on[k]);
-        copy(hj, tparams + G0, ws + w.ph_tg[k]);
+        hpp.src[2 * k] = params + G0;
+        hpp.dst[2 * k] = ws + w.ph_on[k];
+        hpp.src[2 * k + 1] = tparams + G0;
+        hpp.dst[2 * k + 1] = ws + w.ph_tg[k];
         tr(params + G0 + p.Lh.c_win, ws + w.h_winT[k], 3 * EMB, EMB);
         tr(params + G0 + p.Lh.c_wout, ws + w.h_woutT[k], EMB, EMB);
         tr(params + G0 + p.Lh.c_w2, ws + w.h_w2T[k], EM, EMB);
     }
+    hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((hj.total + 255) / 256), 8), dim3(256), 0, s, hj, hpp);
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((3 * EMB * EMB + 255) / 256), (unsigned)tj.n), dim3(256), 0, s,
+                       tj);
     (void)hipMemsetAsync(ws + w.d2, 0, sizeof(float) * (size_t)c.T * c.Ron * c.A, s);
     (void)hipMemsetAsync(ws + w.dq, 0, sizeof(float) * (size_t)c.T * c.Ron, s);
     hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + w.msum);
