@@ -37,9 +37,11 @@ struct RCfg {
     float gamma, lmbda;
 };
 
+constexpr int64_t REFIL_HSP = 12 * 2 * 3 * 64 * 4;  // split hypernet in_trans (hyper_split_kernel)
 struct WsR {
     int64_t pa_on, pa_tg, ph_on[4], ph_tg[4];
     int64_t a_winT, a_woutT, a_w2T, a_wihT, h_winT[4], h_woutT[4], h_w2T[4];
+    int64_t h_wsp[8];  // hypernet in_trans as split-bf16 A operands (hyper_fwd), [k + 4 net]
     int64_t ein, x1, qkv, P, o, x2, x3, gi_on, gi_tg, hs_on, hs_tg, gr, gz, gn, ghn, mac, tmac;
     int64_t x1m[4], qkvm[4], Pm[4], om[4], x2m[4], X[4], Xtg[4], dX[4], doutm[4], dqkvm[4], dfc1m[4];
     int64_t dq, d2, part, msum, dgi, dgh, dfc2, dout, dqkv, dfc1;
@@ -112,6 +114,7 @@ Plan make_plan(const MlgRefilLearnerCfg* cfg, int T1) {
         w.h_woutT[k] = take(EMB * EMB);
         w.h_w2T[k] = take(EMB * EM);
     }
+    for (int k = 0; k < 8; ++k) w.h_wsp[k] = take(REFIL_HSP);
     w.ein = take(I * NE * c.K1);
     w.x1 = take(I * NE * EMB);
     w.qkv = take(I * NE * 3 * EMB);
@@ -234,6 +237,60 @@ CopyJobs hyper_jobs(const RHyper& L) {
     J.j[J.n++] = cj(L.c_b2, L.b2, 1, EM, 1, EM);
     J.total = L.total;
     return J;
+}
+
+// Hypernet in_trans [192][64] as split-bf16 MFMA A operands for hyper_fwd (the rollout's wsp tiles 0-11 layout:
+// element ((reg * 64 + lane) * 4 + q), reg = (tile * 2 + kk) * 3 + piece), blockIdx.y = (hypernet, net) block.
+struct HSplit {
+    const float* src[8];
+    float* dst[8];
+};
+__global__ void hyper_split_kernel(HSplit J) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= REFIL_HSP) return;
+    const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
+    const int pc = reg % 3, kk = (reg / 3) % 2, mt = reg / 6;
+    const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * (lane >> 4) + i0 % 4;
+    const float* W = J.src[blockIdx.y] + (int64_t)(mt * 16 + (lane & 15)) * EMB;
+    J.dst[blockIdx.y][k] = split_bf16_pair(W[f0], W[f0 + 1], pc);
+}
+
+// Y = in_trans(X) over one 16-row tile (X, Y in LDS) as split-bf16 fp32 emulation (six partial products; the
+// rollout's entity_block_reg scheme): X rows split once per 32-wide K step in the wsp K order, weights streamed in
+// 3-tile stages. Replaces dense_lds<false>(win, ...) -- 144 bf16 MFMAs instead of 192 f32 MFMAs.
+__device__ inline void in_trans_lds_b16(const float* __restrict__ wsp, const float* X, float* Y, int ldy, int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    Split3 xs[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+        xs[kk] = split3(ld4(X + col * LDX + 2 * kk * 16 + 4 * g), ld4(X + col * LDX + (2 * kk + 1) * 16 + 4 * g));
+    const u32x4* ws = reinterpret_cast<const u32x4*>(wsp) + lane;
+    bf16x8 wb[2][18];
+    auto load = [&](int stg, bf16x8 (&w)[18]) {
+#pragma unroll
+        for (int i = 0; i < 18; ++i) w[i] = __builtin_bit_cast(bf16x8, ws[(stg * 18 + i) * 64]);
+    };
+    load(0, wb[0]);
+#pragma unroll
+    for (int stg = 0; stg < 4; ++stg) {
+        if (stg + 1 < 4) load(stg + 1, wb[(stg + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8(&w)[18] = wb[stg & 1];
+#pragma unroll
+        for (int ti = 0; ti < 3; ++ti) {
+            floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                Split3 a;
+                a.p[0] = w[ti * 6 + kk * 3];
+                a.p[1] = w[ti * 6 + kk * 3 + 1];
+                a.p[2] = w[ti * 6 + kk * 3 + 2];
+                acc = mfma_x6(a, xs[kk], acc);
+            }
+            st_row(Y, ldy, stg * 3 + ti, acc, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // All the prologue's weight transposes in one launch: blockIdx.y = job.
@@ -581,6 +638,7 @@ __global__ void __launch_bounds__(128) q_kernel(RCfg c, MlgEntityBatch bt, RAgen
 
 // ---- hypernet forward: grid (I, 8): y = k + 4 * net -------------------------------------------------------
 struct HypPtrs {
+    const float* Wsp[8];  // split in_trans of (k, net) at [k + 4 net]
     const float* Pon[4];
     const float* Ptg[4];
     float* x1m[4];
@@ -639,7 +697,11 @@ __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt
     wave_sync();
     dense_lds<true>(P + L.w1, L.K1, P + L.b1, EMB / 16, s_ein, LDI, L.K1 / 16, s_x1, LDX, lane);
     wave_sync();
+#if defined(MLG_HYPER_F32)
     dense_lds<false>(P + L.win, EMB, nullptr, 3 * EMB / 16, s_x1, LDX, EMB / 16, s_qkv, LDQ, lane);
+#else
+    in_trans_lds_b16(hp.Wsp[k + 4 * net], s_x1, s_qkv, LDQ, lane);
+#endif
     wave_sync();
     if (!net) {
         for (int q = lane; q < NE * EMB; q += 64) hp.x1m[k][(int64_t)i * NE * EMB + q] = s_x1[(q / EMB) * LDX + q % EMB];
@@ -1279,6 +1341,15 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         tr(params + G0 + p.Lh.c_w2, ws + w.h_w2T[k], EM, EMB);
     }
     hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((hj.total + 255) / 256), 8), dim3(256), 0, s, hj, hpp);
+    HSplit hs{};
+    for (int k = 0; k < 4; ++k) {
+        const int64_t G0 = p.n_agent + (int64_t)k * p.Lh.c_total;
+        hs.src[k] = params + G0 + p.Lh.c_win;
+        hs.src[k + 4] = tparams + G0 + p.Lh.c_win;
+        hs.dst[k] = ws + w.h_wsp[k];
+        hs.dst[k + 4] = ws + w.h_wsp[k + 4];
+    }
+    hipLaunchKernelGGL(hyper_split_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 8), dim3(256), 0, s, hs);
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((3 * EMB * EMB + 255) / 256), (unsigned)tj.n), dim3(256), 0, s,
                        tj);
     (void)hipMemsetAsync(ws + w.d2, 0, sizeof(float) * (size_t)c.T * c.Ron * c.A, s);
@@ -1299,6 +1370,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
                        ws + w.pa_on, ws + w.pa_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.mac, ws + w.tmac, ws + w.msum);
     // ---- mixer ----
     HypPtrs hp;
+    for (int k = 0; k < 8; ++k) hp.Wsp[k] = ws + w.h_wsp[k];
     for (int k = 0; k < 4; ++k) {
         hp.Pon[k] = ws + w.ph_on[k];
         hp.Ptg[k] = ws + w.ph_tg[k];
