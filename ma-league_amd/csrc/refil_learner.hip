@@ -41,7 +41,7 @@ constexpr int64_t REFIL_HSP = 12 * 2 * 3 * 64 * 4;  // split hypernet in_trans (
 struct WsR {
     int64_t pa_on, pa_tg, ph_on[4], ph_tg[4];
     int64_t a_winT, a_woutT, a_w2T, a_wihT, h_winT[4], h_woutT[4], h_w2T[4];
-    int64_t h_wsp[8];  // hypernet in_trans as split-bf16 A operands (hyper_fwd), [k + 4 net]
+    int64_t h_wsp[10];  // in_trans as split-bf16 A operands: hypernet k of net at [k + 4 net], agent net at [8 + net]
     int64_t ein, x1, qkv, P, o, x2, x3, gi_on, gi_tg, hs_on, hs_tg, gr, gz, gn, ghn, mac, tmac;
     int64_t x1m[4], qkvm[4], Pm[4], om[4], x2m[4], X[4], Xtg[4], dX[4], doutm[4], dqkvm[4], dfc1m[4];
     int64_t dq, d2, part, msum, dgi, dgh, dfc2, dout, dqkv, dfc1;
@@ -114,7 +114,7 @@ Plan make_plan(const MlgRefilLearnerCfg* cfg, int T1) {
         w.h_woutT[k] = take(EMB * EMB);
         w.h_w2T[k] = take(EMB * EM);
     }
-    for (int k = 0; k < 8; ++k) w.h_wsp[k] = take(REFIL_HSP);
+    for (int k = 0; k < 10; ++k) w.h_wsp[k] = take(REFIL_HSP);
     w.ein = take(I * NE * c.K1);
     w.x1 = take(I * NE * EMB);
     w.qkv = take(I * NE * 3 * EMB);
@@ -242,8 +242,8 @@ CopyJobs hyper_jobs(const RHyper& L) {
 // Hypernet in_trans [192][64] as split-bf16 MFMA A operands for hyper_fwd (the rollout's wsp tiles 0-11 layout:
 // element ((reg * 64 + lane) * 4 + q), reg = (tile * 2 + kk) * 3 + piece), blockIdx.y = (hypernet, net) block.
 struct HSplit {
-    const float* src[8];
-    float* dst[8];
+    const float* src[10];
+    float* dst[10];
 };
 __global__ void hyper_split_kernel(HSplit J) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -418,6 +418,7 @@ __device__ __forceinline__ uint32_t dead_bits(const RCfg& c, uint32_t em) {
 struct AgentPtrs {
     const float* P;
     float *x1, *qkv, *Pw, *o, *x2, *x3, *gi;
+    const float* wsp;  // split-bf16 in_trans (hyper_split_kernel layout)
 };
 
 __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
@@ -466,7 +467,11 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, 
         wave_sync();
         dense_lds<true>(A.P + L.w1, L.K1, A.P + L.b1, EMB / 16, s_ein, LDI, L.K1 / 16, s_x1, LDX, lane);
         wave_sync();
+#if defined(MLG_HYPER_F32)
         dense_lds<false>(A.P + L.win, EMB, nullptr, 3 * EMB / 16, s_x1, LDX, EMB / 16, s_qkv, LDQ, lane);
+#else
+        in_trans_lds_b16(A.wsp, s_x1, s_qkv, LDQ, lane);
+#endif
         wave_sync();
         if (online) {
             for (int k = lane; k < NE * EMB; k += 64) A.x1[(int64_t)i * NE * EMB + k] = s_x1[(k / EMB) * LDX + k % EMB];
@@ -1349,7 +1354,11 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hs.dst[k] = ws + w.h_wsp[k];
         hs.dst[k + 4] = ws + w.h_wsp[k + 4];
     }
-    hipLaunchKernelGGL(hyper_split_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 8), dim3(256), 0, s, hs);
+    hs.src[8] = params + La.c_win;
+    hs.src[9] = tparams + La.c_win;
+    hs.dst[8] = ws + w.h_wsp[8];
+    hs.dst[9] = ws + w.h_wsp[9];
+    hipLaunchKernelGGL(hyper_split_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 10), dim3(256), 0, s, hs);
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((3 * EMB * EMB + 255) / 256), (unsigned)tj.n), dim3(256), 0, s,
                        tj);
     (void)hipMemsetAsync(ws + w.d2, 0, sizeof(float) * (size_t)c.T * c.Ron * c.A, s);
@@ -1358,8 +1367,9 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     const int64_t n_ein = (int64_t)c.I * NE * c.K1;
     hipLaunchKernelGGL(ein_kernel, dim3((unsigned)((n_ein + 255) / 256)), dim3(256), 0, s, c, bt, ws + w.ein);
     // ---- agent forward ----
-    AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on};
-    AgentPtrs tg{ws + w.pa_tg, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ws + w.gi_tg};
+    AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on,
+                 ws + w.h_wsp[8]};
+    AgentPtrs tg{ws + w.pa_tg, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ws + w.gi_tg, ws + w.h_wsp[9]};
     hipLaunchKernelGGL(ent_fwd_kernel, dim3((unsigned)((c.I + 1) / 2), 2), dim3(64), 0, s, c, bt, bufs->groupA, La,
                        ws + w.ein, on, tg, ws + w.msum);
     const int nt_on = (c.Ron + 15) / 16, nt_tg = (c.Rtg + 15) / 16;
