@@ -41,7 +41,7 @@ constexpr int64_t REFIL_HSP = 12 * 2 * 3 * 64 * 4;  // split hypernet in_trans (
 struct WsR {
     int64_t pa_on, pa_tg, ph_on[4], ph_tg[4];
     int64_t a_winT, a_woutT, a_w2T, a_wihT, h_winT[4], h_woutT[4], h_w2T[4];
-    int64_t h_wsp[10];  // in_trans as split-bf16 A operands: hypernet k of net at [k + 4 net], agent net at [8 + net]
+    int64_t h_wsp[10], h_wspT[5];  // + in_trans^T split for hyper_bwd (hypernet k) / ent_bwd (agent: [4])  // in_trans as split-bf16 A operands: hypernet k of net at [k + 4 net], agent net at [8 + net]
     int64_t ein, x1, qkv, P, o, x2, x3, gi_on, gi_tg, hs_on, hs_tg, gr, gz, gn, ghn, mac, tmac;
     int64_t x1m[4], qkvm[4], Pm[4], om[4], x2m[4], X[4], Xtg[4], dX[4], doutm[4], dqkvm[4], dfc1m[4];
     int64_t dq, d2, part, msum, dgi, dgh, dfc2, dout, dqkv, dfc1;
@@ -115,6 +115,7 @@ Plan make_plan(const MlgRefilLearnerCfg* cfg, int T1) {
         w.h_w2T[k] = take(EMB * EM);
     }
     for (int k = 0; k < 10; ++k) w.h_wsp[k] = take(REFIL_HSP);
+    for (int k = 0; k < 5; ++k) w.h_wspT[k] = take(REFIL_HSP);
     w.ein = take(I * NE * c.K1);
     w.x1 = take(I * NE * EMB);
     w.qkv = take(I * NE * 3 * EMB);
@@ -253,6 +254,52 @@ __global__ void hyper_split_kernel(HSplit J) {
     const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * (lane >> 4) + i0 % 4;
     const float* W = J.src[blockIdx.y] + (int64_t)(mt * 16 + (lane & 15)) * EMB;
     J.dst[blockIdx.y][k] = split_bf16_pair(W[f0], W[f0 + 1], pc);
+}
+
+// in_trans^T [64][192] (the dX1 = W_in^T dQKV operand of the backward kernels) as split-bf16 A operands, from the
+// canonical in_trans [192][64]: element ((reg * 64 + lane) * 4 + q), reg = (tile * 6 + kk) * 3 + piece, tile < 4,
+// kk < 6 (K = 192). blockIdx.y = block (src[y] canonical in_trans, dst[y]).
+__global__ void hyper_splitT_kernel(HSplit J) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= REFIL_HSP) return;
+    const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
+    const int pc = reg % 3, kk = (reg / 3) % 6, mt = reg / 18;
+    const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * (lane >> 4) + i0 % 4;
+    const int row = mt * 16 + (lane & 15);
+    const float* W = J.src[blockIdx.y];
+    J.dst[blockIdx.y][k] = split_bf16_pair(W[(int64_t)f0 * EMB + row], W[(int64_t)(f0 + 1) * EMB + row], pc);
+}
+
+// acc[mt] += in_trans^T . X over one 16-row tile (X = dQKV rows in LDS, K = 192) as split-bf16 fp32 emulation;
+// replaces mm_lds<4>(acc, winT, 3 * EMB, 0, X, LDQ, 12, lane). Weights streamed per output tile (18 loads).
+__device__ inline void in_transT_lds_b16(floatx4 (&acc)[4], const float* __restrict__ wspT, const float* X, int lane) {
+    const int col = lane & 15, g = lane >> 4;
+    Split3 xs[6];
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk)
+        xs[kk] = split3(ld4(X + col * LDQ + 2 * kk * 16 + 4 * g), ld4(X + col * LDQ + (2 * kk + 1) * 16 + 4 * g));
+    const u32x4* ws = reinterpret_cast<const u32x4*>(wspT) + lane;
+    bf16x8 wb[2][18];
+    auto load = [&](int mt, bf16x8 (&w)[18]) {
+#pragma unroll
+        for (int i = 0; i < 18; ++i) w[i] = __builtin_bit_cast(bf16x8, ws[(mt * 18 + i) * 64]);
+    };
+    load(0, wb[0]);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+        if (mt + 1 < 4) load(mt + 1, wb[(mt + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8(&w)[18] = wb[mt & 1];
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+            Split3 a;
+            a.p[0] = w[kk * 3];
+            a.p[1] = w[kk * 3 + 1];
+            a.p[2] = w[kk * 3 + 2];
+            acc[mt] = mfma_x6(a, xs[kk], acc[mt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // Y = in_trans(X) over one 16-row tile (X, Y in LDS) as split-bf16 fp32 emulation (six partial products; the
@@ -947,6 +994,7 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, M
 
 // ---- hypernet backward: grid (I, 4), one wave ---------------------------------------------------------------
 struct HypBwd {
+    const float* wspT[4];
     const float* Pon[4];
     const float* woutT[4];
     const float* w2T[4];
@@ -1020,7 +1068,11 @@ __global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c, MlgEntityBatch bt
     // dx1 = W_in^T dqkv * relu'(x1)
     floatx4 dx1[4];
     bias_init<4>(dx1, nullptr, 0, lane);
+#if defined(MLG_HYPER_F32)
     mm_lds<4>(dx1, hb.winT[k], 3 * EMB, 0, s_dqkv, LDQ, 3 * EMB / 16, lane);
+#else
+    in_transT_lds_b16(dx1, hb.wspT[k], s_dqkv, lane);
+#endif
     const float* x1 = hb.x1m[k] + ((int64_t)i * NE + col) * EMB;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1134,6 +1186,7 @@ __global__ void __launch_bounds__(256) rec_bwd_kernel(RCfg c, MlgEntityBatch bt,
 // ---- agent entity block backward: one wave per item pair --------------------------------------------------
 struct EntBwd {
     const float *wihT, *w2T, *woutT, *winT;
+    const float* wspT;
     const float *x1, *qkv, *Pw, *x3, *dgi;
     float *dfc2, *dout, *dqkv, *dfc1;
 };
@@ -1224,7 +1277,11 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, 
             eb.dqkv[(int64_t)ii * NE * 3 * EMB + q] = s_dqkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)];
         floatx4 dx1[4];
         bias_init<4>(dx1, nullptr, 0, lane);
+#if defined(MLG_HYPER_F32)
         mm_lds<4>(dx1, eb.winT, 3 * EMB, 0, s_dqkv, LDQ, 3 * EMB / 16, lane);
+#else
+        in_transT_lds_b16(dx1, eb.wspT, s_dqkv, lane);
+#endif
         const float* x1 = eb.x1 + ((int64_t)ii * NE + col) * EMB;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1359,6 +1416,14 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     hs.dst[8] = ws + w.h_wsp[8];
     hs.dst[9] = ws + w.h_wsp[9];
     hipLaunchKernelGGL(hyper_split_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 10), dim3(256), 0, s, hs);
+    HSplit hsT{};
+    for (int k = 0; k < 4; ++k) {
+        hsT.src[k] = hs.src[k];
+        hsT.dst[k] = ws + w.h_wspT[k];
+    }
+    hsT.src[4] = params + La.c_win;
+    hsT.dst[4] = ws + w.h_wspT[4];
+    hipLaunchKernelGGL(hyper_splitT_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 5), dim3(256), 0, s, hsT);
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((3 * EMB * EMB + 255) / 256), (unsigned)tj.n), dim3(256), 0, s,
                        tj);
     (void)hipMemsetAsync(ws + w.d2, 0, sizeof(float) * (size_t)c.T * c.Ron * c.A, s);
@@ -1413,6 +1478,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hb.woutT[k] = ws + w.h_woutT[k];
         hb.w2T[k] = ws + w.h_w2T[k];
         hb.winT[k] = ws + w.h_winT[k];
+        hb.wspT[k] = ws + w.h_wspT[k];
         hb.x1m[k] = ws + w.x1m[k];
         hb.qkvm[k] = ws + w.qkvm[k];
         hb.Pm[k] = ws + w.Pm[k];
@@ -1425,7 +1491,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     // ---- agent backward ----
     hipLaunchKernelGGL(rec_bwd_kernel, dim3((unsigned)nt_on), dim3(256), 0, s, c, bt, La, ws + w.pa_on, ws + w.hs_on,
                        ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.dq, ws + w.dgi, ws + w.dgh, ws + w.msum);
-    EntBwd eb{ws + w.a_wihT, ws + w.a_w2T, ws + w.a_woutT, ws + w.a_winT, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.x3,
+    EntBwd eb{ws + w.a_wihT, ws + w.a_w2T, ws + w.a_woutT, ws + w.a_winT, ws + w.h_wspT[4], ws + w.x1, ws + w.qkv, ws + w.P, ws + w.x3,
               ws + w.dgi, ws + w.dfc2, ws + w.dout, ws + w.dqkv, ws + w.dfc1};
     hipLaunchKernelGGL(ent_bwd_kernel, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt, eb, ws + w.msum);
     // ---- weight gradients, clip, RMSprop ----
