@@ -1,27 +1,33 @@
-"""bench.py -- env-steps/sec (rollout + learn), 5v5 QMIX, 4096 envs per GPU (BASELINE.json configs 2-4).
+"""bench.py -- env-steps/sec (rollout + learn), 5v5 QMIX, 4096 envs per GPU (BASELINE.json configs 2-5).
 
 One "step" = one training iteration of a learner: one batched rollout launch over its 4096 envs + insert into
 the HBM replay buffer + one QLearner.train on 32 sampled episodes (MultiAgentExperiment._train_episode,
 src/runs/train/ma_experiment.py:224-241). value = env steps (t_env increments, parallel_stepper.py:178-179)
 of all ranks / max-over-ranks time.
 
-Modes (--mode auto = ai at every N: the metric's config-2 workload per GPU, weak scaling):
-  ai        config 2: one learner vs the scripted AI per GPU; N > 1 = N independent learners (one per GPU,
-            4096 envs each, no data-path collective: learners never exchange anything on the rollout/learn path)
-  refil     config 5: REFIL (entity-attention agent, imagined groups, FlexQMixer), 3-8 agents per env padded to 8,
-            4096 envs per GPU vs the scripted AI (entity env variant); N > 1 = independent replicas
-  league    config 3 (N = 2: two PFSP self-play learners, opponent swap over RCCL) / config 4 (N >= 4:
-            AlphaStar roles, half main players, half main exploiters, historical snapshots): one league player
-            per GPU; every --match-len iterations a league iteration exchanges parameters (all_gather) and
-            payoff (all_reduce) over RCCL and picks the next opponent. Works at N = 1 too (the player faces
-            its own snapshots): the per-GPU cost of a league learner.
-N > 1: one process per GPU (torch.distributed.run); rollouts and learners never cross GPUs.
+Modes:
+  auto      (default) two legs in one run, both at every N:
+            * ``value`` = config 2 per GPU: one learner vs the scripted AI on every rank (N independent learners,
+              no data-path collective; weak scaling) -- the metric's "5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X";
+            * ``league`` = the league at the same N: config 3 at N = 2 (two PFSP self-play learners, opponent swap
+              over RCCL), config 4 at N >= 4 (AlphaStar roles: half main players, half main exploiters, historical
+              snapshots), at N = 1 one league player facing its own snapshots (the per-GPU cost of a league
+              learner, the denominator of the league's scaling). The league exchange (payoff all_reduce,
+              parameter all_gather, barrier, matchmaking) runs every --match-len iterations INSIDE the timed
+              region; its wall time is reported (exchange_ms_*).
+  ai        config 2 only
+  league    the league leg only (as ``value``)
+  refil     config 5: REFIL (entity-attention agent, imagined groups, FlexQMixer), 3-8 agents per env padded to
+            8, 4096 envs per GPU vs the scripted AI (entity env variant); N > 1 = replicas
+N > 1: one process per GPU (torch.distributed.run, RCCL); rollouts and learners never cross GPUs. Under
+torch.distributed.run with one process the league's collectives still run (RCCL at world size 1).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -34,6 +40,8 @@ import torch  # noqa: E402
 
 FP32_MFMA_PEAK = 157.3e12  # MI355X dense fp32 (MFMA == VALU rate), MI355X_MICROARCH.md chip table
 HBM_PEAK = 8.0e12
+METRIC = "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X"
+COUNTERS_JSON = os.path.join(ROOT, "profiles", "counters.json")
 
 
 def agent_flops_per_forward(N, d_in, H, A):
@@ -50,45 +58,112 @@ def refil_flops_per_forward(NA, NE, D0, E, H, A, heads=4):
             + 2 * NA * H * A)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", default="auto", choices=["auto", "ai", "league", "refil"])
-    ap.add_argument("--match-len", type=int, default=5, help="league: training iterations per league iteration")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
-    ap.add_argument("--device", type=int, default=None, help="GPU index for every rank (rehearsal on one GPU)")
-    ap.add_argument("--envs", type=int, default=4096)
-    ap.add_argument("--episode-limit", type=int, default=100)
-    ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per rollout launch (scripts/gpu_traffic.sh -> profiles/)")
-    a = ap.parse_args()
+# ---- distributed plumbing ----------------------------------------------------------------------------------
+class Ctx:
+    """Where this rank runs: torch.distributed (or not), its device, where reductions stage their tensors."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.device is not None:
-        local_rank = a.device
-    mode = a.mode if a.mode != "auto" else "ai"
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-        else:
-            dist.init_process_group(a.backend)
-    dev = torch.device(f"cuda:{local_rank}")
-    torch.cuda.set_device(dev)
+    def __init__(self, dist, dev):
+        self.dist, self.dev = dist, dev
+        self.world = dist.get_world_size() if dist else 1
+        self.rank = dist.get_rank() if dist else 0
+        self.rdev = dev if (dist and dist.get_backend() == "nccl") else torch.device("cpu")
 
-    from maleague.custom_logging import MainLogger
-    from maleague.runs import MultiAgentExperiment
+    def sync(self):
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def reduce(self, x: float, op: str) -> float:
+        if not self.dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.rdev)
+        self.dist.all_reduce(t, op={"max": self.dist.ReduceOp.MAX, "sum": self.dist.ReduceOp.SUM}[op])
+        return float(t.item())
+
+    def gather(self, x: float) -> list:
+        if not self.dist:
+            return [x]
+        t = torch.tensor([x], dtype=torch.float64, device=self.rdev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [float(o.item()) for o in out]
+
+
+def timed_loop(ctx: Ctx, iteration, stepper, steps: int, warmup: int) -> dict:
+    """W untimed iterations, then exactly K timed ones bracketed by barrier + device sync on both sides.
+    Rollout launches inside the timed region are timed with HIP events on their own stream (stepper.timing)."""
+    for i in range(warmup):
+        iteration(i)
+    ctx.sync()
+    ctx.barrier()
+    timing_ok = ctx.dev.type == "cuda"
+    stepper.timing = [] if timing_ok else None
+    t0_env = stepper.t_env
+    rows0 = int(stepper.agent_rows.item())
+    ctx.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        iteration(i)
+    ctx.sync()
+    ctx.barrier()
+    elapsed_local = time.perf_counter() - t0
+    local_steps = stepper.t_env - t0_env
+    rows = (int(stepper.agent_rows.item()) - rows0) / steps
+    ev_ms = [st.elapsed_time(en) for st, en in stepper.timing] if timing_ok else []
+    stepper.timing = None
+    elapsed = ctx.reduce(elapsed_local, "max")
+    per_rank = ctx.gather(local_steps / elapsed_local)
+    total = int(ctx.reduce(float(local_steps), "sum"))
+    return {"elapsed": elapsed, "env_steps": total, "local_env_steps": local_steps, "per_rank": per_rank,
+            "value": total / elapsed, "ms_per_step": elapsed / steps * 1e3, "rows_per_launch": rows,
+            "avg_kernel_ms": (sum(ev_ms) / len(ev_ms)) if ev_ms else None}
+
+
+def league_iteration(inst, match_len: int, exchange_s: list):
+    """One training iteration of a league player; every ``match_len`` iterations a league iteration first
+    (LeagueInstance.sync: payoff all_reduce, parameter / checkpoint all_gather, barrier, matchmaking --
+    matchmaking_league_instance.py:36-68), its wall time appended to ``exchange_s``."""
+
+    def it(i):
+        if i % match_len == 0:
+            t0 = time.perf_counter()
+            inst.sync()
+            exchange_s.append(time.perf_counter() - t0)
+        inst.play(1)
+
+    return it
+
+
+def run_league_leg(ctx: Ctx, inst, steps: int, warmup: int, match_len: int) -> dict:
+    """The league leg of the bench (also driven by tests/test_bench_league.py over gloo on CPU)."""
+    ex_warm, ex = [], []
+    warm_it = league_iteration(inst, match_len, ex_warm)
+    timed_it = league_iteration(inst, match_len, ex)
+    n = [0]
+
+    def it(i):
+        (warm_it if n[0] < warmup else timed_it)(i)
+        n[0] += 1
+
+    r = timed_loop(ctx, it, inst.experiment.stepper, steps, warmup)
+    ex_ms = [e * 1e3 for e in ex]
+    lg = inst.league
+    r.update({"league_iterations": len(ex), "exchange_ms_mean": sum(ex_ms) / max(1, len(ex_ms)),
+              "exchange_ms_max": max(ex_ms) if ex_ms else None,
+              "exchange_frac": sum(ex) / r["elapsed"] if r["elapsed"] > 0 else None,
+              "collective_backend": lg.backend, "world_size": ctx.world,
+              "opponents_rank0": [h[1] for h in inst.history], "historical_snapshots": len(lg.historical_meta),
+              "evictions": lg.evictions,
+              "payoff_games": float(lg.payoff.tensor[..., 0].sum().item())})
+    return r
+
+
+# ---- experiments ---------------------------------------------------------------------------------------------
+def make_args(mode, a, rank, local_rank):
     from maleague.utils.config import build_config, to_args
-
     plan = a.plan or ("refil_8" if mode == "refil" else "medium_1h_4t")
     overrides = [f"batch_size_run={a.envs}", "runner=parallel", "buffer_cpu_only=False",
                  f"env_args.match_build_plan={plan}", f"env_args.episode_limit={a.episode_limit}",
@@ -102,148 +177,217 @@ def main():
     import numpy as np
     np.random.seed(rank)  # replay sampling (reproducible learning curve -> reproducible episode lengths)
     torch.manual_seed(rank)
-    args = to_args(cfg)
-    inst = None
-    if mode in ("ai", "refil"):
-        exp = MultiAgentExperiment(args, MainLogger(log_interval=10 ** 12))
-        exp._init_stepper()
-        if mode == "refil":
-            ea = args.env_args
-            workload = (f"refil_{plan}_{ea.get('min_agents', 3)}to{ea.get('max_agents', 8)}agents_{a.envs}envs_"
-                        f"ep{a.episode_limit}")
-            parallelism = f"replicas{world}"
-        else:
-            workload = f"qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
-            parallelism = f"replicas{world}"
-    else:
-        from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
-        lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=8 * world)
-        if world >= 4:
-            roles = league_roles_for(world, args)
-            inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="rolebased", role=roles, seed=0)
-            n_main = roles.count("main")
-            workload = f"pfsp_league_{n_main}main_{world - n_main}exploiter_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
-        else:
-            inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="matchmaking", seed=0)
-            workload = f"selfplay_pfsp_{world}learners_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
-        exp = inst.experiment
-        parallelism = f"league{world}_rccl"
-    stepper = exp.stepper
-    B = stepper.batch_size
-    # steady-state exploration (epsilon floor 0.05), as SURVEY §8d prescribes for timing runs
-    stepper.t_env = 10 ** 6
-    episode = 0
+    return to_args(cfg), plan
 
-    def iteration(i):
-        nonlocal episode
-        if inst is None:
-            exp._train_episode(episode)
-            episode += B
-        else:
-            if i % a.match_len == 0:
-                inst.sync()  # league iteration: payoff all_reduce + parameter all_gather over RCCL, next match
-            inst.play(1)
 
-    for i in range(a.warmup):
-        iteration(i)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    # rollout-kernel timing with HIP events on the stream the kernel is launched on
-    stepper.timing = []
-    t0_env = stepper.t_env
-    rows0 = int(stepper.agent_rows.item())
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        iteration(i)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    env_steps = stepper.t_env - t0_env
-    local_env_steps = env_steps
-    rows_per_launch = (int(stepper.agent_rows.item()) - rows0) / a.steps
-    if dist:
-        rdev = dev if a.backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        s = torch.tensor([env_steps], dtype=torch.float64, device=rdev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        env_steps = int(s.item())
-    ev_ms = [st.elapsed_time(en) for st, en in stepper.timing]
-    stepper.timing = None
-    value = env_steps / elapsed
+def league_workload(world, plan, a, roles=None):
+    if world >= 4:
+        n_main = roles.count("main")
+        return (f"pfsp_league_{n_main}main_{world - n_main}exploiter_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
+                "BASELINE config 4 (PFSP league: main players + main exploiters, historical snapshots, RCCL)")
+    if world > 1:
+        return (f"selfplay_pfsp_{world}learners_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
+                f"BASELINE config 3 (self-play QMIX, {world} PFSP learners, opponent swap via RCCL)")
+    return (f"league_player_vs_own_snapshots_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
+            "1-GPU league player (self-play vs its own snapshots): the per-GPU league cost, scaling denominator")
 
-    # roofline of the dominant kernel (the rollout): fp32 MFMA-bound agent cell
+
+def kernel_names(mode, N, A, kc1=0):
+    v7 = "rollout_v2_kernel<64, true, 5, 10>" if (N, A) == (5, 15) else (
+        "rollout_v2_kernel<64, true, 3, 6>" if (N, A) == (3, 11) else "rollout_v2_kernel<64, true>")
+    sp7 = "rollout_sp7_kernel<10, 10>" if (N, A) == (5, 15) else (
+        "rollout_sp7_kernel<6, 6>" if (N, A) == (3, 11) else "rollout_sp7_kernel<0, 0>")
+    return {"ai": v7, "league": sp7, "refil": f"refil_rollout_kernel<{kc1}>"}[mode]
+
+
+def load_counters(kernel):
+    """Committed rocprofv3 counter results for ``kernel`` (scripts/gpu_counters.sh -> profiles/counters.json):
+    HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction), MFMA-busy fraction
+    (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)), wave-parked fraction, profiled commit."""
+    if not os.path.exists(COUNTERS_JSON):
+        return {}
+    with open(COUNTERS_JSON) as f:
+        return json.load(f).get("kernels", {}).get(kernel, {})
+
+
+def roofline(mode, stepper, r, steps, B):
     info = stepper.get_env_info()
     sides = 2 if mode == "league" else 1
     N, A = info["n_agents"] // sides, info["n_actions"]
+    kc1 = (info.get("entity_shape", 0) + A + 15) // 16 if mode == "refil" else 0
     if mode == "refil":
         fl = refil_flops_per_forward(N, info["n_entities"], info["entity_shape"] + A, 64, 64, A)
     else:
-        d_in = info["obs_shape"] + A + N
-        fl = sides * agent_flops_per_forward(N, d_in, 64, A)
+        fl = sides * agent_flops_per_forward(N, info["obs_shape"] + A + N, 64, A)
     # agent forwards per launch: every env steps len times and records one final action (len + 1 forwards)
-    forwards = (local_env_steps + a.steps * B) / a.steps
-    avg_kernel_s = sum(ev_ms) / len(ev_ms) / 1e3
-    achieved = fl * forwards / avg_kernel_s
-    issued = fl / (sides * N) * rows_per_launch / avg_kernel_s if mode == "ai" else None
-    traffic = None
-    kc1 = (info.get("entity_shape", 0) + A + 15) // 16 if mode == "refil" else 0
-    # the default rollout kernel: v7 (split-bf16 GRU), compile-time shape for the 5v5 / 3v3 plans
-    v7 = "rollout_v2_kernel<64, true, 5, 10>" if (N, info["n_actions"]) == (5, 15) else (
-        "rollout_v2_kernel<64, true, 3, 6>" if (N, info["n_actions"]) == (3, 11) else "rollout_v2_kernel<64, true>")
-    sp7 = "rollout_sp7_kernel<10, 10>" if (N, info["n_actions"]) == (5, 15) else (
-        "rollout_sp7_kernel<6, 6>" if (N, info["n_actions"]) == (3, 11) else "rollout_sp7_kernel<0, 0>")
-    kernel = {"ai": v7, "league": sp7,  # the bench runs H = 64 (rnn_hidden_dim below)
-              "refil": f"refil_rollout_kernel<{kc1}>"}[mode]
-    if a.traffic_json and os.path.exists(a.traffic_json):
-        with open(a.traffic_json) as f:
-            traffic = json.load(f).get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    forwards = (r["local_env_steps"] + steps * B) / steps
+    avg_s = r["avg_kernel_ms"] / 1e3
+    achieved = fl * forwards / avg_s
+    kernel = kernel_names(mode, N, A, kc1)
+    cnt = load_counters(kernel)
+    traffic = cnt.get("hbm_bytes_per_launch")
+    out = {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+           "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic, "kernel": kernel,
+           "avg_kernel_ms": r["avg_kernel_ms"], "flops_per_launch": fl * forwards,
+           "hbm_gbps": traffic / avg_s / 1e9 if traffic else None,
+           "hbm_frac": traffic / avg_s / HBM_PEAK if traffic else None,
+           "mfma_busy": cnt.get("mfma_busy"), "wave_parked": cnt.get("wait_any_frac"),
+           "counters_commit": cnt.get("commit")}
+    if mode == "ai":
+        issued = fl / N * r["rows_per_launch"] / avg_s
+        out.update({"issued_tflops": issued / 1e12, "issued_frac": issued / FP32_MFMA_PEAK,
+                    "issued_rows_per_launch": r["rows_per_launch"]})
+        if kernel.startswith("rollout_v2_kernel<64, true"):
+            out["note"] = ("fp32 algorithmic FLOPs vs the fp32 MFMA peak; the GRU products run as split-bf16 fp32 "
+                           "emulation (6 bf16 MFMA partial products each, DESIGN.md §4a)")
+    return out
 
-    cpu = None
-    if rank == 0 and world == 1 and mode in ("ai", "refil") and not a.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import cpu_baseline
-        threads = min(16, os.cpu_count() or 1)
-        if mode == "refil":
-            r = cpu_baseline.run_refil(seconds=a.cpu_seconds, B=32, episode_limit=a.episode_limit, threads=threads)
-            what = "C entity env + PyTorch-CPU EntityAttentionRNNAgent / REFILLearner (refil_ref)"
+
+def cpu_baselines(mode, a):
+    """The CPU legs on the host cores, in a child process that never touches the GPU (it also forks the
+    process-model leg's env workers): oracle/cpu_baseline.py."""
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--json", "--seconds",
+           str(a.cpu_seconds), "--episode-limit", str(a.episode_limit), "--legs",
+           "refil" if mode == "refil" else "vector,process"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=max(300, 8 * a.cpu_seconds))
+    if p.returncode != 0:
+        return {"error": p.stderr[-400:]}
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", default="auto", choices=["auto", "ai", "league", "refil"])
+    ap.add_argument("--match-len", type=int, default=5, help="league: training iterations per league iteration")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
+    ap.add_argument("--device", type=int, default=None, help="GPU index for every rank (rehearsal on one GPU)")
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--episode-limit", type=int, default=100)
+    ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+    # stdout carries exactly one line, the JSON result: native libraries (RCCL prints a version banner on its first
+    # communicator) write to fd 1, so fd 1 is pointed at stderr and the result goes to a saved copy of stdout
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
+    launched = "WORLD_SIZE" in os.environ  # torch.distributed.run (any nproc) -> a process group, RCCL
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = a.device if a.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if launched:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
         else:
-            r = cpu_baseline.run(seconds=a.cpu_seconds, B=64, episode_limit=a.episode_limit, threads=threads)
-            what = "oracle stepper + C env + PyTorch-CPU DRQN/QMIX learner"
-        cpu = {"value": r["value"], "unit": "env-steps/s", "cores": r["cores"], "kind": "port",
-               "sample": f"{r['runs']} runs x {r['B']} envs (+1 train each), {r['env_steps']} env steps in "
-                         f"{r['seconds']:.1f}s; {what}"}
+            dist.init_process_group(a.backend)
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+    ctx = Ctx(dist, dev)
+
+    from maleague.custom_logging import MainLogger
+    from maleague.runs import MultiAgentExperiment
+
+    legs = {"auto": ["ai", "league"], "ai": ["ai"], "league": ["league"], "refil": ["refil"]}[a.mode]
+    results = {}
+    for leg in legs:
+        args, plan = make_args(leg, a, rank, local_rank)
+        inst = None
+        if leg in ("ai", "refil"):
+            exp = MultiAgentExperiment(args, MainLogger(log_interval=10 ** 12))
+            exp._init_stepper()
+            if leg == "refil":
+                ea = args.env_args
+                workload = (f"refil_{plan}_{ea.get('min_agents', 3)}to{ea.get('max_agents', 8)}agents_{a.envs}envs_"
+                            f"ep{a.episode_limit}")
+                cfg_name = "BASELINE config 5 (REFIL, 3-8 agents per env, 4096 envs per GPU)"
+            else:
+                workload = f"qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}"
+                cfg_name = "BASELINE config 2 (QMIX 5v5, 4096 envs per GPU, one learner per GPU vs scripted AI)"
+            parallelism = f"replicas{world}"
+        else:
+            from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
+            lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=4 * world)
+            roles = league_roles_for(world, args) if world >= 4 else None
+            if roles:
+                inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="rolebased", role=roles, seed=0)
+            else:
+                inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="matchmaking", seed=0)
+            workload, cfg_name = league_workload(world, plan, a, roles)
+            exp = inst.experiment
+            parallelism = f"league{world}_{lg.backend}"
+        stepper = exp.stepper
+        B = stepper.batch_size
+        stepper.t_env = 10 ** 6  # steady-state exploration (epsilon floor 0.05), SURVEY §8d
+        if inst is None:
+            ep = [0]
+
+            def iteration(i, exp=exp, B=B, ep=ep):
+                exp._train_episode(ep[0])
+                ep[0] += B
+
+            r = timed_loop(ctx, iteration, stepper, a.steps, a.warmup)
+        else:
+            r = run_league_leg(ctx, inst, a.steps, a.warmup, a.match_len)
+        r["roofline"] = roofline(leg, stepper, r, a.steps, B)
+        r.update({"workload": workload, "represents": cfg_name, "parallelism": parallelism, "envs_per_gpu": B,
+                  "mean_episode_len": r["env_steps"] / max(1, a.steps * B * world)})
+        results[leg] = r
+        del exp, inst, stepper
+        torch.cuda.empty_cache()
+
+    head = legs[0]
+    h = results[head]
+    cpu = None
+    if rank == 0 and world == 1 and head in ("ai", "refil") and not a.no_cpu_baseline:
+        c = cpu_baselines(head, a)
+        if "error" in c:
+            cpu = {"value": None, "unit": "env-steps/s", "error": c["error"]}
+        else:
+            main_leg = c["legs"][0]
+            cpu = {"value": main_leg["value"], "unit": "env-steps/s", "cores": main_leg["cores"], "kind": "port",
+                   "sample": main_leg["sample"], "cpu_model": c.get("cpu_model"), "host_cpus": c.get("host_cpus"),
+                   "legs": c["legs"]}
     if rank == 0:
-        out = {"metric": "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X",
-               "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-               "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        out = {"metric": METRIC, "value": h["value"], "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
+               "warmup": a.warmup, "ms_per_step": h["ms_per_step"], "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "f32",
                "data": ("synthetic (entity battles, 3-8 agents per env padded to 8, random-init REFIL)"
-                        if mode == "refil" else "synthetic (spec-v1 5v5 battles, random-init QMIX)"),
-               "config": {"workload": workload, "mode": mode, "envs_per_gpu": B, "episode_limit": a.episode_limit,
-                          "learner_batch": 32, "rnn_hidden_dim": 64, "buffer_size": 5000,
-                          "parallelism": parallelism, **({"match_len": a.match_len} if inst else {})},
-               "env_steps": env_steps, "mean_episode_len": env_steps / max(1, a.steps * B * world),
-               "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12,
-                            "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic,
-                            "kernel": kernel, "avg_kernel_ms": avg_kernel_s * 1e3,
-                            "flops_per_launch": fl * forwards},
-               "cpu_baseline": cpu}
-        if issued is not None:
-            out["roofline"].update({"issued_tflops": issued / 1e12, "issued_frac": issued / FP32_MFMA_PEAK,
-                                    "issued_rows_per_launch": rows_per_launch})
-        if mode == "ai" and kernel.startswith("rollout_v2_kernel<64, true"):
-            out["roofline"]["note"] = ("fp32 algorithmic FLOPs vs the fp32 MFMA peak; the GRU products run as "
-                                       "split-bf16 fp32 emulation (6 bf16 MFMA partial products each, DESIGN.md §4a)")
-        if inst is not None:
-            out["league"] = {"opponents_rank0": [h[1] for h in inst.history],
-                             "historical_snapshots": len(inst.league.historical_meta)}
-        print(json.dumps(out))
+                        if head == "refil" else "synthetic (spec-v1 5v5 battles, random-init QMIX)"),
+               "config": {"workload": h["workload"], "represents": h["represents"], "mode": a.mode,
+                          "envs_per_gpu": h["envs_per_gpu"], "episode_limit": a.episode_limit, "learner_batch": 32,
+                          "rnn_hidden_dim": 64, "buffer_size": 5000, "parallelism": h["parallelism"],
+                          **({"match_len": a.match_len} if head == "league" else {})},
+               "env_steps": h["env_steps"], "mean_episode_len": h["mean_episode_len"],
+               "per_rank_value": h["per_rank"], "roofline": h["roofline"], "cpu_baseline": cpu}
+        if head == "league":
+            out["league"] = {k: h[k] for k in ("league_iterations", "exchange_ms_mean", "exchange_ms_max",
+                                               "exchange_frac", "collective_backend", "world_size",
+                                               "opponents_rank0", "historical_snapshots", "evictions")}
+        if "league" in results and head != "league":
+            L = results["league"]
+            out["league"] = {"value": L["value"], "unit": "env-steps/s", "ms_per_step": L["ms_per_step"],
+                             "represents": L["represents"], "workload": L["workload"],
+                             "parallelism": L["parallelism"], "per_rank_value": L["per_rank"],
+                             "env_steps": L["env_steps"], "mean_episode_len": L["mean_episode_len"],
+                             "match_len": a.match_len,
+                             **{k: L[k] for k in ("league_iterations", "exchange_ms_mean", "exchange_ms_max",
+                                                  "exchange_frac", "collective_backend", "world_size",
+                                                  "opponents_rank0", "historical_snapshots", "evictions",
+                                                  "payoff_games")},
+                             "rollout_kernel": L["roofline"]["kernel"], "avg_kernel_ms": L["avg_kernel_ms"],
+                             "roofline_frac": L["roofline"]["frac"],
+                             "note": "league scaling = league.value at N / league.value at N = 1 (same leg, "
+                                     "same per-GPU workload: weak scaling)"}
+        sys.stdout.flush()
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 

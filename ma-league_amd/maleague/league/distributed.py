@@ -10,6 +10,13 @@ league iteration:
 They run once per league iteration (play_time_mins), never on the per-step data path. The payoff table and
 the agent pool (current parameters of every player + historical snapshots) are replicated on every rank, so
 matchmaking is local and needs no coordinator process.
+
+The collectives run whenever a process group exists, world size 1 included (``torchrun --nproc-per-node 1``
+exercises the RCCL branch on one GPU); without one (plain ``python``) the pool degenerates to local copies.
+The historical pool has a fixed capacity (its slots are payoff rows / columns); when it is full the oldest
+snapshot of the parent holding the most snapshots is evicted -- its slot, payoff row and column reused by the
+new snapshot -- identically on every rank (the reference appends HistoricalPlayers without bound,
+players.py:32-60, agent_pool_instance.py:94-103).
 """
 from __future__ import annotations
 
@@ -28,8 +35,9 @@ log = logging.getLogger(__name__)
 class DistributedLeague:
     def __init__(self, n_players: int, device, reference_compat: bool = False, seed: int = 0,
                  max_historical: int = 0):
-        self.rank = dist.get_rank() if dist.is_initialized() else 0
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self._dist = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank() if self._dist else 0
+        self.world = dist.get_world_size() if self._dist else 1
         self.n = n_players
         self.capacity = n_players + max_historical  # payoff rows/cols: players, then historical snapshots
         self.device = torch.device(device)
@@ -39,8 +47,8 @@ class DistributedLeague:
         # agent pool (replicated): current parameters of every player, historical snapshots
         self.current = None            # [n_players, n_params]
         self.historical = None         # [max_historical, n_params]
-        self.historical_meta: List[tuple] = []  # (pid, parent pid, trained_steps)
-        self.pool_full_skips = 0  # checkpoint requests dropped because the historical pool was full
+        self.historical_meta: List[tuple] = []  # (pid, parent pid, trained_steps), oldest first
+        self.evictions = 0  # snapshots evicted to make room for newer ones (pool full)
 
     def player(self) -> int:
         return self.rank % self.n
@@ -70,8 +78,12 @@ class DistributedLeague:
         """gloo (CPU tests, single-GPU rehearsals) reduces host tensors; RCCL reduces device tensors in place."""
         return self.device.type == "cuda" and dist.get_backend() == "gloo"
 
+    @property
+    def backend(self) -> str:
+        return dist.get_backend() if self._dist else "local"
+
     def sync_payoff(self):
-        if self.world > 1:
+        if self._dist:
             if self._host_staged():
                 d = self._delta.cpu()
                 dist.all_reduce(d, op=dist.ReduceOp.SUM)
@@ -86,7 +98,7 @@ class DistributedLeague:
     def share_params(self, flat: torch.Tensor):
         """Every rank's flat parameter vector (index = rank)."""
         flat = flat.detach().contiguous()
-        if self.world == 1:
+        if not self._dist:
             return [flat.clone()]
         if self._host_staged():
             host = flat.cpu()
@@ -98,41 +110,61 @@ class DistributedLeague:
         return out
 
     def exchange(self, flat: torch.Tensor, trained_steps: int, checkpoint: bool):
-        """all_gather [params | trained_steps | checkpoint flag] of every player; refresh the replicated pool and
-        append a historical snapshot for every player that asked for a checkpoint (in player order, so every
-        rank assigns the same historical pids). trained_steps travels as two float32 halves (steps mod 2^24 and
-        steps >> 24), exact up to 2^48 (the reference's checkpoint thresholds are 2e9 / 4e9 steps). Returns the
-        list of new (historical pid, parent pid); a player whose request found the pool full is not in it (and
-        a warning is logged), so the caller resets its checkpoint clock only for snapshots actually taken."""
+        """all_gather [params | trained_steps | checkpoint flag | range flag] of every player; refresh the
+        replicated pool and append a historical snapshot for every player that asked for a checkpoint (in player
+        order, so every rank assigns the same historical pids). trained_steps travels as two float32 halves (steps
+        mod 2^24 and steps >> 24), exact up to 2^48 (the reference's checkpoint thresholds are 2e9 / 4e9 steps); a
+        value outside that range is flagged in the message and every rank raises after the gather (a rank raising
+        before it would leave the others blocked in the collective). When the pool is full the oldest snapshot of
+        the parent with the most snapshots is evicted (``_evict``). Returns the list of new (historical pid,
+        parent pid)."""
         n_p = flat.numel()
         steps = int(trained_steps)
-        if not 0 <= steps < 2 ** 48:
-            raise ValueError(f"trained_steps {steps} outside the exchange's exact range [0, 2^48)")
-        meta_in = [float(steps & 0xFFFFFF), float(steps >> 24), 1.0 if checkpoint else 0.0]
+        bad = not 0 <= steps < 2 ** 48
+        s = min(max(steps, 0), 2 ** 48 - 1)
+        meta_in = [float(s & 0xFFFFFF), float(s >> 24), 1.0 if checkpoint else 0.0, 1.0 if bad else 0.0]
         msg = torch.cat([flat.detach().reshape(-1).to(torch.float32), torch.tensor(meta_in, device=flat.device)])
         gathered = self.share_params(msg)
         allm = torch.stack(gathered)[: self.n]
+        meta = allm[:, n_p:].detach().cpu().numpy().astype(np.int64)
+        if meta[:, 3].any():
+            raise ValueError(f"trained_steps outside the exchange's exact range [0, 2^48) on player(s) "
+                             f"{np.nonzero(meta[:, 3])[0].tolist()} (this player: {steps})")
         if self.current is None:
             self.current = torch.empty(self.n, n_p, dtype=torch.float32, device=flat.device)
             cap = self.capacity - self.n
             self.historical = torch.empty(max(cap, 0), n_p, dtype=torch.float32, device=flat.device)
         self.current.copy_(allm[:, :n_p])
-        meta = allm[:, n_p:].detach().cpu().numpy().astype(np.int64)
         new = []
         for pid in range(self.n):
             if meta[pid, 2] > 0:
-                k = len(self.historical_meta)
-                if self.n + k >= self.capacity:
-                    self.pool_full_skips += 1
-                    if self.pool_full_skips == 1 or self.pool_full_skips % 100 == 0:
-                        log.warning("league: historical pool full (%d snapshots): checkpoint of player %d skipped "
-                                    "(%d skips so far; raise max_historical)", k, pid, self.pool_full_skips)
-                    continue
-                self.historical[k].copy_(self.current[pid])
-                hp = self.n + k
+                if self.historical.shape[0] == 0:
+                    continue  # no historical capacity at all (max_historical = 0)
+                if len(self.historical_meta) < self.historical.shape[0]:
+                    hp = self.n + len(self.historical_meta)
+                else:
+                    hp = self._evict()
+                self.historical[hp - self.n].copy_(self.current[pid])
                 self.historical_meta.append((hp, pid, int(meta[pid, 0] + (meta[pid, 1] << 24))))
                 new.append((hp, pid))
         return new
+
+    def _evict(self) -> int:
+        """Free a historical slot: the oldest snapshot of the parent that holds the most snapshots (ties: the
+        parent whose oldest snapshot is older). Its payoff row and column are zeroed so the new snapshot starts
+        with no games. Deterministic in the replicated state, hence identical on every rank."""
+        counts = {}
+        for _, parent, _ in self.historical_meta:
+            counts[parent] = counts.get(parent, 0) + 1
+        most = max(counts.values())
+        idx = next(i for i, (_, parent, _) in enumerate(self.historical_meta) if counts[parent] == most)
+        hp = self.historical_meta.pop(idx)[0]
+        for t in (self.payoff.tensor, self._delta):
+            t[hp, :, :] = 0
+            t[:, hp, :] = 0
+        self.evictions += 1
+        log.info("league: historical pool full (%d snapshots): evicted snapshot %d", len(self.historical_meta) + 1, hp)
+        return hp
 
     def params_of(self, pid: int) -> torch.Tensor:
         if pid < self.n:
@@ -147,5 +179,5 @@ class DistributedLeague:
         return self.sampling.sample(opponents, prio_measure=wr, weighting=weighting)
 
     def barrier(self):
-        if self.world > 1:
+        if self._dist:
             dist.barrier()

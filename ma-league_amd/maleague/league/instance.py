@@ -90,7 +90,7 @@ class LeagueInstance:
         ckpt = self.me.ready_to_checkpoint(self.view()) if self.mode == "rolebased" else False
         taken = self.league.exchange(agent_vector(home), steps, ckpt)
         if ckpt and any(parent == self.pid for _, parent in taken):
-            self.me.checkpoint()  # only when the snapshot exists (pool not full): otherwise it asks again
+            self.me.checkpoint()  # only when the snapshot exists (max_historical > 0): otherwise it asks again
         self.league.barrier()
         view = self.view()
         if self.matchmaker is not None:
@@ -107,7 +107,7 @@ class LeagueInstance:
         return self.opponent, hist
 
     def _any(self, flag: bool) -> bool:
-        if self.league.world == 1:
+        if not self.league._dist:
             return bool(flag)
         t = torch.tensor([1.0 if flag else 0.0],
                          device="cpu" if dist.get_backend() == "gloo" else self.league.device)

@@ -5,10 +5,22 @@ synthetic env in C (env_ref.c via ctypes, one call per env per step like EnvWork
 forward batched over all B*N rows per step in PyTorch-CPU (basic_controller.py:38-50), epsilon-greedy,
 and one QLearner.train (learner_ref.QLearnerRef, PyTorch-CPU autograd + RMSprop) on 32 sampled episodes
 per run -- the loop shape of ma_experiment.py:224-241. Runs for a bounded wall-clock sample.
+
+Legs (bench.py runs this file as a child process that never touches the GPU, ``--json``):
+  vector   run():               one process, the B envs stepped in a loop, the agent batched over B*N rows
+  process  run_process_model(): the reference's process model (parallel_stepper.py:32-39,
+           env_worker_process.py:27-71): B = host cores env-worker processes, one env each, a
+           ("step", actions) / result-dict round trip per env per step over a pipe, the parent batching the
+           agent forward over the B*N rows and training once per run
+  refil    run_refil():         config 5 on the host
 """
 from __future__ import annotations
 
+import json
+import multiprocessing as mp
 import os
+import platform
+import sys
 import time
 from types import SimpleNamespace
 
@@ -207,5 +219,167 @@ def run_refil(seconds=15.0, B=32, episode_limit=100, eps=0.05, threads=None, see
             "cores": threads, "B": B}
 
 
+def _env_worker(conn, env_kw):
+    """EnvWorker.run (env_worker_process.py:27-71): a command loop over one env."""
+    e = envref.RefEnv(**env_kw)
+    while True:
+        cmd, data = conn.recv()
+        if cmd == "step":
+            rew, done, info = e.step(data)
+            conn.send((rew, done, info, e.state(), e.avail(), e.obs()))
+        elif cmd == "reset":
+            e.reset()
+            conn.send((e.state(), e.avail(), e.obs()))
+        elif cmd == "close":
+            conn.close()
+            return
+        else:
+            raise NotImplementedError(cmd)
+
+
+def run_process_model(seconds=15.0, B=None, episode_limit=100, eps=0.05, threads=None, seed=0, batch_size=32,
+                      capacity=512):
+    """ParallelStepper.run in the reference's process model: B worker processes (one env each); per step the
+    parent sends ("step", actions) to every running env, then receives every result (parallel_stepper.py:143-191),
+    with the stepper bookkeeping of stepper_ref.run and one QLearner.train per run."""
+    B = B or min(16, os.cpu_count() or 1)
+    threads = threads or B
+    p = PLAN_MEDIUM_1H_4T
+    U, N = 10, 5
+    A, d_obs, S = 5 + U, 8 * U, 6 * U
+    d_in = d_obs + A + N
+    ctx = mp.get_context("fork")  # this process never touched a GPU; workers only run the C env
+    conns, procs = [], []
+    for b in range(B):
+        a, w = ctx.Pipe()
+        kw = dict(team=p["team"], role=p["role"], melee=p["melee"], scripted=p["scripted"],
+                  episode_limit=episode_limit, seed=seed, env_index=b)
+        pr = ctx.Process(target=_env_worker, args=(w, kw), daemon=True)
+        pr.start()
+        conns.append(a)
+        procs.append(pr)
+    torch.set_num_threads(threads)
+    agent, mix = _init_params(d_in, 64, A, N, S, seed=seed)
+    args = SimpleNamespace(n_agents=N, n_actions=A, mixer="qmix", mixing_embed_dim=32, hypernet_layers=2,
+                           double_q=True, gamma=0.99, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10,
+                           target_update_interval=200, obs_last_action=True, obs_agent_id=True)
+    learner = LR.QLearnerRef(agent, mix, args)
+    T1 = episode_limit + 1
+    eye = torch.eye(N).unsqueeze(0).expand(B, -1, -1).reshape(B * N, N)
+    buffer, rng = [], np.random.RandomState(seed)
+    env_steps, runs, trains = 0, 0, 0
+    t_start = time.perf_counter()
+    try:
+        while time.perf_counter() - t_start < seconds:
+            batch = SR.new_batch(B, T1, N, A, d_obs, S)
+            for c in conns:
+                c.send(("reset", None))
+            for i, c in enumerate(conns):
+                batch["state"][i, 0], batch["avail_actions"][i, 0], batch["obs"][i, 0] = c.recv()
+                batch["filled"][i, 0] = 1
+            h = torch.zeros(B * N, 64)
+            terminated = [False] * B
+            running = list(range(B))
+            t = 0
+            while True:
+                obs = torch.from_numpy(batch["obs"][:, t].reshape(B * N, d_obs))
+                last = torch.from_numpy(batch["actions_onehot"][:, t - 1].reshape(B * N, A)) if t > 0 \
+                    else torch.zeros(B * N, A)
+                with torch.no_grad():  # forward on all B rows, selection on the running ones (:132-134)
+                    q, h = LR.drqn_forward(learner.p, torch.cat([obs, last, eye], 1), h)
+                ids = list(running)
+                qv = q.view(B, N, A)[ids]
+                av = torch.from_numpy(batch["avail_actions"][ids, t])
+                acts = LR.greedy_select(qv, av).numpy()
+                coin = rng.rand(*acts.shape) < eps
+                for (k, n) in zip(*np.nonzero(coin)):
+                    acts[k, n] = rng.choice(np.nonzero(av[k, n].numpy())[0])
+                for k, i in enumerate(ids):
+                    batch["actions"][i, t, :, 0] = acts[k]
+                    batch["actions_onehot"][i, t, np.arange(N), acts[k]] = 1.0
+                sent = [i for k, i in enumerate(ids) if not terminated[i]]
+                for k, i in enumerate(ids):
+                    if not terminated[i]:
+                        conns[i].send(("step", acts[k]))
+                running = [i for i in range(B) if not terminated[i]]
+                if all(terminated):
+                    break
+                for i in sent:
+                    rew, done, info, st, avl, ob = conns[i].recv()
+                    env_steps += 1
+                    terminated[i] = done
+                    batch["reward"][i, t, 0] = rew[0]
+                    batch["terminated"][i, t, 0] = done
+                    batch["state"][i, t + 1], batch["avail_actions"][i, t + 1], batch["obs"][i, t + 1] = st, avl, ob
+                    batch["filled"][i, t + 1] = 1
+                t += 1
+            runs += 1
+            for b in range(B):
+                buffer.append({k: v[b] for k, v in batch.items()})
+            del buffer[:-capacity]
+            if len(buffer) >= batch_size:
+                idx = rng.choice(len(buffer), batch_size, replace=False)
+                smp = {k: torch.from_numpy(np.stack([buffer[i][k] for i in idx])) for k in buffer[0]}
+                T = int(smp["filled"].sum(1).max())
+                smp = {k: v[:, :T].clone() for k, v in smp.items()}
+                learner.train(smp, env_steps, runs * B)
+                trains += 1
+        elapsed = time.perf_counter() - t_start
+    finally:
+        for c in conns:
+            try:
+                c.send(("close", None))
+            except OSError:
+                pass
+        for pr in procs:
+            pr.join(timeout=5)
+            if pr.is_alive():
+                pr.terminate()
+    return {"value": env_steps / elapsed, "env_steps": env_steps, "seconds": elapsed, "runs": runs, "trains": trains,
+            "cores": threads, "B": B, "workers": B}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or None
+
+
+def main(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", action="store_true")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--episode-limit", type=int, default=100)
+    ap.add_argument("--legs", default="vector,process")
+    a = ap.parse_args(argv)
+    threads = min(16, os.cpu_count() or 1)
+    legs = []
+    for leg in a.legs.split(","):
+        if leg == "vector":
+            r = run(seconds=a.seconds, B=64, episode_limit=a.episode_limit, threads=threads)
+            what = "vectorised port: one process, oracle stepper + C env + PyTorch-CPU DRQN/QMIX learner"
+        elif leg == "process":
+            r = run_process_model(seconds=a.seconds, episode_limit=a.episode_limit)
+            what = (f"reference process model: {r['workers']} env-worker processes (one env each, pipe round trip "
+                    f"per env per step) + PyTorch-CPU DRQN/QMIX learner in the parent")
+        elif leg == "refil":
+            r = run_refil(seconds=a.seconds, B=32, episode_limit=a.episode_limit, threads=threads)
+            what = "C entity env + PyTorch-CPU EntityAttentionRNNAgent / REFILLearner (refil_ref)"
+        else:
+            raise SystemExit(f"unknown leg {leg}")
+        legs.append({"leg": leg, "value": r["value"], "cores": r["cores"], "B": r["B"],
+                     "sample": f"{r['runs']} runs x {r['B']} envs (+1 train each), {r['env_steps']} env steps in "
+                               f"{r['seconds']:.1f}s; {what}"})
+    out = {"legs": legs, "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
+    print(json.dumps(out) if a.json else out)
+
+
 if __name__ == "__main__":
-    print(run(seconds=10))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    main()

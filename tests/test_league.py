@@ -211,7 +211,7 @@ class _FakeExperiment:
             self.home_mac.agent.w.add_(1.0)
 
 
-def _league_worker(rank, world, port, mode, out):
+def _league_worker(rank, world, port, mode, out, max_hist=None, iters=6):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -220,23 +220,25 @@ def _league_worker(rank, world, port, mode, out):
     from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
     args = SimpleNamespace(matchmaking="pfsp", league_checkpoint_min_steps=300, league_checkpoint_max_steps=600,
                            env_args={})
-    lg = DistributedLeague(n_players=world, device="cpu", seed=0, max_historical=4 * world)
+    lg = DistributedLeague(n_players=world, device="cpu", seed=0,
+                           max_historical=4 * world if max_hist is None else max_hist)
     exp = _FakeExperiment(rank)
     roles = league_roles_for(world, args) if mode == "rolebased" else None
     inst = LeagueInstance(args, None, lg, mode=mode, role=roles, seed=0, experiment=exp)
-    hist = inst.run(league_iterations=6, iterations_per_match=2)
+    hist = inst.run(league_iterations=iters, iterations_per_match=2)
     out.put((rank, lg.payoff.tensor.numpy().tolist(), list(lg.historical_meta), hist,
-             [a.tolist() for a in exp.adversaries]))
+             [a.tolist() for a in exp.adversaries], lg.evictions))
     dist.destroy_process_group()
 
 
-def _run_league(world, mode):
+def _run_league(world, mode, max_hist=None, iters=6):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_league_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_league_worker, args=(r, world, port, mode, q, max_hist, iters))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=180) for _ in procs], key=lambda r: r[0])
@@ -250,7 +252,7 @@ def test_league_instances_gloo_world2_pfsp():
     """Config 3 shape: 2 learners, PFSP matchmaking; payoff and agent pool replicated identically."""
     res = _run_league(2, "matchmaking")
     pay0 = np.array(res[0][1])
-    for rank, pay, hmeta, hist, advs in res:
+    for rank, pay, hmeta, hist, advs, _ in res:
         np.testing.assert_array_equal(np.array(pay), pay0)
         assert len(hist) == 6
         for (_, opp, is_hist), adv in zip(hist, advs):
@@ -267,7 +269,7 @@ def test_league_instances_gloo_world4_alphastar():
     pay0, meta0 = np.array(res[0][1]), res[0][2]
     assert len(meta0) > 0, "checkpoints were taken"
     assert all(parent in range(4) for _, parent, _ in meta0)
-    for rank, pay, meta, hist, advs in res:
+    for rank, pay, meta, hist, advs, _ in res:
         np.testing.assert_array_equal(np.array(pay), pay0)
         assert meta == meta0
         for (_, opp, is_hist), adv in zip(hist, advs):
@@ -276,37 +278,72 @@ def test_league_instances_gloo_world4_alphastar():
                 assert opp in (0, 1) or any(h[0] == opp and h[1] in (0, 1) for h in meta0)
 
 
-def test_exchange_exact_steps_and_full_pool(caplog):
-    """trained_steps past 2^24 survive the exchange exactly (reference thresholds 2e9 / 4e9), and a
-    checkpoint request that finds the historical pool full is reported as not taken (and logged)."""
-    import logging
-    from maleague.league import DistributedLeague
-    lg = DistributedLeague(n_players=1, device="cpu", max_historical=1)
+def test_exchange_exact_steps_and_eviction():
+    """trained_steps past 2^24 survive the exchange exactly (reference thresholds 2e9 / 4e9). VERDICT r2
+    #5: a checkpoint that finds the historical pool full evicts the oldest snapshot (its payoff row / column
+    zeroed) instead of being dropped; ADVICE r2: an out-of-range trained_steps raises after the gather."""
+    from maleague.league import DistributedLeague, PayoffEntry
+    lg = DistributedLeague(n_players=1, device="cpu", max_historical=2)
     flat = torch.arange(5, dtype=torch.float32)
     steps = 4_000_000_007
     assert lg.exchange(flat, steps, True) == [(1, 0)]
     assert lg.historical_meta == [(1, 0, steps)]
-    with caplog.at_level(logging.WARNING, logger="maleague.league.distributed"):
-        assert lg.exchange(flat + 1, steps + 1, True) == []
-    assert lg.pool_full_skips == 1 and "pool full" in caplog.text
-    assert lg.historical_meta == [(1, 0, steps)] and torch.equal(lg.params_of(1), flat)
+    assert lg.exchange(flat + 1, steps + 1, True) == [(2, 0)]
+    lg.record(0, 1, PayoffEntry.WIN, 3)
+    lg.record(0, 2, PayoffEntry.LOSS, 2)
+    lg.sync_payoff()
+    assert lg.exchange(flat + 2, steps + 2, True) == [(1, 0)]  # slot of the oldest snapshot reused
+    assert lg.historical_meta == [(2, 0, steps + 1), (1, 0, steps + 2)] and lg.evictions == 1
+    assert torch.equal(lg.params_of(1), flat + 2) and torch.equal(lg.params_of(2), flat + 1)
+    pay = lg.payoff.tensor
+    assert float(pay[0, 1].abs().sum()) == 0.0 and float(pay[1, :].abs().sum()) == 0.0
+    assert float(pay[0, 2, PayoffEntry.LOSS]) == 2.0
     with pytest.raises(ValueError):
         lg.exchange(flat, 2 ** 48, False)
 
 
-def test_checkpoint_clock_kept_when_pool_full():
-    """LeagueInstance.sync resets the player's checkpoint clock only when its snapshot was actually stored."""
+def test_eviction_picks_parent_with_most_snapshots():
+    from maleague.league import DistributedLeague
+    lg = DistributedLeague(n_players=2, device="cpu", max_historical=3)
+    lg.rank = 0
+    flat = torch.zeros(4)
+    lg.historical_meta = [(2, 1, 10), (3, 0, 11), (4, 0, 12)]
+    lg.current = torch.zeros(2, 4)
+    lg.historical = torch.zeros(3, 4)
+    assert lg._evict() == 3  # parent 0 holds two snapshots: its oldest goes
+    assert lg.historical_meta == [(2, 1, 10), (4, 0, 12)]
+    del flat
+
+
+def test_league_eviction_gloo_world4_past_capacity():
+    """a world-4 AlphaStar league runs far past the historical capacity; every rank ends with the
+    same pool and payoff, the newest snapshots present."""
+    res = _run_league(4, "rolebased", max_hist=2, iters=12)
+    pay0, meta0 = np.array(res[0][1]), res[0][2]
+    assert len(meta0) == 2, meta0
+    for rank, pay, meta, hist, advs, _ in res:
+        np.testing.assert_array_equal(np.array(pay), pay0)
+        assert meta == meta0
+    evicted = res[0][5]
+    assert evicted > 0, "the pool never filled"
+    steps = [s for _, _, s in meta0]
+    assert steps == sorted(steps)  # oldest first
+
+
+def test_checkpoint_clock_reset_when_stored():
+    """LeagueInstance.sync resets the player's checkpoint clock when its snapshot was stored (always, now that
+    a full pool evicts) and not when there is no historical capacity at all."""
     from types import SimpleNamespace
     from maleague.league import DistributedLeague, LeagueInstance
     args = SimpleNamespace(matchmaking="pfsp", league_checkpoint_min_steps=100, league_checkpoint_max_steps=200,
                            env_args={})
-    lg = DistributedLeague(n_players=1, device="cpu", seed=0, max_historical=1)
-    exp = _FakeExperiment(0)
-    inst = LeagueInstance(args, None, lg, mode="rolebased", role=["main"], seed=0, experiment=exp)
-    calls = []
-    inst.me.ready_to_checkpoint = lambda view: True
-    inst.me.checkpoint = lambda: calls.append(len(lg.historical_meta))
-    inst.sync()
-    assert calls == [1]          # snapshot stored -> clock reset
-    inst.sync()
-    assert calls == [1] and lg.pool_full_skips == 1  # pool full -> no reset, the player asks again
+    for cap, expect in ((1, [1, 1]), (0, [])):
+        lg = DistributedLeague(n_players=1, device="cpu", seed=0, max_historical=cap)
+        exp = _FakeExperiment(0)
+        inst = LeagueInstance(args, None, lg, mode="rolebased", role=["main"], seed=0, experiment=exp)
+        calls = []
+        inst.me.ready_to_checkpoint = lambda view: True
+        inst.me.checkpoint = lambda: calls.append(len(lg.historical_meta))
+        inst.sync()
+        inst.sync()
+        assert calls == expect
