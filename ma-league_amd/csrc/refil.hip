@@ -12,6 +12,9 @@
 // half-wave per env) step the env with the unit state in LDS; the agent phase runs per env: entity inputs ->
 // fc1 (MFMA, 16 entity rows) -> in_trans -> attention (lane per head x query), then both envs' 2 x 8 agent rows
 // form one 16-row tile for out_trans -> fc2 -> GRUCell -> fc3 with the hidden state in VGPRs.
+#include <cstdlib>
+#include <cstring>
+
 #include "mlg_host.h"
 #include "refil_device.h"
 
@@ -929,6 +932,8 @@ __global__ void __launch_bounds__(64) refil_agent_step_kernel(RAgent L, const fl
     }
 }
 
+#include "refil_ro4.inc"
+
 }  // namespace
 
 extern "C" int mlg_refil_debug_set_stamps(void* ptr) {
@@ -998,6 +1003,25 @@ extern "C" int mlg_refil_rollout(const MlgEntityEnvSpec* spec, MlgEnvState* st, 
     while (p < sp.grid) p <<= 1;
     RoArgs a{sp.U, S, d->n_actions, d->entity_shape, S, spec->min_agents, spec->max_agents, bt.B, 1.0f / (float)p};
     const RAgent L = agent_layout(d);
+    // default: four envs per wave (refil_ro4.inc) for the entity width of the env variant (K1 = 32);
+    // MLG_REFIL_ROLLOUT=v1 selects the two-env kernel (A/B, parity tests run both)
+    const char* var = getenv("MLG_REFIL_ROLLOUT");
+    const bool v1 = (var && strcmp(var, "v1") == 0) || L.K1 != 32;
+    if (!v1) {
+        const size_t lds4 = sizeof(R4Shared);
+        static bool attr4 = false;
+        if (!attr4) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(refil_rollout4_kernel<2>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4);
+            if (e != hipSuccess) return mlg::fail("refil_rollout: LDS %zu B: %s", lds4, hipGetErrorString(e));
+            attr4 = true;
+        }
+        const int per_block4 = R4_ENVS * R4_WAVES;
+        hipLaunchKernelGGL(refil_rollout4_kernel<2>, dim3((unsigned)((bt.B + per_block4 - 1) / per_block4)),
+                           dim3(64 * R4_WAVES), lds4, (hipStream_t)stream, *spec, *st, L, packed, bt, *info, a,
+                           test_mode ? 0.f : epsilon, test_mode);
+        return mlg::check_launch("refil_rollout4");
+    }
     auto kern = L.K1 <= 16 ? refil_rollout_kernel<1> : (L.K1 <= 32 ? refil_rollout_kernel<2> : refil_rollout_kernel<3>);
     const size_t lds = sizeof(RoShared);
     static bool attr_set[3] = {false, false, false};

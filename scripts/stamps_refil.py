@@ -28,7 +28,8 @@ st = VecEnvState(spec, B, dev)
 run = torch.zeros(6 * B, dtype=torch.int32, device=dev)
 ri = _native.MlgRunInfo(run[0:B].data_ptr(), run[4 * B:5 * B].data_ptr(), run[B:3 * B].data_ptr(),
                         run[3 * B:4 * B].data_ptr(), None, None)
-grid = (B + 1) // 2
+v1 = os.environ.get("MLG_REFIL_ROLLOUT") == "v1"
+grid = (B + 1) // 2 + 64  # waves of the two-env kernel (upper bound for the four-env one)
 buf = torch.zeros(grid * 16, dtype=torch.int64, device=dev)
 _native.call("mlg_refil_debug_set_stamps", _native.ptr(buf))
 for i in range(3):
@@ -37,8 +38,12 @@ for i in range(3):
                  _native.ptr(ag.packed()), _native.byref(mb), _native.byref(ri), 0.05, 0, _native.stream_ptr())
 torch.cuda.synchronize()
 a = buf.view(grid, 16).cpu().numpy().astype(np.float64)
-names = ["ein build", "entity_block (fc1/in_trans/attn)", "post (out/fc2/GRU)", "fc3+select+record", "env exec",
-         "env resolve", "env reduce/reward", "hp update + observe", "finish/tails"]
+a = a[a[:, 15] == 1]
+grid = len(a)
+names = (["ein build", "entity_block (fc1/in_trans/attn)", "post (out/fc2/GRU)", "fc3+select+record", "env exec",
+          "env resolve", "env reduce/reward", "hp update + observe", "finish/tails"] if v1 else
+         ["loop top", "entity pairs (fc1/in_trans/attn)", "post (out/fc2/GRU)", "fc3+select+onehot", "env exec",
+          "env resolve", "env reduce/reward", "hp update + observe", "finish/tails"])
 tot = a[:, 14].mean()
 print(f"waves={grid} mean cycles/wave={tot:.0f} ({tot / 100e6 * 1e3:.2f} ms at 100 MHz s_memtime)")
 for k, n in enumerate(names):

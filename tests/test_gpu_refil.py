@@ -79,9 +79,18 @@ def _rollout(device, B=12, T=40, seed=5, eps=0.0, test_mode=True, ring=None, age
     return spec, ag, a, np_batch(batch), summary, st
 
 
-@pytest.mark.parametrize("eps,test_mode", [(0.0, True), (0.3, False)])
-def test_rollout_teacher_forced_vs_oracle(device, eps, test_mode):
-    B, T, seed = 12, 40, 5
+@pytest.fixture(params=["v4", "v1"])
+def rollout_variant(request, monkeypatch):
+    """v4: four envs per wave (refil_ro4.inc, the default); v1: the two-env kernel (MLG_REFIL_ROLLOUT=v1)."""
+    monkeypatch.setenv("MLG_REFIL_ROLLOUT", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("eps,test_mode,B,T,seed", [(0.0, True, 12, 40, 5), (0.3, False, 12, 40, 5),
+                                                    (0.05, False, 64, 100, 11)])
+def test_rollout_teacher_forced_vs_oracle(device, rollout_variant, eps, test_mode, B, T, seed):
+    """Teacher-forced: the oracle env replays the recorded actions; every greedy pick is an oracle argmax within Q_TOL,
+    every epsilon draw bit-exact. The 64-env case runs config 5's episode limit (100) with partial workgroups."""
     spec, ag, a, nb, summ, _ = _rollout(device, B, T, seed, eps, test_mode)
     refs = ref_entity_envs_for(spec, B, seed=seed)
     NA, A = spec.n_agents, spec.n_actions
@@ -130,7 +139,7 @@ def test_rollout_teacher_forced_vs_oracle(device, eps, test_mode):
     assert n_greedy > 0 and (test_mode or n_rand > 0)
 
 
-def test_rollout_ring_full_write_equals_zeroed(device):
+def test_rollout_ring_full_write_equals_zeroed(device, rollout_variant):
     """full-write mode writes every byte of the slots (garbage-filled here): identical to the zeroed batch."""
     *_, nb0, s0, st = _rollout(device, B=10, T=30, seed=9, eps=0.2, test_mode=False)
     # same env state as the first run started from: a fresh state advanced by nothing
@@ -140,7 +149,7 @@ def test_rollout_ring_full_write_equals_zeroed(device):
     np.testing.assert_array_equal(s0["len"], s1["len"])
 
 
-def test_rollout_fixed_team_sizes(device):
+def test_rollout_fixed_team_sizes(device, rollout_variant):
     """k = 8 (full teams) and k = 3 (smallest): absent slots masked, padded agents only no-op."""
     for k in (3, 8):
         spec, ag, a, nb, summ, _ = _rollout(device, B=6, T=25, seed=2, kmin=k, kmax=k)
