@@ -169,15 +169,18 @@ struct CopyJob {
     int rows_dst, cols_dst, rows_src, cols_src;
 };
 struct CopyJobs {
-    CopyJob j[16];
+    static constexpr int kCap = 16;
+    CopyJob j[kCap];
     int n;
     int64_t total;
+    bool overflow;
 };
 
 // One launch packs several parameter blocks with the same layout: blockIdx.y selects the (src, dst) pair.
 struct CopyPairs {
-    const float* src[8];
-    float* dst[8];
+    static constexpr int kCap = 8;  // agent: online + target; hypernets: 4 x (online + target)
+    const float* src[kCap];
+    float* dst[kCap];
 };
 __global__ void copy_jobs_kernel(CopyJobs J, CopyPairs pp) {
     const float* __restrict__ src = pp.src[blockIdx.y];
@@ -204,38 +207,41 @@ __global__ void copy_jobs_kernel(CopyJobs J, CopyPairs pp) {
 CopyJob cj(int64_t src, int64_t dst, int rd, int cd, int rs, int cs, int64_t src2 = -1) {
     return CopyJob{src, src2, dst, rd, cd, rs, cs};
 }
+// bounded append: a table filled past its capacity is reported by run_train instead of overrunning
+void push(CopyJobs& J, const CopyJob& c) {
+    if (J.n < CopyJobs::kCap) J.j[J.n++] = c;
+    else J.overflow = true;
+}
 
 CopyJobs agent_jobs(const RAgent& L) {
-    CopyJobs J;
-    J.n = 0;
-    J.j[J.n++] = cj(L.c_w1, L.w1, EMB, L.K1, EMB, L.D0);
-    J.j[J.n++] = cj(L.c_b1, L.b1, 1, EMB, 1, EMB);
-    J.j[J.n++] = cj(L.c_win, L.win, 3 * EMB, EMB, 3 * EMB, EMB);
-    J.j[J.n++] = cj(L.c_wout, L.wout, EMB, EMB, EMB, EMB);
-    J.j[J.n++] = cj(L.c_bout, L.bout, 1, EMB, 1, EMB);
-    J.j[J.n++] = cj(L.c_w2, L.w2, EMB, EMB, EMB, EMB);
-    J.j[J.n++] = cj(L.c_b2, L.b2, 1, EMB, 1, EMB);
-    J.j[J.n++] = cj(L.c_wih, L.wih, 3 * EMB, EMB, 3 * EMB, EMB);
-    J.j[J.n++] = cj(L.c_whh, L.whh, 3 * EMB, EMB, 3 * EMB, EMB);
-    J.j[J.n++] = cj(L.c_bih, L.bih, 1, 3 * EMB, 1, 3 * EMB);
-    J.j[J.n++] = cj(L.c_bhh, L.bhh, 1, 3 * EMB, 1, 3 * EMB);
-    J.j[J.n++] = cj(L.c_bih, L.brz, 1, 2 * EMB, 1, 2 * EMB, L.c_bhh);
-    J.j[J.n++] = cj(L.c_w3, L.w3, L.Ap, EMB, L.A, EMB);
-    J.j[J.n++] = cj(L.c_b3, L.b3, 1, L.Ap, 1, L.A);
+    CopyJobs J{};
+    push(J, cj(L.c_w1, L.w1, EMB, L.K1, EMB, L.D0));
+    push(J, cj(L.c_b1, L.b1, 1, EMB, 1, EMB));
+    push(J, cj(L.c_win, L.win, 3 * EMB, EMB, 3 * EMB, EMB));
+    push(J, cj(L.c_wout, L.wout, EMB, EMB, EMB, EMB));
+    push(J, cj(L.c_bout, L.bout, 1, EMB, 1, EMB));
+    push(J, cj(L.c_w2, L.w2, EMB, EMB, EMB, EMB));
+    push(J, cj(L.c_b2, L.b2, 1, EMB, 1, EMB));
+    push(J, cj(L.c_wih, L.wih, 3 * EMB, EMB, 3 * EMB, EMB));
+    push(J, cj(L.c_whh, L.whh, 3 * EMB, EMB, 3 * EMB, EMB));
+    push(J, cj(L.c_bih, L.bih, 1, 3 * EMB, 1, 3 * EMB));
+    push(J, cj(L.c_bhh, L.bhh, 1, 3 * EMB, 1, 3 * EMB));
+    push(J, cj(L.c_bih, L.brz, 1, 2 * EMB, 1, 2 * EMB, L.c_bhh));
+    push(J, cj(L.c_w3, L.w3, L.Ap, EMB, L.A, EMB));
+    push(J, cj(L.c_b3, L.b3, 1, L.Ap, 1, L.A));
     J.total = L.gsp;  // the rollout's pre-split sections (gsp, wsp) are not read by the learner
     return J;
 }
 
 CopyJobs hyper_jobs(const RHyper& L) {
-    CopyJobs J;
-    J.n = 0;
-    J.j[J.n++] = cj(L.c_w1, L.w1, EMB, L.K1, EMB, L.D0);
-    J.j[J.n++] = cj(L.c_b1, L.b1, 1, EMB, 1, EMB);
-    J.j[J.n++] = cj(L.c_win, L.win, 3 * EMB, EMB, 3 * EMB, EMB);
-    J.j[J.n++] = cj(L.c_wout, L.wout, EMB, EMB, EMB, EMB);
-    J.j[J.n++] = cj(L.c_bout, L.bout, 1, EMB, 1, EMB);
-    J.j[J.n++] = cj(L.c_w2, L.w2, EM, EMB, EM, EMB);
-    J.j[J.n++] = cj(L.c_b2, L.b2, 1, EM, 1, EM);
+    CopyJobs J{};
+    push(J, cj(L.c_w1, L.w1, EMB, L.K1, EMB, L.D0));
+    push(J, cj(L.c_b1, L.b1, 1, EMB, 1, EMB));
+    push(J, cj(L.c_win, L.win, 3 * EMB, EMB, 3 * EMB, EMB));
+    push(J, cj(L.c_wout, L.wout, EMB, EMB, EMB, EMB));
+    push(J, cj(L.c_bout, L.bout, 1, EMB, 1, EMB));
+    push(J, cj(L.c_w2, L.w2, EM, EMB, EM, EMB));
+    push(J, cj(L.c_b2, L.b2, 1, EM, 1, EM));
     J.total = L.total;
     return J;
 }
@@ -243,8 +249,9 @@ CopyJobs hyper_jobs(const RHyper& L) {
 // Hypernet in_trans [192][64] as split-bf16 MFMA A operands for hyper_fwd (the rollout's wsp tiles 0-11 layout:
 // element ((reg * 64 + lane) * 4 + q), reg = (tile * 2 + kk) * 3 + piece), blockIdx.y = (hypernet, net) block.
 struct HSplit {
-    const float* src[10];
-    float* dst[10];
+    static constexpr int kCap = 10;  // 4 hypernets + the agent, online + target
+    const float* src[kCap];
+    float* dst[kCap];
 };
 __global__ void hyper_split_kernel(HSplit J) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -347,7 +354,8 @@ struct TrJob {
     int rows, cols;
 };
 struct TrJobs {
-    TrJob j[16];
+    static constexpr int kCap = 16;
+    TrJob j[kCap];
     int n;
 };
 __global__ void transpose_kernel(TrJobs J) {
@@ -1379,6 +1387,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     const WsR& w = p.w;
     // ---- pack: three launches (agent blocks, hypernet blocks, all transposes) ----
     const CopyJobs aj = agent_jobs(p.La), hj = hyper_jobs(p.Lh);
+    MLG_REQUIRE(!aj.overflow && !hj.overflow, "refil learner: pack job table over capacity (%d)", CopyJobs::kCap);
+    static_assert(2 * 4 <= CopyPairs::kCap && 2 * 4 + 2 <= HSplit::kCap, "prologue tables: one slot per block");
     CopyPairs ap{}, hpp{};
     ap.src[0] = params;
     ap.dst[0] = ws + w.pa_on;
@@ -1387,7 +1397,11 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((aj.total + 255) / 256), 2), dim3(256), 0, s, aj, ap);
     const RAgent& La = p.La;
     TrJobs tj{};
-    auto tr = [&](const float* src, float* dst, int rows, int cols) { tj.j[tj.n++] = TrJob{src, dst, rows, cols}; };
+    bool tr_bad = false;  // the transpose grid covers jobs of <= 3 * EMB * EMB elements, TrJobs::kCap jobs
+    auto tr = [&](const float* src, float* dst, int rows, int cols) {
+        if (tj.n < TrJobs::kCap && (int64_t)rows * cols <= 3 * EMB * EMB) tj.j[tj.n++] = TrJob{src, dst, rows, cols};
+        else tr_bad = true;
+    };
     tr(params + La.c_win, ws + w.a_winT, 3 * EMB, EMB);
     tr(params + La.c_wout, ws + w.a_woutT, EMB, EMB);
     tr(params + La.c_w2, ws + w.a_w2T, EMB, EMB);
@@ -1402,6 +1416,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         tr(params + G0 + p.Lh.c_wout, ws + w.h_woutT[k], EMB, EMB);
         tr(params + G0 + p.Lh.c_w2, ws + w.h_w2T[k], EM, EMB);
     }
+    MLG_REQUIRE(!tr_bad, "refil learner: transpose job table over capacity or job larger than the grid");
     hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((hj.total + 255) / 256), 8), dim3(256), 0, s, hj, hpp);
     HSplit hs{};
     for (int k = 0; k < 4; ++k) {

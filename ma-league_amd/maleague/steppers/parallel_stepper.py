@@ -132,7 +132,8 @@ class ParallelStepper(EnvStepper):
 
     def initialize(self, scheme, groups, preprocess, home_mac, away_mac=None):
         if away_mac is not None:
-            raise NotImplementedError("self-play (away MAC) rollout is a next-round item (SURVEY §8f)")
+            raise NotImplementedError("ParallelStepper drives one policy; self-play (home + away MAC) is "
+                                      "SelfPlayParallelStepper (steppers.SELF_REGISTRY['parallel'])")
         self.new_batch_fn = partial(EpisodeBatch, scheme, groups, self.batch_size, self.episode_limit + 1,
                                     preprocess=preprocess, device=self.device)
         self.home_mac = home_mac

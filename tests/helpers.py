@@ -83,3 +83,37 @@ def ref_entity_envs_for(spec, B, seed=0):
     return [envref.RefEntityEnv(spec.roles, spec.melees, spec.min_agents, spec.max_agents, grid=spec.grid,
                                 episode_limit=spec.episode_limit, stochastic=spec.stochastic, seed=seed, env_index=b)
             for b in range(B)]
+
+
+def assert_near_tie_divergence(ref_sides, got_sides, q_sides, B, tol=1e-5):
+    """two kernels that agree in fp32 up to summation order must produce the same episodes except where a
+    near-tie flips an argmax. For every episode that differs (over every side of a self-play pair), the first differing
+    step t must have identical pre-transition data (state, obs, avail, filled: the env states agree up to t) and differ
+    in the actions, and each differing pick must be a near-tie of the fp32 oracle's Q along the recorded trajectory
+    (|Q[a_got] - Q[a_ref]| <= tol, both available). Returns the number of differing episodes."""
+    import numpy as np
+    pre_keys = ("state", "obs", "avail_actions", "filled")
+    n_diff = 0
+    for b in range(B):
+        t_first = None
+        T1 = got_sides[0]["actions"].shape[1]
+        for t in range(T1):
+            if any(not np.array_equal(r[k][b, t], g[k][b, t]) for r, g in zip(ref_sides, got_sides) for k in g):
+                t_first = t
+                break
+        if t_first is None:
+            continue
+        n_diff += 1
+        flips = 0
+        for r, g, q in zip(ref_sides, got_sides, q_sides):
+            for k in pre_keys:
+                if k in g:
+                    assert np.array_equal(r[k][b, t_first], g[k][b, t_first]), (b, t_first, k)
+            av = g["avail_actions"][b, t_first].astype(bool)
+            for n in np.nonzero(r["actions"][b, t_first, :, 0] != g["actions"][b, t_first, :, 0])[0]:
+                ag, ar = int(g["actions"][b, t_first, n, 0]), int(r["actions"][b, t_first, n, 0])
+                assert av[n, ag] and av[n, ar], (b, t_first, n)
+                assert abs(float(q[b, t_first, n, ag]) - float(q[b, t_first, n, ar])) <= tol, (b, t_first, n, ag, ar)
+                flips += 1
+        assert flips > 0, f"episode {b} diverges at t={t_first} without an action flip"
+    return n_diff

@@ -178,3 +178,49 @@ def test_qlearner_sampled_view_equals_truncated_copy(device):
     # host reads of the view materialise the same episodes
     for k in ("obs", "actions", "filled"):
         assert torch.equal(view[k], copy_[k]), k
+
+
+def test_qlearner_vs_oracle_full_config2_sample(device):
+    """the config-2 shapes -- a 4096-env, episode_limit 100 train-mode rollout written into the HBM
+    replay ring, 32 episodes sampled in place (the learner reads the slot map over the buffer's full length), one
+    QLearner.train against the oracle on the truncated gathered copy of the same 32 episodes."""
+    from maleague.components.episode_batch import EpisodeBatch
+    from maleague.components.replay_buffer import ReplayBuffer
+    from maleague.controllers import BasicMAC
+    from maleague.custom_logging import MainLogger
+    from maleague.learners import QLearner
+    from maleague.steppers import ParallelStepper
+    B = 4096
+    args = qmix_args(batch_size_run=B, seed=7, env_args={"match_build_plan": "medium_1h_4t", "grid_size": 20,
+                                                         "stochastic_spawns": True, "episode_limit": 100})
+    stepper = ParallelStepper(args, MainLogger())
+    info = stepper.get_env_info()
+    args.n_agents, args.n_actions, args.state_shape = info["n_agents"], info["n_actions"], info["state_shape"]
+    scheme, groups, preprocess = scheme_for(info, torch)
+    proto = EpisodeBatch(scheme, groups, 1, 2, preprocess=preprocess, device=device)
+    torch.manual_seed(5)
+    mac = BasicMAC(proto.scheme, groups, args)
+    learner = QLearner(mac, proto.scheme, _Log(), args, name="home")
+    agent0 = {k: v.detach().cpu().clone() for k, v in mac.agent.state_dict().items()}
+    mixer0 = {k: v.detach().cpu().clone() for k, v in learner.mixer.state_dict().items()}
+    learner.build_optimizer()
+    stepper.initialize(scheme, groups, preprocess, mac)
+    ring = ReplayBuffer(scheme, groups, 5000, 101, preprocess=preprocess, device=device)
+    assert stepper.attach_replay(ring)
+    stepper.t_env = 10 ** 6  # epsilon floor 0.05
+    batch, _ = stepper.run(test_mode=False)
+    ring.insert_episode_batch(batch)
+    np.random.seed(4)
+    sample = ring.sample(32, view=True)
+    T = int(sample.max_t_filled())
+    assert T >= 30
+    tb = {k: v[:, :T].detach().cpu().clone() for k, v in sample.data.transition_data.items()}
+    ref = LR.QLearnerRef(agent0, mixer0, copy.copy(args))
+    want = ref.train(tb, 10 ** 6, 0)
+    learner.train(sample, 10 ** 6, 0)
+    for k in ["loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]:
+        np.testing.assert_allclose(learner.last_stats[k], want[k], rtol=2e-4, atol=1e-6, err_msg=k)
+    for k, v in learner.mac.agent.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), ref.agent_state()[k].numpy(), atol=5e-5, rtol=0, err_msg=k)
+    for k, v in learner.mixer.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), ref.mixer_state()[k].numpy(), atol=5e-5, rtol=0, err_msg=k)

@@ -10,7 +10,7 @@ import torch
 
 import envref
 import learner_ref as LR
-from helpers import np_batch, qmix_args, ref_envs_for, scheme_for
+from helpers import assert_near_tie_divergence, np_batch, qmix_args, ref_envs_for, scheme_for
 
 pytestmark = pytest.mark.gpu
 
@@ -400,5 +400,6 @@ def test_rollout_v7_split_bf16_gru_matches_fp32(device, plan, generic, monkeypat
             assert np.isfinite(chosen).all(), (b_, t)  # chosen action available
             worst = max(worst, float((best - chosen).max()))
     assert worst <= 1e-5, worst
-    same = [all(np.array_equal(out["v2"][0][kk][b_], nb[kk][b_]) for kk in nb) for b_ in range(B)]
-    assert np.mean(same) >= 0.9, np.mean(same)
+    # episodes that differ from v2's must diverge at a near-tie flip of an argmax, not anywhere
+    n_diff = assert_near_tie_divergence([out["v2"][0]], [nb], [q], B)
+    assert n_diff <= B // 10, n_diff

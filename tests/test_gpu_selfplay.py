@@ -14,7 +14,7 @@ import torch
 import envref
 import learner_ref as LR
 import stepper_ref
-from helpers import np_batch, qmix_args, ref_envs_for, scheme_for
+from helpers import assert_near_tie_divergence, np_batch, qmix_args, ref_envs_for, scheme_for
 
 pytestmark = pytest.mark.gpu
 
@@ -306,12 +306,14 @@ def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, monkeypatch):
     nbs, L = out["sp7"]
     N = args.n_agents
     worst = 0.0
+    qs = []
     for mac, nb in zip((home, away), nbs):
         tb = {kk: torch.from_numpy(v) for kk, v in nb.items()}
         p = {kk: v.detach().cpu() for kk, v in mac.agent.state_dict().items()}
         with torch.no_grad():
             q, _ = LR.mac_unroll(p, tb, N, T=TL + 1)
         q = q.numpy()
+        qs.append(q)
         av = nb["avail_actions"].astype(bool)
         for b_ in range(B):
             for t in range(int(L[b_]) + 1):
@@ -320,6 +322,5 @@ def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, monkeypatch):
                 assert np.isfinite(chosen).all(), (b_, t)
                 worst = max(worst, float((qm.max(axis=-1) - chosen).max()))
     assert worst <= 1e-5, worst
-    ref = out["sp2"][0]
-    same = [all(np.array_equal(ref[s][kk][b_], nbs[s][kk][b_]) for s in (0, 1) for kk in nbs[s]) for b_ in range(B)]
-    assert np.mean(same) >= 0.9, np.mean(same)
+    n_diff = assert_near_tie_divergence(out["sp2"][0], nbs, qs, B)  # only near-tie flips diverge
+    assert n_diff <= B // 10, n_diff
