@@ -486,24 +486,32 @@ RO_PHASE void ro_observe(RoLds& S, const EnvTables& T, const EnvMasks& M, const 
     if (active && u == 0) S.em[e] = (uint32_t)((bal >> (16 * e)) & 0xFFFFu);
 }
 
+// zero bytes [b0, b1) of base with all 64 lanes: 16-byte stores for the aligned middle, byte stores at the edges
+__device__ inline void zero_bytes(void* base, int64_t b0, int64_t b1, int lane) {
+    if (b1 <= b0) return;
+    uint8_t* p = reinterpret_cast<uint8_t*>(base);
+    const uintptr_t ua = ((uintptr_t)(p + b0) + 15) & ~(uintptr_t)15, ub = (uintptr_t)(p + b1) & ~(uintptr_t)15;
+    int64_t m0 = (int64_t)(ua - (uintptr_t)p), m1 = (int64_t)(ub - (uintptr_t)p);
+    if (m0 > b1 || m1 < m0) m0 = m1 = b1;  // too short for an aligned middle
+    for (int64_t i = b0 + lane; i < m0; i += 64) p[i] = 0;
+    for (int64_t i = m0 + 16 * (int64_t)lane; i < m1; i += 16 * 64) *reinterpret_cast<uint4*>(p + i) = make_uint4(0, 0, 0, 0);
+    for (int64_t i = (m1 > b0 ? m1 : b0) + lane; i < b1; i += 64) p[i] = 0;
+}
+
 // zero slots [t0, T1) of every key for env e (full-write ring mode), all 64 lanes
 __device__ inline void ro_zero_tail(const MlgEntityBatch& bt, const RoArgs& a, int64_t slot, int t0, int lane) {
     if (t0 >= bt.T1) return;
     const int64_t r0 = slot * bt.T1 + t0, r1 = (slot + 1) * (int64_t)bt.T1;
-    auto zf = [&](float* p, int64_t inner) {
-        for (int64_t i = r0 * inner + lane; i < r1 * inner; i += 64) p[i] = 0.f;
-    };
-    zf(bt.entities, (int64_t)a.U * a.ED);
-    zf(bt.actions_onehot, (int64_t)a.NA * a.A);
-    zf(bt.reward, 1);
-    for (int64_t i = r0 * a.U * a.U + lane; i < r1 * a.U * a.U; i += 64) bt.obs_mask[i] = 0;
-    for (int64_t i = r0 * a.U + lane; i < r1 * a.U; i += 64) bt.entity_mask[i] = 0;
-    for (int64_t i = r0 * a.NA + lane; i < r1 * a.NA; i += 64) bt.actions[i] = 0;
-    for (int64_t i = r0 * a.NA * a.A + lane; i < r1 * a.NA * a.A; i += 64) bt.avail[i] = 0;
-    for (int64_t i = r0 + lane; i < r1; i += 64) {
-        bt.terminated[i] = 0;
-        bt.filled[i] = 0;
-    }
+    auto z = [&](void* p, int64_t row_bytes) { zero_bytes(p, r0 * row_bytes, r1 * row_bytes, lane); };
+    z(bt.entities, (int64_t)a.U * a.ED * 4);
+    z(bt.actions_onehot, (int64_t)a.NA * a.A * 4);
+    z(bt.reward, 4);
+    z(bt.obs_mask, (int64_t)a.U * a.U);
+    z(bt.entity_mask, a.U);
+    z(bt.actions, (int64_t)a.NA * 8);
+    z(bt.avail, (int64_t)a.NA * a.A * 4);
+    z(bt.terminated, 1);
+    z(bt.filled, 8);
 }
 
 // Workgroup = RO_WAVES waves; every wave owns two envs for the whole episode (no cross-wave dependency after the

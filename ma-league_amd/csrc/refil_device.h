@@ -283,8 +283,13 @@ __device__ inline void attn_fwd(const float* qkv, const uint32_t* mrow, int nq, 
 
 
 // attn_fwd_split for nq <= 8 using all 64 lanes: lane (h = lane >> 4, q = lane & 7, half = (lane >> 3) & 1) scores
-// keys [8 half, 8 half + 8); max, sum and the weighted values are combined with the partner lane (xor 8).
-// Same softmax (exp(s - max) / sum) with a two-way split of the sums.
+// keys [8 half, 8 half + 8); max, sum and the weighted values are combined with the partner lane (lane ^ 8 = DPP
+// row_ror:8 inside the 16-lane row, a VALU move instead of an LDS permute). Rollout form (the recorded actions are
+// the fp32 oracle's argmax within the parity tests' 1e-4 Q tolerance): softmax on v_exp_f32 (__expf) and one
+// reciprocal per row, exp(s - max) * (1 / sum).
+__device__ __forceinline__ float xor8f(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, true));
+}
 __device__ inline void attn_fwd_half(const float* qb, int ldq, const float* kb, const float* vb, int ldkv,
                                      const uint32_t* mrow, int nq, int ne, float* o, int ldo, int lane) {
     const int h = lane >> 4, q = lane & 7, half = (lane >> 3) & 1, k0 = half * 8;
@@ -314,7 +319,7 @@ __device__ inline void attn_fwd_half(const float* qb, int ldq, const float* kb, 
         s[kk] = ((m >> k) & 1u) ? -INFINITY : d * 0.25f;
         mx = fmaxf(mx, s[kk]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 8));
+    mx = fmaxf(mx, xor8f(mx));
     float ov[HD];
 #pragma unroll
     for (int d = 0; d < HD; ++d) ov[d] = 0.f;
@@ -322,15 +327,16 @@ __device__ inline void attn_fwd_half(const float* qb, int ldq, const float* kb, 
     if (mx != -INFINITY) {
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
-            s[kk] = ((m >> (k0 + kk)) & 1u) ? 0.f : expf(s[kk] - mx);
+            s[kk] = ((m >> (k0 + kk)) & 1u) ? 0.f : __expf(s[kk] - mx);
             sum += s[kk];
         }
     }
-    sum += __shfl_xor(sum, 8);
+    sum += xor8f(sum);
     if (mx != -INFINITY) {
+        const float inv = 1.f / sum;
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
-            const float p = s[kk] / sum;
+            const float p = s[kk] * inv;
             const float* vr = vb + (k0 + kk) * ldkv + h * HD;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -343,7 +349,7 @@ __device__ inline void attn_fwd_half(const float* qb, int ldq, const float* kb, 
         }
     }
 #pragma unroll
-    for (int d = 0; d < HD; ++d) ov[d] += __shfl_xor(ov[d], 8);
+    for (int d = 0; d < HD; ++d) ov[d] += xor8f(ov[d]);
     if (qv_ok && half == 0) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)

@@ -128,3 +128,36 @@ def test_refil_learner_padded_steps_are_inert(device, golden):
         for k in s1:
             np.testing.assert_allclose(s2[k], s1[k], rtol=1e-5, atol=1e-7, err_msg=k)
         np.testing.assert_allclose(L2._flat.flat.cpu().numpy(), L1._flat.flat.cpu().numpy(), atol=1e-6, rtol=0)
+
+
+def test_refil_learner_matches_oracle_config5_batch(device):
+    """the config-5 learner shape -- 32 episodes (drawn from a 64-env rollout of the HIP REFIL kernel
+    at episode_limit 100, eps 0.05, 3..8 agents per env) truncated at max_t_filled, one train call vs the oracle."""
+    from test_gpu_refil import _rollout
+    spec, ag, a0, nb, summ, _ = _rollout(device, B=64, T=100, seed=21, eps=0.05, test_mode=False)
+    rng = np.random.RandomState(3)
+    ids = np.sort(rng.choice(64, 32, replace=False))
+    T = int(summ["len"][ids].max()) + 1
+    arrs = {k: np.ascontiguousarray(v[ids, :T]) for k, v in nb.items()}
+    a = refil_args(device="cuda")
+    eb = _batch_from(arrs, device)
+    torch.manual_seed(6)
+    from maleague.modules.mixers import FlexQMixer
+    mixer_p = {k: v.detach().cpu().numpy() for k, v in FlexQMixer(refil_args(device="cpu")).state_dict().items()}
+    agent_p = {k: v.detach().cpu().numpy() for k, v in ag.state_dict().items()}
+    L, _ = _learner(eb, agent_p, mixer_p, a)
+    ref = RR.REFILLearnerRef(agent_p, mixer_p, refil_args(device="cpu"))
+    batch = {k: torch.from_numpy(v) for k, v in arrs.items()}
+    g = torch.Generator().manual_seed(9)
+    groupA = torch.bernoulli(torch.rand(32, 1, 1, generator=g).repeat(1, 1, 16), generator=g).to(torch.uint8)
+    want = ref.train(batch, groupA, episode_num=0)
+    L.train(eb, 0, episode_num=0, groupA=groupA.to(device))
+    got = L.last_stats
+    for k in want:
+        np.testing.assert_allclose(got[k], want[k], rtol=2e-4, atol=1e-5, err_msg=k)
+    for k, v in L.mac.agent.named_parameters():
+        np.testing.assert_allclose(v.detach().cpu().numpy(), ref.agent[k].detach().numpy(), atol=2e-5, rtol=0,
+                                   err_msg=f"agent {k}")
+    for k, v in L.mixer.named_parameters():
+        np.testing.assert_allclose(v.detach().cpu().numpy(), ref.mixer[k].detach().numpy(), atol=2e-5, rtol=0,
+                                   err_msg=f"mixer {k}")
