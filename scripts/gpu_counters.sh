@@ -23,5 +23,5 @@ for m in ${MODES:-ai league refil}; do
   pass $m sq2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
   pass $m sq3 SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_FLAT GRBM_GUI_ACTIVE
 done
-python3 scripts/parse_counters.py $OUT "${COMMIT:-unknown}" > $OUT/counters.json || exit 1
+python3 scripts/parse_counters.py $OUT "${COMMIT:-unknown}" ${MERGE:-} > $OUT/counters.json || exit 1
 cat $OUT/counters.json

@@ -55,4 +55,8 @@ for k, cs in vals.items():
     if m.get("SQ_INSTS_MFMA"):
         d["valu_per_mfma"] = m.get("SQ_INSTS_VALU", 0.0) / m["SQ_INSTS_MFMA"]
     out[k] = d
+if len(sys.argv) > 3 and os.path.exists(sys.argv[3]):  # merge into an existing counters.json (other kernels kept)
+    prev = json.load(open(sys.argv[3])).get("kernels", {})
+    prev.update(out)
+    out = prev
 print(json.dumps({"kernels": out, "note": __doc__.strip().splitlines()[0]}, indent=1))
