@@ -610,6 +610,8 @@ __global__ void __launch_bounds__(256) rec_kernel(RCfg c, RAgent L, const float*
 #pragma unroll
         for (int kc = 0; kc < HC; ++kc) wr[q][kc] = ld4(P + L.whh + (int64_t)(q * H + w * 16 + col) * H + kc * 16 + 4 * g);
     const floatx4 bhn = ld4(P + L.bhh + 2 * H + f0);
+    const __amdgpu_buffer_rsrc_t rs_h = mlg_rsrc(hsg), rs_gr = mlg_rsrc(ws_gr), rs_gz = mlg_rsrc(ws_gz),
+                                 rs_gn = mlg_rsrc(ws_gn), rs_ghn = mlg_rsrc(ws_ghn);
     for (int i = tid; i < 16 * LDX; i += blockDim.x) hs[0][i] = 0.f;
     if (valid) *reinterpret_cast<floatx4*>(hsg + (int64_t)r * H + f0) = floatx4{0.f, 0.f, 0.f, 0.f};
     const int rr = valid ? r : 0;
@@ -637,21 +639,21 @@ __global__ void __launch_bounds__(256) rec_kernel(RCfg c, RAgent L, const float*
         const floatx4 hp = ld4(hs[cur] + col * LDX + f0);
         floatx4 rg, zg, ng, hn;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            rg[q] = sigm(ar[q]);
-            zg[q] = sigm(az[q]);
-            ng[q] = tanhf(gin[q] + rg[q] * ahn[q]);
+        for (int q = 0; q < 4; ++q) {  // gates on v_exp_f32 / v_rcp_f32 (as the QMIX learner's recurrence)
+            rg[q] = fast_sigmoid(ar[q]);
+            zg[q] = fast_sigmoid(az[q]);
+            ng[q] = fast_tanh(gin[q] + rg[q] * ahn[q]);
             hn[q] = ng[q] + zg[q] * (hp[q] - ng[q]);
         }
         *reinterpret_cast<floatx4*>(hs[cur ^ 1] + col * LDX + f0) = hn;
-        if (valid) {
+        {  // branch-free stores (dropped rows: out-of-range buffer offsets), so the prefetch waits count them
             const int64_t o = ((int64_t)t * R + r) * H + f0;
-            *reinterpret_cast<floatx4*>(hsg + o + (int64_t)R * H) = hn;
+            st4_if(rs_h, o + (int64_t)R * H, hn, valid);
             if (online) {
-                *reinterpret_cast<floatx4*>(ws_gr + o) = rg;
-                *reinterpret_cast<floatx4*>(ws_gz + o) = zg;
-                *reinterpret_cast<floatx4*>(ws_gn + o) = ng;
-                *reinterpret_cast<floatx4*>(ws_ghn + o) = ahn;
+                st4_if(rs_gr, o, rg, valid);
+                st4_if(rs_gz, o, zg, valid);
+                st4_if(rs_gn, o, ng, valid);
+                st4_if(rs_ghn, o, ahn, valid);
             }
         }
         __syncthreads();
@@ -713,10 +715,13 @@ struct HypPtrs {
 __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
                                                        RHyper L, const float* __restrict__ ein, HypPtrs hp,
                                                        const float* __restrict__ msum) {
-    __shared__ float s_ein[NE * LDI];
-    __shared__ float s_x1[NE * LDX];
-    __shared__ float s_qkv[NE * LDQ];
-    __shared__ float s_o[32 * LDX];
+    // s_ein and s_x1 live inside s_o (dead before the attention writes it): 21 KB of LDS per item instead of 29 KB,
+    // seven workgroups per CU instead of five
+    static_assert(NE * LDI + NE * LDX <= 32 * LDX, "s_ein + s_x1 alias s_o");
+    __shared__ __attribute__((aligned(16))) float s_qkv[NE * LDQ];
+    __shared__ __attribute__((aligned(16))) float s_o[32 * LDX];
+    float* const s_ein = s_o;
+    float* const s_x1 = s_o + NE * LDI;
     __shared__ uint32_t s_m[3][16];
     __shared__ uint32_t s_dead;
     const int lane = threadIdx.x;
@@ -737,7 +742,6 @@ __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt
     const int ie = b * c.T + ts;
     const float* P = net ? hp.Ptg[k] : hp.Pon[k];
     const int V = net ? 1 : nvar(k);
-    for (int q = lane; q < 32 * LDX; q += 64) s_o[q] = 0.f;
     if (lane < 16) {
         const int q = lane;
         const uint32_t em = em_bits(c, bt, b, ts);
@@ -768,6 +772,9 @@ __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt
         for (int q = lane; q < NE * 3 * EMB; q += 64)
             hp.qkvm[k][(int64_t)i * NE * 3 * EMB + q] = s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)];
     }
+    wave_sync();  // s_ein / s_x1 dead: s_o (same bytes) zeroed for the attention outputs
+    for (int q = lane; q < 32 * LDX; q += 64) s_o[q] = 0.f;
+    wave_sync();
     for (int v = 0; v < V; ++v)
         attn_fwd(s_qkv, s_m[v], c.NA, c.NE, s_o + v * NAS * LDX, LDX,
                  net ? nullptr : hp.Pm[k] + ((int64_t)v * c.I + i) * 1024, lane);
@@ -1150,6 +1157,7 @@ __global__ void __launch_bounds__(256) rec_bwd_kernel(RCfg c, MlgEntityBatch bt,
         }
     }
     floatx4 dh = {0.f, 0.f, 0.f, 0.f};
+    const __amdgpu_buffer_rsrc_t rs_gi = mlg_rsrc(dgi), rs_gh = mlg_rsrc(dgh);
     Step nx = load_step(Te - 1);
     int cur = 0;
     for (int t = Te - 1; t >= 0; --t) {
@@ -1172,21 +1180,21 @@ __global__ void __launch_bounds__(256) rec_bwd_kernel(RCfg c, MlgEntityBatch bt,
         *reinterpret_cast<floatx4*>(gh + f0) = drp;
         *reinterpret_cast<floatx4*>(gh + H + f0) = dzp;
         *reinterpret_cast<floatx4*>(gh + 2 * H + f0) = dghn;
-        if (valid) {
+        {  // branch-free stores (dropped rows: out-of-range buffer offsets)
             const int64_t o3 = ((int64_t)t * R + r) * 3 * H + f0;
-            *reinterpret_cast<floatx4*>(dgi + o3) = drp;
-            *reinterpret_cast<floatx4*>(dgi + o3 + H) = dzp;
-            *reinterpret_cast<floatx4*>(dgi + o3 + 2 * H) = dnp;
-            *reinterpret_cast<floatx4*>(dgh + o3) = drp;
-            *reinterpret_cast<floatx4*>(dgh + o3 + H) = dzp;
-            *reinterpret_cast<floatx4*>(dgh + o3 + 2 * H) = dghn;
+            st4_if(rs_gi, o3, drp, valid);
+            st4_if(rs_gi, o3 + H, dzp, valid);
+            st4_if(rs_gi, o3 + 2 * H, dnp, valid);
+            st4_if(rs_gh, o3, drp, valid);
+            st4_if(rs_gh, o3 + H, dzp, valid);
+            st4_if(rs_gh, o3 + 2 * H, dghn, valid);
         }
         __syncthreads();
-        floatx4 dprev = dhd;
         const float* ghr = sgh[cur] + col * LDG + 4 * g;
+        floatx4 dp[4] = {dhd, floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) dprev = mfma_chunk(wt[kc], ld4(ghr + kc * 16), dprev);
-        dh = dprev;
+        for (int kc = 0; kc < KC; ++kc) dp[kc & 3] = mfma_chunk(wt[kc], ld4(ghr + kc * 16), dp[kc & 3]);
+        dh = (dp[0] + dp[1]) + (dp[2] + dp[3]);  // four independent MFMA chains instead of one of 48
         cur ^= 1;
     }
 }
