@@ -122,13 +122,17 @@ def timed_loop(ctx: Ctx, iteration, stepper, steps: int, warmup: int) -> dict:
             "avg_kernel_ms": (sum(ev_ms) / len(ev_ms)) if ev_ms else None}
 
 
-def league_iteration(inst, match_len: int, exchange_s: list):
+def league_iteration(inst, match_len: int, exchange_s: list, ctx=None):
     """One training iteration of a league player; every ``match_len`` iterations a league iteration first
     (LeagueInstance.sync: payoff all_reduce, parameter / checkpoint all_gather, barrier, matchmaking --
-    matchmaking_league_instance.py:36-68), its wall time appended to ``exchange_s``."""
+    matchmaking_league_instance.py:36-68), its wall time appended to ``exchange_s``. The exchange reads the
+    replicated state on the host, so it drains this rank's queued iterations first; the drain is excluded from
+    the exchange's time (it is training time), the wait for the other ranks is not."""
 
     def it(i):
         if i % match_len == 0:
+            if ctx is not None:
+                ctx.sync()
             t0 = time.perf_counter()
             inst.sync()
             exchange_s.append(time.perf_counter() - t0)
@@ -140,8 +144,8 @@ def league_iteration(inst, match_len: int, exchange_s: list):
 def run_league_leg(ctx: Ctx, inst, steps: int, warmup: int, match_len: int) -> dict:
     """The league leg of the bench (also driven by tests/test_bench_league.py over gloo on CPU)."""
     ex_warm, ex = [], []
-    warm_it = league_iteration(inst, match_len, ex_warm)
-    timed_it = league_iteration(inst, match_len, ex)
+    warm_it = league_iteration(inst, match_len, ex_warm, ctx)
+    timed_it = league_iteration(inst, match_len, ex, ctx)
     n = [0]
 
     def it(i):

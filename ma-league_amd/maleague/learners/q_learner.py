@@ -161,6 +161,9 @@ class QLearner(Learner):
         self.mac.update_trained_steps(self._stats[6])
         self._stats_fresh = True
         if callable(t_env):  # lazily resolved t_env: the kernels above are already queued
+            up = getattr(t_env, "upper", None)
+            if up is not None and up() - self.log_stats_t < self.args.learner_log_interval:
+                return  # no log due for any t_env still possible: no wait for the runs in flight
             t_env = t_env()
         if t_env - self.log_stats_t >= self.args.learner_log_interval:
             for k, v in self.last_stats.items():

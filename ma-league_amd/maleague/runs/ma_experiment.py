@@ -19,6 +19,22 @@ from ..learners import REGISTRY as learner_REGISTRY
 from ..steppers import build_stepper
 
 
+class LazyTEnv:
+    """t_env for a learner's log check without a host sync: call() = the exact value (waits for the runs in
+    flight), upper() = an upper bound that needs no wait (the learner skips resolving when even the bound is
+    below its next log time)."""
+
+    def __init__(self, stepper):
+        self._st = stepper
+
+    def __call__(self) -> int:
+        return self._st.t_env
+
+    def upper(self) -> int:
+        b = getattr(self._st, "t_env_bounds", None)
+        return b()[1] if b is not None else self._st.t_env
+
+
 def find_latest_model_path(path: str, load_step: int = 0):
     """src/utils/run_utils.py:20-37."""
     steps = [int(n) for n in os.listdir(path) if os.path.isdir(os.path.join(path, n)) and n.isdigit()]
@@ -167,7 +183,7 @@ class MultiAgentExperiment:
                 # (steps past max_t_filled are masked out, so loss and gradients equal the truncated batch's),
                 # and t_env resolves only after the learner is queued -- no host sync between the launches
                 sample = self.home_buffer.sample(self.args.batch_size, view=True)
-                self.home_learner.train(sample, lambda: self.stepper.t_env, episode_num)
+                self.home_learner.train(sample, LazyTEnv(self.stepper), episode_num)
                 return
             sample = self.home_buffer.sample(self.args.batch_size)
             max_ep_t = int(sample.max_t_filled())

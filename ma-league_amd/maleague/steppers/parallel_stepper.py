@@ -8,6 +8,7 @@ summary (episode length, return, won/draw) for t_env and the logger.
 """
 from __future__ import annotations
 
+from collections import deque
 from collections.abc import Sequence
 from functools import partial
 
@@ -101,8 +102,9 @@ class ParallelStepper(EnvStepper):
         # running count of agent rows the rollout kernels pushed through the MFMA cell (diagnostics / bench)
         self.agent_rows = torch.zeros(1, dtype=torch.int64, device=self.device)
         pin = self.device.type == "cuda"
-        self._info_host = torch.zeros(6 * B, dtype=torch.int32, pin_memory=pin)
-        self._pending = None  # (run_id, event, test_mode): summary copy in flight
+        # run summaries in flight: one pinned host buffer per run, up to _HOST_RING runs unresolved
+        self._info_hosts = [torch.zeros(6 * B, dtype=torch.int32, pin_memory=pin) for _ in range(self._HOST_RING)]
+        self._pendings = deque()  # (run_id, event, test_mode, host buffer): summary copies in flight
         self._post = []       # resolved runs awaiting host post-processing (logger, env_infos)
         self._runs = {}       # run_id -> (last_run dict, EnvInfos), the latest two
         self._run_id = 0
@@ -116,6 +118,7 @@ class ParallelStepper(EnvStepper):
         self._ring = None   # ReplayBuffer written in place (zero-copy insert), see attach_replay()
 
     _batch_keys = ("state", "obs", "actions", "avail_actions", "reward", "terminated", "actions_onehot", "filled")
+    _HOST_RING = 4
 
     def _build_spec(self, env_args, config_dir):
         return TeamsEnvSpec.from_env_args(env_args, config_dir)
@@ -143,6 +146,10 @@ class ParallelStepper(EnvStepper):
         return self.env_info
 
     # ---- the run summary travels back asynchronously; host state resolves on first use --------------
+    # Nothing in a training iteration needs the host to wait for the GPU: the epsilon of the next run is exact
+    # without the previous run's episode lengths once the schedule is flat over every t_env still possible
+    # (t_env_bounds), the learner's log check likewise, so the host runs up to _HOST_RING runs ahead and a
+    # slow or contended host core does not stall the device (one process per GPU, eight per node).
     @property
     def t_env(self) -> int:
         self._resolve()
@@ -150,7 +157,7 @@ class ParallelStepper(EnvStepper):
 
     @t_env.setter
     def t_env(self, value: int):
-        if getattr(self, "_pending", None) is not None:
+        if getattr(self, "_pendings", None):
             self._resolve()
         self._t_env = int(value)
 
@@ -169,15 +176,49 @@ class ParallelStepper(EnvStepper):
         self._finish_post()
         return self._runs[self._run_id][0] if self._run_id in self._runs else None
 
+    def t_env_bounds(self):
+        """(lower, upper) bounds of t_env without waiting: the resolved value, plus B * episode_limit per
+        train-mode run still in flight."""
+        lo = self._t_env
+        pend = sum(1 for p in self._pendings if not p[2])
+        return lo, lo + pend * self.batch_size * self.episode_limit
+
+    def _epsilon(self, mac, test_mode):
+        """action_selector.epsilon = schedule.eval(t_env) (parallel_stepper.py / basic_controller semantics),
+        resolved on the host only while the (monotone) schedule still changes inside t_env_bounds()."""
+        sel = mac.action_selector
+        lo, hi = self.t_env_bounds()
+        e = sel.schedule.eval(lo)
+        if hi != lo and sel.schedule.eval(hi) != e:
+            e = sel.schedule.eval(self.t_env)
+        sel.epsilon = e
+        if test_mode:
+            sel.epsilon = 0.0
+            return 0.0
+        return float(e)
+
+    def _queue_summary(self, test_mode):
+        """Async D2H of this run's summary into a pinned buffer of the ring (stream-ordered before the next
+        run's kernel rewrites the device copy), then an event marking it."""
+        while len(self._pendings) >= self._HOST_RING:
+            self._resolve_one()
+        host = self._info_hosts[(self._run_id + 1) % self._HOST_RING]
+        host.copy_(self._info, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._run_id += 1
+        self._pendings.append((self._run_id, ev, test_mode, host))
+
     def _resolve(self):
-        """Wait for the latest rollout's summary (t_env, t); the rest of the host work is deferred."""
-        if getattr(self, "_pending", None) is None:
-            return
-        run_id, ev, test_mode = self._pending
-        self._pending = None
+        """Wait for every run in flight (t_env, t); the rest of the host work is deferred."""
+        while getattr(self, "_pendings", None):
+            self._resolve_one()
+
+    def _resolve_one(self):
+        run_id, ev, test_mode, buf = self._pendings.popleft()
         ev.synchronize()
         B = self.batch_size
-        host = self._info_host.numpy().copy()
+        host = buf.numpy().copy()
         ep_len = host[0:B]
         self._t = int(ep_len.max())
         if not test_mode:
@@ -243,9 +284,7 @@ class ParallelStepper(EnvStepper):
         pass
 
     def reset(self):
-        self._resolve()
-        self._t = 0
-        self.env_steps_this_run = 0
+        pass  # per-run host state resolves lazily (_resolve_one); nothing to wait for before a launch
 
     def _launch(self, batch: EpisodeBatch, epsilon: float, test_mode: bool):
         mb, keep = self._to_mlg(batch)
@@ -276,11 +315,7 @@ class ParallelStepper(EnvStepper):
         self.reset()
         self.logger.test_mode = test_mode
         self.home_mac.init_hidden(batch_size=self.batch_size)
-        sel = self.home_mac.action_selector
-        sel.epsilon = sel.schedule.eval(self.t_env)
-        eps = 0.0 if test_mode else float(sel.epsilon)
-        if test_mode:
-            sel.epsilon = 0.0
+        eps = self._epsilon(self.home_mac, test_mode)
         ring = self._ring if not test_mode else None
         if ring is not None and ring.has_outstanding():
             # the previous train-mode run's episodes still occupy the ring's next slots (not inserted yet):
@@ -299,12 +334,8 @@ class ParallelStepper(EnvStepper):
             self.home_batch = self.new_batch_fn()
             self._launch(self.home_batch, eps, test_mode)
         # summary of this run: async D2H into pinned memory; t_env / env_infos resolve on first use, the
-        # previous run's host post-processing runs now, while this rollout is on the GPU
-        self._info_host.copy_(self._info, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self._run_id += 1
-        self._pending = (self._run_id, ev, test_mode)
+        # earlier runs' host post-processing runs now, while this rollout is on the GPU
+        self._queue_summary(test_mode)
         self._finish_post()
         return self.home_batch, LazyEnvInfos(self, self._run_id)
 

@@ -42,12 +42,7 @@ class SelfPlayParallelStepper(ParallelStepper):
                 getattr(self.away_mac.action_selector, "epsilon", None))
 
     def _epsilon_of(self, mac, test_mode):
-        sel = mac.action_selector
-        sel.epsilon = sel.schedule.eval(self.t_env)
-        eps = 0.0 if test_mode else float(sel.epsilon)
-        if test_mode:
-            sel.epsilon = 0.0
-        return eps
+        return self._epsilon(mac, test_mode)
 
     def run(self, test_mode=False):
         if self.home_mac is None or self.away_mac is None:
@@ -106,11 +101,7 @@ class SelfPlayParallelStepper(ParallelStepper):
             ev[1].record()
             self.timing.append(ev)
         del keep
-        self._info_host.copy_(self._info, non_blocking=True)
-        done = torch.cuda.Event()
-        done.record()
-        self._run_id += 1
-        self._pending = (self._run_id, done, test_mode)
+        self._queue_summary(test_mode)
         self._finish_post()
         return self.home_batch, self.away_batch, LazyEnvInfos(self, self._run_id)
 

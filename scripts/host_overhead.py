@@ -1,0 +1,51 @@
+"""Host time per training iteration of config 2 (launch-side Python + ctypes), measured without syncs, next to the
+GPU time per iteration: the loop is host-bound when the first approaches the second."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ma-league_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from maleague.custom_logging import MainLogger  # noqa: E402
+from maleague.runs import MultiAgentExperiment  # noqa: E402
+
+
+class A:
+    plan, envs, episode_limit = None, 4096, 100
+
+
+args, _ = bench.make_args("ai", A, 0, 0)
+exp = MultiAgentExperiment(args, MainLogger(log_interval=10 ** 12))
+exp._init_stepper()
+st = exp.stepper
+st.t_env = 10 ** 6
+B = st.batch_size
+for i in range(5):
+    exp._train_episode(i * B)
+torch.cuda.synchronize()
+host = []
+t0 = time.perf_counter()
+for i in range(20):
+    h0 = time.perf_counter()
+    exp._train_episode((5 + i) * B)
+    host.append(time.perf_counter() - h0)
+t_host = time.perf_counter() - t0
+torch.cuda.synchronize()
+t_all = time.perf_counter() - t0
+host.sort()
+print(f"host per iteration: median {host[10] * 1e3:.3f} ms, max {host[-1] * 1e3:.3f} ms; host loop {t_host / 20 * 1e3:.3f} "
+      f"ms/it; wall incl. GPU {t_all / 20 * 1e3:.3f} ms/it")
+
+if os.environ.get("PROFILE"):
+    import cProfile
+    import pstats
+    pr = cProfile.Profile()
+    pr.enable()
+    for i in range(20):
+        exp._train_episode((25 + i) * B)
+    pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
