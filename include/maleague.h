@@ -190,6 +190,12 @@ typedef struct {
     float *workspace;            /* mlg_qlearner_workspace_floats() floats */
     float *stats;                /* [8] out: loss, grad_norm, td_error_abs, q_taken_mean, target_mean,
                                     mask_sum, count_nonzero(mask), 0 */
+    /* optional (NULL = off), folded into the same launches instead of separate copies / adds: */
+    float *target_sync;          /* [n_agent + n_mixer] receives the updated parameters (the target update
+                                    q_learner.py:127-128 when it is due after this step; usually target_params) */
+    double *trained_steps;       /* [1] += count_nonzero(mask) (Agent.trained_steps, q_learner.py:104) */
+    const int32_t *host_rows;    /* HOST copy of the slot map (B <= 64): travels as a kernel argument,
+                                    batch.rows is then ignored */
 } MlgLearnerBufs;
 
 int64_t mlg_qlearner_param_counts(const MlgLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);

@@ -107,7 +107,7 @@ struct WsLayout {
     int64_t p_on, p_tg, wihT, mix_on, mix_tg;
     int64_t in, x, hs, hs_tg, gi_on, gi_tg, gr, gz, gn, ghn, mac, tmac, dq, d2, dgi, dgh, da;
     int64_t srow, l1act, d1, da2, df2, dv2;
-    int64_t part, msum, nrm, slab, total;
+    int64_t part, msum, rows, nrm, slab, total;
     int n_mix_tiles, n_tasks;
 };
 
@@ -201,6 +201,7 @@ __device__ void mask_sum_block(const MlgBatch& bt, int B, int T, float* __restri
 // Fused learner prologue (one launch instead of eight): block 0 sums the mask (mask_sum_block); the other blocks
 // pack the online / target agent weights (pack_agent_elem), transpose W_ih (dX pass), pack the online / target
 // QMixer hypernets (pack_mixer_elem) and zero the sparse delta buffers d2 and dq.
+constexpr int MLG_INLINE_ROWS = 64;  // largest batch whose slot map travels as a kernel argument
 struct PrepJob {
     AgentLayout L;
     MlgAgentParams ap_on, ap_tg;
@@ -218,11 +219,27 @@ struct PrepJob {
     MlgBatch bt;
     int B, T;
     float* msum;
+    int n_rows_in;          // > 0: the slot map travels here (host_rows); block 0 stores it to rows_dst
+    int32_t* rows_dst;
+    int32_t rows_in[MLG_INLINE_ROWS];
 };
+static_assert(sizeof(PrepJob) <= 3072, "PrepJob must fit the kernel-argument segment");
 
 __global__ void __launch_bounds__(1024) prep_kernel(PrepJob J) {
     __shared__ float red[1024];
     if (blockIdx.x == 0) {
+        if (J.n_rows_in > 0) {  // the block reads the slot map from LDS; later launches from rows_dst
+            __shared__ int32_t srows[MLG_INLINE_ROWS];
+            if (threadIdx.x < J.n_rows_in) {
+                srows[threadIdx.x] = J.rows_in[threadIdx.x];
+                J.rows_dst[threadIdx.x] = J.rows_in[threadIdx.x];
+            }
+            __syncthreads();
+            MlgBatch b2 = J.bt;
+            b2.rows = srows;
+            mask_sum_block(b2, J.B, J.T, J.msum, red);
+            return;
+        }
         mask_sum_block(J.bt, J.B, J.T, J.msum, red);
         return;
     }
@@ -1398,7 +1415,7 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
                                                       float* __restrict__ grads, float* __restrict__ sq, int64_t n_params,
                                                       float lr, float alpha, float eps, float max_norm, int N,
                                                       float* __restrict__ stats, const float* __restrict__ nrm_part,
-                                                      int n_nrm) {
+                                                      int n_nrm, float* __restrict__ tsync, double* __restrict__ trained) {
     __shared__ float red[1024];
     const int tid = threadIdx.x;
     float s = 0.f;
@@ -1411,7 +1428,9 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
         grads[i] = gi;
         const float a = alpha * sq[i] + (1.f - alpha) * gi * gi;  // RMSprop square_avg
         sq[i] = a;
-        params[i] -= lr * gi / (sqrtf(a) + eps);
+        const float pn = params[i] - lr * gi / (sqrtf(a) + eps);
+        params[i] = pn;
+        if (tsync) tsync[i] = pn;  // target update due after this step (q_learner.py:127-128), same launch
     }
     if (blockIdx.x == 0) {
         float s4[4];
@@ -1430,6 +1449,7 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
             stats[5] = ms;
             stats[6] = ms;
             stats[7] = 0.f;
+            if (trained) trained[0] += (double)ms;  // Agent.trained_steps (q_learner.py:104)
         }
     }
 }
@@ -1529,6 +1549,7 @@ Plan make_plan(const MlgLearnerCfg* cfg, int T1) {
     w.n_mix_tiles = (int)((RM + 15) / 16);
     w.part = take((int64_t)w.n_mix_tiles * 4);
     w.msum = take(4);
+    w.rows = take(MLG_INLINE_ROWS);
     w.nrm = 0;  // placed after the slab (size known once the jobs are built)
     w.slab = o;
     w.total = o;  // + slab size, filled by make_jobs
@@ -1577,7 +1598,9 @@ template <int H>
 int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hipStream_t s) {
     const LCfg& c = p.c;
     float* ws = bufs->workspace;
-    const MlgBatch& bt = bufs->batch;
+    MlgBatch bt = bufs->batch;
+    int32_t* rows_ws = reinterpret_cast<int32_t*>(ws + p.w.rows);
+    if (bufs->host_rows) bt.rows = rows_ws;  // filled by prep_kernel's block 0 from its argument
     const float* params = bufs->params;
     const float* tparams = bufs->target_params;
     // ---- fused prologue: pack online / target agent + mixer, W_ih^T, zero d2 / dq, mask sum ----
@@ -1614,6 +1637,12 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     pj.B = c.B;
     pj.T = c.T;
     pj.msum = ws + p.w.msum;
+    pj.n_rows_in = 0;
+    pj.rows_dst = rows_ws;
+    if (bufs->host_rows) {
+        pj.n_rows_in = c.B;
+        for (int b = 0; b < c.B; ++b) pj.rows_in[b] = bufs->host_rows[b];
+    }
     {
         const int64_t work = 2 * p.L.total + 3 * (int64_t)c.H * c.H + (c.mixer == 2 ? 2 * p.mp.total : 0) + pj.n_d2 + pj.n_dq;
         const int blocks = 1 + (int)std::min<int64_t>((work + 1023) / 1024, 512);
@@ -1684,7 +1713,7 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + p.w.part,
                        p.w.n_mix_tiles, ws + p.w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr,
                        cfg->optim_alpha, cfg->optim_eps, cfg->grad_norm_clip, c.N, bufs->stats, ws + p.w.nrm,
-                       n_red_blocks);
+                       n_red_blocks, bufs->target_sync, bufs->trained_steps);
     return mlg::check_launch("qlearner_train");
 }
 
@@ -1726,6 +1755,8 @@ extern "C" int mlg_qlearner_train(const MlgLearnerCfg* c, const MlgLearnerBufs* 
     MLG_REQUIRE(bt.state && bt.obs && bt.actions && bt.avail && bt.reward && bt.terminated && bt.actions_onehot && bt.filled,
                 "qlearner_train: batch has null tensors");
     MLG_REQUIRE(bt.B == c->B && bt.T1 >= c->T, "qlearner_train: batch B=%d T1=%d vs cfg B=%d T=%d", bt.B, bt.T1, c->B, c->T);
+    MLG_REQUIRE(!b->host_rows || c->B <= MLG_INLINE_ROWS, "qlearner_train: host_rows needs B <= %d (got %d)",
+                MLG_INLINE_ROWS, c->B);
     Plan p = make_plan(c, bt.T1);
     hipStream_t s = (hipStream_t)stream;
     if (c->H == 64) return run_train<64>(p, c, b, s);

@@ -71,7 +71,8 @@ class MlgLearnerCfg(ctypes.Structure):
 
 class MlgLearnerBufs(ctypes.Structure):
     _fields_ = [("batch", MlgBatch)] + [(n, ctypes.c_void_p) for n in ["params", "grads", "square_avg",
-                                                                      "target_params", "workspace", "stats"]]
+                                                                      "target_params", "workspace", "stats",
+                                                                      "target_sync", "trained_steps", "host_rows"]]
 
 
 class MlgEntityEnvSpec(ctypes.Structure):

@@ -25,13 +25,19 @@ def _time_stride_ok(t: torch.Tensor, T1: int) -> bool:
         t.shape[d] == 1 or t.stride(d) == exp[d - 2] for d in range(2, t.dim()))
 
 
-def mlg_batch(batch, required=KEYS):
+def _sampled_view(batch) -> bool:
+    """A SampledEpisodeBatch not yet materialised: kernels read the buffer through its slot map."""
+    return getattr(batch, "host_rows", None) is not None and getattr(batch, "_data", None) is None
+
+
+def mlg_batch(batch, required=KEYS, device_rows=True):
     """Build an MlgBatch for `batch` (EpisodeBatch), making tensors contiguous when the layout is not
-    a plain [B][T1][...] array. Returns (MlgBatch, keepalive-list)."""
+    a plain [B][T1][...] array. Returns (MlgBatch, keepalive-list). With device_rows=False a sampled view's
+    slot map is left out (MlgBatch.rows = NULL): the caller hands its host copy to the kernel instead."""
     rows = None
-    if getattr(batch, "rows", None) is not None and getattr(batch, "_data", None) is None:
+    if _sampled_view(batch):
         # sampled view of a replay buffer: point at the buffer itself, episodes through the slot map
-        rows = batch.rows
+        rows = batch.rows if device_rows else None
         data = batch.ring.data.transition_data
     else:
         data = batch.data.transition_data
@@ -70,7 +76,7 @@ ENTITY_DTYPES = {"entities": torch.float32, "obs_mask": torch.uint8, "entity_mas
 def mlg_entity_batch(batch):
     """Entity-scheme EpisodeBatch (REFIL, config 5) -> MlgEntityBatch. Returns (MlgEntityBatch, keepalive)."""
     rows = None
-    if getattr(batch, "rows", None) is not None and getattr(batch, "_data", None) is None:
+    if _sampled_view(batch):
         rows = batch.rows
         data = batch.ring.data.transition_data
     else:

@@ -170,11 +170,19 @@ class SampledEpisodeBatch(EpisodeBatch):
         self.scheme, self.groups, self.preprocess = ring.scheme, ring.groups, ring.preprocess
         self.batch_size, self.max_seq_length, self.device = len(ep_ids), ring.max_seq_length, ring.device
         self.ep_ids = np.asarray(ep_ids, dtype=np.int64)
-        host = torch.from_numpy(self.ep_ids.astype(np.int32))
-        if torch.device(self.device).type == "cuda":
-            host = host.pin_memory()
-        self.rows = host.to(self.device, non_blocking=True)
+        self.host_rows = np.ascontiguousarray(self.ep_ids, dtype=np.int32)  # kernel-argument slot map
+        self._rows = None
         self._data = None
+
+    @property
+    def rows(self) -> torch.Tensor:
+        """The slot map on the device (int32 [B]); copied on first use only."""
+        if self._rows is None:
+            host = torch.from_numpy(self.host_rows)
+            if torch.device(self.device).type == "cuda":
+                host = host.pin_memory()
+            self._rows = host.to(self.device, non_blocking=True)
+        return self._rows
 
     @property
     def data(self):

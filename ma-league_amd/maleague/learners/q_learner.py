@@ -146,19 +146,28 @@ class QLearner(Learner):
             raise _native.NativeError(lib.mlg_last_error().decode())
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.zeros(int(need * 1.25) + 1024, dtype=torch.float32, device=self.device)
-        mb, keep = mlg_batch(batch)
+        # a sampled view of the device buffer hands its slot map over as a kernel argument (no H2D copy)
+        host_rows = getattr(batch, "host_rows", None)
+        if host_rows is not None and (batch.batch_size > 64 or getattr(batch, "_data", None) is not None):
+            host_rows = None
+        mb, keep = mlg_batch(batch, device_rows=host_rows is None)
+        # the target update due after this step (q_learner.py:127-128) is written by the optimizer launch itself
+        sync = (episode_num - self.last_target_update_episode) / self.args.target_update_interval >= 1.0
+        # no host sync per train step: trained steps accumulate on the device (Agent.trained_steps)
+        counter = self.mac.agent.trained_counter(self.device)
         bufs = _native.MlgLearnerBufs(mb, self._flat.flat.data_ptr(), self._grads.data_ptr(), self._sq.data_ptr(),
-                              self._tflat.flat.data_ptr(), self._ws.data_ptr(), self._stats.data_ptr())
+                                      self._tflat.flat.data_ptr(), self._ws.data_ptr(), self._stats.data_ptr(),
+                                      self._tflat.flat.data_ptr() if sync else None, counter.data_ptr(),
+                                      None if host_rows is None else host_rows.ctypes.data)
         _native.call("mlg_qlearner_train", _native.byref(cfg), _native.byref(bufs), _native.stream_ptr(self.device))
         del keep
         self._step += 1
         self.mac.agent.mark_dirty()
         self.train_calls += 1
-        if (episode_num - self.last_target_update_episode) / self.args.target_update_interval >= 1.0:
-            self.update_targets()
+        if sync:
+            self.target_mac.agent.mark_dirty()
+            self.logger.info(f"Updated {self.name}target network.")
             self.last_target_update_episode = episode_num
-        # no host sync per train step: trained steps accumulate on the device, stats are read when logged
-        self.mac.update_trained_steps(self._stats[6])
         self._stats_fresh = True
         if callable(t_env):  # lazily resolved t_env: the kernels above are already queued
             up = getattr(t_env, "upper", None)

@@ -32,6 +32,13 @@ class AgentNetwork(nn.Module):
         self._trained_host = int(value)
         self._trained_dev = None
 
+    def trained_counter(self, device) -> torch.Tensor:
+        """The device-side float64 running count a learner kernel adds to (created at 0 on first use)."""
+        if self._trained_dev is None or self._trained_dev.device != torch.device(device):
+            extra = 0.0 if self._trained_dev is None else float(self._trained_dev.item())
+            self._trained_dev = torch.full((), extra, dtype=torch.float64, device=device)
+        return self._trained_dev
+
     def add_trained_steps(self, update):
         if torch.is_tensor(update):
             if self._trained_dev is None:
@@ -61,6 +68,7 @@ class DRQNAgentNetwork(AgentNetwork):
         self._packed = None
         self._packed_key = None
         self._dirty = 0
+        self._h0 = None
 
     # ---- kernel plumbing --------------------------------------------------------------------
     def dims(self) -> _native.MlgAgentDims:
@@ -102,7 +110,12 @@ class DRQNAgentNetwork(AgentNetwork):
 
     # ---- reference API -------------------------------------------------------------------------
     def init_hidden(self):
-        return self.fc1.weight.new(1, self.args.rnn_hidden_dim).zero_()
+        """A zero [1, H] state; one cached tensor per device (callers expand it and never write into it), so a
+        rollout's MAC reset launches no fill."""
+        w = self.fc1.weight
+        if self._h0 is None or self._h0.device != w.device or self._h0.dtype != w.dtype:
+            self._h0 = w.new_zeros(1, self.args.rnn_hidden_dim)
+        return self._h0
 
     def forward(self, inputs, hidden_state):
         H = self.args.rnn_hidden_dim
