@@ -14,6 +14,7 @@
 //               (deterministic slab reduction; MFMA with the row index as K)
 //   finish      loss/stat reduction, clip_grad_norm_(10), RMSprop step                       (:104-105, learner.py:25-31)
 // Tensors saved for backward are t-major: [T][R][F] with R = B * N agent rows (r = b * N + n).
+#include <mutex>
 #include <algorithm>
 
 #include "agent_device.h"
@@ -106,9 +107,9 @@ struct LCfg {
 struct WsLayout {
     int64_t p_on, p_tg, wihT, mix_on, mix_tg;
     int64_t in, x, hs, hs_tg, gi_on, gi_tg, gr, gz, gn, ghn, mac, tmac, dq, d2, dgi, dgh, da;
-    int64_t srow, l1act, d1, da2, df2, dv2;
+    int64_t srow, l1act, d1, da2, df2, dv2, hyp_on, hyp_tg;
     int64_t part, msum, rows, nrm, slab, total;
-    int n_mix_tiles, n_tasks;
+    int n_mix_tiles, n_tasks, hyp_stride;
 };
 
 __host__ __device__ inline int64_t a4(int64_t v) { return mlg_align4(v); }
@@ -735,6 +736,94 @@ struct MixerPF {
     static constexpr int T1H = Mx::T1H, TE = Mx::TE, L1T = Mx::L1T;
     static constexpr int OW1 = Mx::OW1, OWF = Mx::OWF, OB1 = Mx::OB1, OVH = Mx::OVH;
 
+    // The state-only half of forward(): layer 1, hyper_w_1's second layer for every agent (pre-abs), hyper_w_final's
+    // second layer (pre-abs) and V(s) (identical in the 4 lanes of a row). Same operations as forward().
+    __device__ static void hyper(const MixPtrs& M, const MixPack& mp, int S, int N, const float* s, floatx4 (&l1)[L1T],
+                                 floatx4 (&w1p)[NMAX][TE], floatx4 (&wfp)[TE], float& v, int lane) {
+        const int col = lane & 15, g = lane >> 4;
+        {  // layer 1
+            floatx4 sv[SPC], wl[L1T][SPC];
+#pragma unroll
+            for (int kc = 0; kc < SPC; ++kc) sv[kc] = load_chunk(s, kc * 16 + 4 * g, S);
+#pragma unroll
+            for (int mt = 0; mt < L1T; ++mt) {
+                l1[mt] = ld4(M.mb1 + mt * 16 + 4 * g);
+#pragma unroll
+                for (int kc = 0; kc < SPC; ++kc) wl[mt][kc] = ld4(M.m1 + (int64_t)(mt * 16 + col) * mp.Sp + kc * 16 + 4 * g);
+            }
+#pragma unroll
+            for (int kc = 0; kc < SPC; ++kc)
+#pragma unroll
+                for (int mt = 0; mt < L1T; ++mt) l1[mt] = mfma_chunk(wl[mt][kc], sv[kc], l1[mt]);
+#pragma unroll
+            for (int mt = 0; mt < L1T; ++mt) {
+                if (mt >= OB1 && mt < OVH) continue;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) l1[mt][q] = fmaxf(l1[mt][q], 0.f);
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) {
+            if (n >= N) break;
+            floatx4 wa[TE][T1H];
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc) {
+                w1p[n][cc] = ld4(M.ba2 + n * E + cc * 16 + 4 * g);
+#pragma unroll
+                for (int kc = 0; kc < T1H; ++kc)
+                    wa[cc][kc] = ld4(M.a2 + (int64_t)(n * E + cc * 16 + col) * HE + kc * 16 + 4 * g);
+            }
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc)
+#pragma unroll
+                for (int kc = 0; kc < T1H; ++kc) w1p[n][cc] = mfma_chunk(wa[cc][kc], l1[OW1 + kc], w1p[n][cc]);
+        }
+        floatx4 wf[TE][T1H], wv[TE];
+        floatx4 bv = ld4(M.bv2p + 4 * g);
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) {
+            wfp[cc] = ld4(M.bf2 + cc * 16 + 4 * g);
+            wv[cc] = ld4(M.v2p + (int64_t)col * E + cc * 16 + 4 * g);
+#pragma unroll
+            for (int kc = 0; kc < T1H; ++kc) wf[cc][kc] = ld4(M.f2 + (int64_t)(cc * 16 + col) * HE + kc * 16 + 4 * g);
+        }
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc)
+#pragma unroll
+            for (int kc = 0; kc < T1H; ++kc) wfp[cc] = mfma_chunk(wf[cc][kc], l1[OWF + kc], wfp[cc]);
+#pragma unroll
+        for (int kc = 0; kc < TE; ++kc) bv = mfma_chunk(wv[kc], l1[OVH + kc], bv);
+        v = __shfl(bv[0], col);
+    }
+
+    // The Q-dependent half: the mixing with hyper()'s outputs (b1 = layer-1 tiles OB1..), forward()'s order.
+    __device__ static float mix(int N, const float* qrow, const floatx4 (&b1)[TE], const floatx4 (&w1p)[NMAX][TE],
+                                const floatx4 (&wfp)[TE], float v, floatx4 (&pre)[TE], floatx4 (&hid)[TE]) {
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) pre[cc] = b1[cc];
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) {
+            if (n >= N) break;
+            const float qn = qrow[n];
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pre[cc][q] += qn * fabsf(w1p[n][cc][q]);
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                hid[cc][q] = pre[cc][q] > 0.f ? pre[cc][q] : expm1f(pre[cc][q]);
+                part += hid[cc][q] * fabsf(wfp[cc][q]);
+            }
+        }
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        return part + v;
+    }
+
     __device__ static float forward(const MixPtrs& M, const MixPack& mp, int S, int N, const float* s, const float* qrow,
                                     floatx4 (&l1)[L1T], floatx4 (&pre)[TE], floatx4 (&hid)[TE], floatx4 (&wfp)[TE],
                                     floatx4 (&w1p)[NMAX][TE], int lane) {
@@ -1113,6 +1202,220 @@ __global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtr
     }
     // ---- dQ per agent row (t-major) and its one-hot expansion for dW2 ----
     if (valid && g == 0) {
+        for (int n = 0; n < N; ++n) {
+            const int r = b * N + n;
+            o.dq[(int64_t)t * c.R + r] = dq[n];
+            const int a = (int)bt.actions[(bslot(bt, b) * bt.T1 + t) * N + n];
+            o.d2[((int64_t)t * c.R + r) * c.A + a] = dq[n];
+        }
+    }
+}
+
+// ================================================================================================
+// Split mixer (default for the FAST shapes): the QMixer's hypernetworks read only the state (qmix.py:41-52: hyper_w_1,
+// hyper_b_1, hyper_w_final, V), not the agent network, so their forward -- about two thirds of mix_td's matrix work --
+// runs in mix_pre_kernel on a second stream while the agent recurrence runs (run_train). Per (b, t) row it stores the
+// pre-abs hyper_w_1 outputs of every agent, the pre-abs hyper_w_final outputs, hyper_b_1 and V: online on s_t, target
+// on s_{t+1}; the online net also stores its layer-1 activations and the state row for the weight gradients.
+// mix_td2_kernel then gathers the Qs, mixes (MixerPF::mix), forms the TD error and runs the mixer backward exactly as
+// mix_td_kernel does. Same operations in the same order: bit-identical to mix_td_kernel<.., true>.
+struct HypOut {
+    float *on, *tg;  // [RM][hs]: w1p [N*E] | wfp [E] | b1 [E] | v (padded to 4)
+    float *la, *srow;
+    int hs;
+};
+
+template <int HE, int E>
+__global__ void __launch_bounds__(128) mix_pre_kernel(LCfg c, MlgBatch bt, MixPtrs Mon, MixPtrs Mtg, MixPack mp,
+                                                      HypOut o) {
+    using Mx = Mixer<HE, E>;
+    using MP = MixerPF<HE, E, 4, MIXPF_N>;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, g = lane >> 4;
+    const bool tgt = wv == 0;  // wave 0: target net on s_{t+1}; wave 1: online net on s_t
+    const int rm = blockIdx.x * 16 + col;
+    const int Tm = c.T - 1;
+    const bool valid = rm < c.RM;
+    const int b = valid ? rm / Tm : 0, t = valid ? rm % Tm : 0;
+    const int N = c.N, S = c.S, NE = N * E, L1 = 2 * HE + 2 * E;
+    const float* s = valid ? bt.state + (bslot(bt, b) * bt.T1 + t + (tgt ? 1 : 0)) * S : nullptr;
+    floatx4 l1[Mx::L1T], w1p[MIXPF_N][Mx::TE], wfp[Mx::TE];
+    float v;
+    MP::hyper(tgt ? Mtg : Mon, mp, S, N, s, l1, w1p, wfp, v, lane);
+    if (!valid) return;
+    float* h = (tgt ? o.tg : o.on) + (int64_t)rm * o.hs;
+#pragma unroll
+    for (int n = 0; n < MIXPF_N; ++n) {
+        if (n >= N) break;
+#pragma unroll
+        for (int cc = 0; cc < Mx::TE; ++cc) *reinterpret_cast<floatx4*>(h + n * E + cc * 16 + 4 * g) = w1p[n][cc];
+    }
+#pragma unroll
+    for (int cc = 0; cc < Mx::TE; ++cc) {
+        *reinterpret_cast<floatx4*>(h + NE + cc * 16 + 4 * g) = wfp[cc];
+        *reinterpret_cast<floatx4*>(h + NE + E + cc * 16 + 4 * g) = l1[Mx::OB1 + cc];
+    }
+    if (g == 0) h[NE + 2 * E] = v;
+    if (!tgt) {
+        float* la = o.la + (int64_t)rm * L1;
+#pragma unroll
+        for (int mt = 0; mt < Mx::L1T; ++mt) *reinterpret_cast<floatx4*>(la + mt * 16 + 4 * g) = l1[mt];
+        if (g == 0)
+            for (int k = 0; k < S; ++k) o.srow[(int64_t)rm * S + k] = s[k];
+    }
+}
+
+template <int HE, int E>
+__global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPtrs Mon, const float* __restrict__ mac,
+                                                      const float* __restrict__ tmac, const float* __restrict__ msum_p,
+                                                      HypOut hy, MixOut o) {
+    using Mx = Mixer<HE, E>;
+    using MP = MixerPF<HE, E, 4, MIXPF_N>;
+    constexpr int TE = Mx::TE, T1H = Mx::T1H;
+    __shared__ float tgt_sh[16];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, g = lane >> 4;
+    const int rm = blockIdx.x * 16 + col;
+    const int Tm = c.T - 1;
+    const bool valid = rm < c.RM;
+    const int b = valid ? rm / Tm : 0, t = valid ? rm % Tm : 0;
+    const int N = c.N, NE = N * E, L1 = 2 * HE + 2 * E;
+    // this lane's hypernet outputs (rows past RM read row 0: finite, and their results are never stored)
+    const float* h = (wv == 0 ? hy.tg : hy.on) + (int64_t)(valid ? rm : 0) * hy.hs;
+    floatx4 w1c[MIXPF_N][TE], wfp[TE], b1[TE];
+#pragma unroll
+    for (int n = 0; n < MIXPF_N; ++n) {
+        if (n >= N) break;
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) w1c[n][cc] = ld4(h + n * E + cc * 16 + 4 * g);
+    }
+#pragma unroll
+    for (int cc = 0; cc < TE; ++cc) {
+        wfp[cc] = ld4(h + NE + cc * 16 + 4 * g);
+        b1[cc] = ld4(h + NE + E + cc * 16 + 4 * g);
+    }
+    const float vv = h[NE + 2 * E];
+    float cq[MAXN], tq[MAXN];
+    for (int n = 0; n < N; ++n) cq[n] = tq[n] = 0.f;
+    if (valid) gather_q_pf<MIXPF_A>(c, bt, mac, tmac, b, t, cq, tq);
+    floatx4 pre[TE], hid[TE];
+    if (wv == 0) {
+        const float tv = MP::mix(N, tq, b1, w1c, wfp, vv, pre, hid);
+        if (g == 0) tgt_sh[col] = tv;
+    }
+    const float m = (valid && t < t_eff(msum_p) - 1) ? mask_at(bt, b, t) : 0.f;  // reference truncation
+    const float rwd = valid ? bt.reward[bslot(bt, b) * bt.T1 + t] : 0.f;
+    const float term = valid ? (float)bt.terminated[bslot(bt, b) * bt.T1 + t] : 0.f;
+    const float msum = msum_p[0];
+    float qtot = 0.f;
+    if (wv == 1) qtot = MP::mix(N, cq, b1, w1c, wfp, vv, pre, hid);
+    __syncthreads();
+    if (wv == 0) return;
+    const float tgt = tgt_sh[col];
+    const float y = rwd + c.gamma * (1.f - term) * tgt;  // q_learner.py:86
+    const float mtd = (qtot - y) * m;                     // :89-95
+    const float dy = 2.f * mtd * m / msum;                // d loss / d q_tot
+    {
+        float p0 = g == 0 ? mtd * mtd : 0.f, p1 = g == 0 ? fabsf(mtd) : 0.f;
+        float p2 = g == 0 ? qtot * m : 0.f, p3 = g == 0 ? y * m : 0.f;
+        p0 = row_sum16(p0);
+        p1 = row_sum16(p1);
+        p2 = row_sum16(p2);
+        p3 = row_sum16(p3);
+        if (lane == 0) {
+            float* pp = o.part + (int64_t)blockIdx.x * 4;
+            pp[0] = p0;
+            pp[1] = p1;
+            pp[2] = p2;
+            pp[3] = p3;
+        }
+    }
+    // ---- QMixer backward (autograd of qmix.py:41-59), as mix_td_kernel ----
+    floatx4 dpre[TE], dwf[TE];
+#pragma unroll
+    for (int cc = 0; cc < TE; ++cc) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float dh = dy * fabsf(wfp[cc][q]);
+            const float sg = wfp[cc][q] > 0.f ? 1.f : (wfp[cc][q] < 0.f ? -1.f : 0.f);
+            dwf[cc][q] = dy * hid[cc][q] * sg;
+            dpre[cc][q] = pre[cc][q] > 0.f ? dh : dh * (hid[cc][q] + 1.f);
+        }
+    }
+    floatx4 dw1h[T1H];
+#pragma unroll
+    for (int mt = 0; mt < T1H; ++mt) dw1h[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float dq[MAXN];
+    for (int n = 0; n < N; ++n) {
+        float part = 0.f;
+        floatx4 aT[TE][T1H];
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc)
+#pragma unroll
+            for (int mt = 0; mt < T1H; ++mt)
+                aT[cc][mt] = ld4(Mon.a2T + (int64_t)(mt * 16 + col) * NE + n * E + cc * 16 + 4 * g);
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) {
+            floatx4 wp = w1c[0][cc];  // w1c[n][cc] without dynamic register indexing
+#pragma unroll
+            for (int k = 1; k < MIXPF_N; ++k)
+                if (k == n) wp = w1c[k][cc];
+            floatx4 dlt;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                part += fabsf(wp[q]) * dpre[cc][q];
+                const float sg = wp[q] > 0.f ? 1.f : (wp[q] < 0.f ? -1.f : 0.f);
+                dlt[q] = cq[n] * dpre[cc][q] * sg;
+            }
+            if (valid) *reinterpret_cast<floatx4*>(o.da2 + (int64_t)rm * NE + n * E + cc * 16 + 4 * g) = dlt;
+#pragma unroll
+            for (int mt = 0; mt < T1H; ++mt) dw1h[mt] = mfma_chunk(aT[cc][mt], dlt, dw1h[mt]);
+        }
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        dq[n] = part;
+    }
+    floatx4 dwfh[T1H];
+#pragma unroll
+    for (int mt = 0; mt < T1H; ++mt) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc)
+            acc = mfma_chunk(ld4(Mon.f2T + (int64_t)(mt * 16 + col) * E + cc * 16 + 4 * g), dwf[cc], acc);
+        dwfh[mt] = acc;
+    }
+    if (valid) {
+        // layer-1 activations (stored by mix_pre_kernel) for the ReLU masks
+        const float* la = hy.la + (int64_t)rm * L1;
+        float* d1 = o.d1 + (int64_t)rm * L1;
+#pragma unroll
+        for (int mt = 0; mt < T1H; ++mt) {  // w1h
+            const floatx4 l = ld4(la + (Mx::OW1 + mt) * 16 + 4 * g);
+            floatx4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = l[q] > 0.f ? dw1h[mt][q] : 0.f;
+            *reinterpret_cast<floatx4*>(d1 + mt * 16 + 4 * g) = v;
+        }
+#pragma unroll
+        for (int mt = 0; mt < T1H; ++mt) {  // wfh
+            const floatx4 l = ld4(la + (Mx::OWF + mt) * 16 + 4 * g);
+            floatx4 acc = dwfh[mt];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = l[q] > 0.f ? acc[q] : 0.f;
+            *reinterpret_cast<floatx4*>(d1 + HE + mt * 16 + 4 * g) = acc;
+        }
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) {  // b1, vh
+            *reinterpret_cast<floatx4*>(d1 + 2 * HE + cc * 16 + 4 * g) = dpre[cc];
+            const floatx4 wv = ld4(Mon.v2p + cc * 16 + 4 * g);
+            const floatx4 l = ld4(la + (Mx::OVH + cc) * 16 + 4 * g);
+            floatx4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = l[q] > 0.f ? dy * wv[q] : 0.f;
+            *reinterpret_cast<floatx4*>(d1 + 2 * HE + E + cc * 16 + 4 * g) = v;
+            *reinterpret_cast<floatx4*>(o.df2 + (int64_t)rm * E + cc * 16 + 4 * g) = dwf[cc];
+        }
+        if (g == 0) o.dv2[rm] = dy;
+    }
+    if (valid && g == 0) {  // dQ per agent row (t-major) and its one-hot expansion for dW2
         for (int n = 0; n < N; ++n) {
             const int r = b * N + n;
             o.dq[(int64_t)t * c.R + r] = dq[n];
@@ -1546,6 +1849,9 @@ Plan make_plan(const MlgLearnerCfg* cfg, int T1) {
     w.da2 = take(RM * c.N * c.E);
     w.df2 = take(RM * c.E);
     w.dv2 = take(RM);
+    w.hyp_stride = c.mixer == 2 ? (int)a4((int64_t)c.N * c.E + 2 * c.E + 1) : 0;  // mix_pre_kernel rows (HypOut)
+    w.hyp_on = take(RM * w.hyp_stride);
+    w.hyp_tg = take(RM * w.hyp_stride);
     w.n_mix_tiles = (int)((RM + 15) / 16);
     w.part = take((int64_t)w.n_mix_tiles * 4);
     w.msum = take(4);
@@ -1592,6 +1898,27 @@ WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     *slab_floats = mlg::layout_bjobs(J, n_tasks, n_red, &slab_part);  // slab partials + per-block norm partials
     p.w.nrm = p.w.slab + slab_part;
     return J;
+}
+
+// Second stream of the learner (one per device, created on first use, process lifetime) with the two events that
+// fork it from and join it back into the caller's stream.
+struct AuxStream {
+    hipStream_t s = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+AuxStream* aux_stream() {
+    static std::mutex mu;
+    static AuxStream per_dev[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    AuxStream& a = per_dev[dev];
+    if (!a.s) {
+        if (hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        for (auto& e : a.ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    }
+    return &a;
 }
 
 template <int H>
@@ -1670,6 +1997,23 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     }
     const int ntiles = (c.R + 15) / 16;
     const int threads = (c.H / 16) * 64;
+    // split mixer: the hypernetwork forward on a second stream, concurrent with the agent network (mix_pre_kernel)
+    const bool fast_mix = p.mp.Sp <= 64 && c.N <= MIXPF_N && c.A <= MIXPF_A && !getenv("MLG_MIX_GENERIC");
+    // opt-in (MLG_MIX_SPLIT=1): measured slower in the full bench (1.57-1.62 vs 1.33 ms per iteration: the
+    // cross-stream fork / join stalls the pipelined host loop), so the one-kernel mix_td stays the default
+    static const bool split_env = getenv("MLG_MIX_SPLIT") != nullptr;
+    const bool split_mix = c.mixer == 2 && fast_mix && split_env;
+    HypOut hy{ws + p.w.hyp_on, ws + p.w.hyp_tg, ws + p.w.l1act, ws + p.w.srow, p.w.hyp_stride};
+    AuxStream* aux = nullptr;
+    if (split_mix) {
+        aux = aux_stream();
+        if (!aux) return mlg::fail("qlearner_train: auxiliary stream: %s", hipGetErrorString(hipGetLastError()));
+        (void)hipEventRecord(aux->ev[0], s);
+        (void)hipStreamWaitEvent(aux->s, aux->ev[0], 0);
+        hipLaunchKernelGGL((mix_pre_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, aux->s, c, bt, Mon, Mtg, p.mp,
+                           hy);
+        (void)hipEventRecord(aux->ev[1], aux->s);
+    }
     hipLaunchKernelGGL((agent_in_kernel<H>), dim3(ntiles, c.T, 2), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                        ws + p.w.p_tg, ws + p.w.in, ws + p.w.x, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.msum);
     static const bool rec16 = getenv("MLG_LEARNER_REC16") != nullptr;  // A/B switch: the 16-row tile recurrence
@@ -1685,7 +2029,11 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
                        ws + p.w.p_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum);
     MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
               ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
-    if (p.mp.Sp <= 64 && c.N <= MIXPF_N && c.A <= MIXPF_A && !getenv("MLG_MIX_GENERIC"))
+    if (split_mix) {
+        (void)hipStreamWaitEvent(s, aux->ev[1], 0);
+        hipLaunchKernelGGL((mix_td2_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, ws + p.w.mac,
+                           ws + p.w.tmac, ws + p.w.msum, hy, mo);
+    } else if (fast_mix)
         hipLaunchKernelGGL((mix_td_kernel<64, 32, true>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, Mtg, p.mp,
                            ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
     else

@@ -168,6 +168,29 @@ __device__ __forceinline__ float rows_sum_transpose4(float x0, float x1, float x
     return __uint_as_float(s[0]) + __uint_as_float(s[1]);
 }
 
+// Inclusive prefix sum over groups of W lanes (W = 8 or 16, groups inside the 16-lane rows) on DPP row shifts --
+// VALU moves -- instead of __shfl_up, which compiles to a chain of ds_bpermute LDS round trips. A lane whose shift
+// source lies below its group's first lane adds 0.
+template <int D>
+__device__ __forceinline__ int dpp_row_shr(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x110 + D, 0xF, 0xF, false);
+}
+template <int W>
+__device__ __forceinline__ int group_incl_scan(int c, int lane) {
+    const int l = lane & (W - 1);
+    int v = dpp_row_shr<1>(c);
+    c += l >= 1 ? v : 0;
+    v = dpp_row_shr<2>(c);
+    c += l >= 2 ? v : 0;
+    v = dpp_row_shr<4>(c);
+    c += l >= 4 ? v : 0;
+    if constexpr (W > 8) {
+        v = dpp_row_shr<8>(c);
+        c += l >= 8 ? v : 0;
+    }
+    return c;
+}
+
 // Raw buffer access with a per-lane byte offset vo and a wave-uniform (SGPR) byte offset so.
 __device__ __forceinline__ floatx4 ld4_rs(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
     return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));

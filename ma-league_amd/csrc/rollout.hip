@@ -38,6 +38,9 @@ struct Stamps {
 #ifdef MLG_STAMPS_LOWRUN
         on = nrun <= MLG_STAMPS_LOWRUN;
 #endif
+#ifdef MLG_STAMPS_MINRUN  // phase slots count only the steps with >= k running envs (full-occupancy breakdown)
+        on = nrun >= MLG_STAMPS_MINRUN;
+#endif
 #ifdef MLG_STAMPS_TIMELINE
         on = nrun == 1 && !seen;
         seen = seen || on;
@@ -144,6 +147,19 @@ __host__ __device__ constexpr int64_t ro_take(int64_t& o, int64_t n) {
     const int64_t v = o;
     o += mlg_align4(n);
     return v;
+}
+
+// The fields the v2-structure env lanes use (status, episode, slot, pending / previous actions); the others alias
+// offset 0 and are never dereferenced by those kernels.
+__host__ __device__ constexpr RoEnvLds make_env_lds_v2(int64_t& o, int n_agents, int re) {
+    RoEnvLds r{};
+    r.spec = ro_take(o, (int64_t)(sizeof(SpecShared) / 4));
+    r.pact = ro_take(o, (int64_t)re * n_agents);
+    r.prev = ro_take(o, (int64_t)re * n_agents);
+    r.status = ro_take(o, re);
+    r.episode = ro_take(o, re);
+    r.slot = ro_take(o, re);
+    return r;
 }
 
 __host__ __device__ constexpr RoEnvLds make_env_lds(int64_t& o, int U, int n_agents, int re = RE) {
@@ -901,8 +917,8 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
 // Env phase: half-wave per env, lane per unit (v2 env above); wave w steps envs 2w and 2w + 1.
 // Barriers per step: A|B, B|C, C|env, env|A.
 struct RolloutLds2 {
-    int32_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, rmap, total;
-    int ldo, ldh, nhb;  // nhb: hidden-state buffers (2: double buffered by step parity; 1: v6, see below)
+    int32_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, rmap, hpl, total;
+    int ldo, ldh, nhb;  // nhb: hidden-state buffers (2: double buffered by step parity; 1: v6 / v7, see below)
     int xpl;            // v7: x held as three bf16 planes per row, row stride XPL_STRIDE words (0: fp32 rows)
     int rms;            // v7: words per wave row map
     RoEnvLds env;
@@ -930,22 +946,29 @@ __host__ __device__ constexpr RolloutLds2 make_rollout_lds2(const AgentLayout& L
     r.b2 = ro_take(o, L.Ap);
     r.gb = ro_take(o, 4 * L.H);
     const int rows = rew * N, rows16 = (rows + 15) / 16 * 16;
+    // v7: one fp32 hidden-state buffer (updated in place: each lane reads and writes only its own two features of a
+    // row, the GRU's h operand comes from the h planes below), so nhb is 1 without v6's aliasing.
+    if (xpl) nhb = 1;
     // nhb == 1 (v6): the obs rows double as the compact h' rows between the GRU and fc2 phases
-    const int64_t nobs = (int64_t)rows * r.ldo, nhx = nhb == 1 ? (int64_t)rows16 * r.ldh : 0;
+    const int64_t nobs = (int64_t)rows * r.ldo, nhx = (nhb == 1 && !xpl) ? (int64_t)rows16 * r.ldh : 0;
     r.obs = ro_take(o, nobs > nhx ? nobs : nhx);
     r.avail = ro_take(o, (int64_t)rows * 2);  // uint64 avail mask per agent row
     r.xb = ro_take(o, (int64_t)rows16 * (xpl ? XPL_STRIDE : r.ldh));
+    // v7: h' of step t as three bf16 planes per compact row of step t (split once, by the fc2 phase), the GRU's h
+    // operand at step t + 1 (x-plane row layout)
+    r.hpl = ro_take(o, xpl ? (int64_t)rows16 * XPL_STRIDE : 0);
     r.hsz = mlg_align4((int64_t)rows * r.ldh);
     r.nhb = nhb;
     r.hb = ro_take(o, nhb * r.hsz);
-    r.pairtab = ro_take(o, (int64_t)N * U);
-    r.avtab = ro_take(o, (int64_t)N * L.A);
+    // index tables: v7 computes them arithmetically (no LDS)
+    r.pairtab = ro_take(o, xpl ? 0 : (int64_t)N * U);
+    r.avtab = ro_take(o, xpl ? 0 : (int64_t)N * L.A);
     r.pk = ro_take(o, (int64_t)rew * 32);
     r.act = ro_take(o, (int64_t)rew * 32);
     r.am = ro_take(o, 16);
     r.rms = rows16 + 16;
     r.rmap = ro_take(o, 8 * r.rms);  // v7: one compact-row map per wave
-    r.env = make_env_lds(o, U, N, rew < RE ? rew : RE);
+    r.env = xpl ? make_env_lds_v2(o, N, rew < RE ? rew : RE) : make_env_lds(o, U, N, rew < RE ? rew : RE);
     r.total = o;
     return r;
 }
@@ -994,8 +1017,12 @@ __device__ void v2_prologue(const MlgEnvSpec& spec, const AgentLayout& L, const 
     rows_cp(L.brz, lay.gb, 1, 2 * H, 2 * H);
     rows_cp(L.bih + 2 * H, lay.gb + 2 * H, 1, H, H);
     rows_cp(L.bhh + 2 * H, lay.gb + 3 * H, 1, H, H);
-    for (int k = tid; k < N * U; k += nthr) smem[lay.pairtab + k] = ((k / U) << 8) | (k % U);
-    for (int k = tid; k < N * A; k += nthr) smem[lay.avtab + k] = ((k / A) << 8) | (k % A);
+    if (!lay.xpl) {
+        for (int k = tid; k < N * U; k += nthr) smem[lay.pairtab + k] = ((k / U) << 8) | (k % U);
+        for (int k = tid; k < N * A; k += nthr) smem[lay.avtab + k] = ((k / A) << 8) | (k % A);
+    } else {  // v7: h planes of step -1 = 0 (h_0 = 0)
+        for (int64_t i = tid; i < (int64_t)(rows + 15) / 16 * 16 * XPL_STRIDE; i += nthr) fm[lay.hpl + i] = 0.f;
+    }
     __syncthreads();
 }
 
@@ -1061,12 +1088,7 @@ __device__ inline StepRows make_rows(const uint32_t* amask, int ebase, int ne, i
     s.amask = amask;
     s.ebase = ebase;
     const int l16 = lane & 15;
-    int c = l16 < ne ? __builtin_popcount(amask[ebase + l16]) : 0;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-        const int v = __shfl_up(c, d, 16);
-        if (l16 >= d) c += v;
-    }
+    int c = group_incl_scan<16>(l16 < ne ? __builtin_popcount(amask[ebase + l16]) : 0, lane);
 #pragma unroll
     for (int l = 0; l < 16; ++l) s.P[l] = __builtin_amdgcn_readlane(c, l);
     s.rows_run = s.P[15];
@@ -1148,23 +1170,32 @@ __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, floa
 // agent n << 1 | 1 (0 for tile padding). Lanes 0-15 (one per env) scatter their env's living agents after a
 // 16-lane scan of the agent counts; the wave reads its own table back (LDS is in order within a wave), so no
 // workgroup barrier and no SGPR-resident prefix array. Returns the tile count.
-__device__ __forceinline__ int rmap_er(int rm, int N) { return (rm >> 8) * N + ((rm >> 1) & 127); }
+// Row-map entry: bit 0 valid, bits 1-7 agent n, bits 8-15 env e, bits 16-23 (v7) the row's compact index at the
+// previous step (where its h' planes are, HPL).
+__device__ __forceinline__ int rmap_env(int rm) { return (rm >> 8) & 255; }
+__device__ __forceinline__ int rmap_er(int rm, int N) { return rmap_env(rm) * N + ((rm >> 1) & 127); }
+__device__ __forceinline__ int rmap_prev(int rm) { return (rm >> 16) & 255; }
 
-__device__ inline int make_rmap(const uint32_t* amask, int* wmap, int lane) {
+// m: amask[lane & 15]; m_prev / x_prev (lanes 0-15): the env's agent mask and exclusive row prefix of the previous
+// step (0 / 0 before the first: row 0 of the zeroed h planes), updated here. Rows only disappear between steps
+// (agents die, envs end), so a row's previous compact index is x_prev + the number of its env's earlier agents
+// in m_prev.
+__device__ inline int make_rmap(uint32_t m, int* wmap, int lane, uint32_t& m_prev, int& x_prev) {
     const int l16 = lane & 15;
-    const uint32_t m = amask[l16];
-    int c = __builtin_popcount(m);
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-        const int v = __shfl_up(c, d, 16);
-        if (l16 >= d) c += v;
-    }
+    int c = group_incl_scan<16>(__builtin_popcount(m), lane);
     const int rows = __builtin_amdgcn_readlane(c, 15);
+    const int x = c - __builtin_popcount(m);
     if (lane < 16) {
-        int p = c - __builtin_popcount(m);
-        for (uint32_t mm = m; mm; mm &= mm - 1) wmap[p++] = (lane << 8) | (__builtin_ctz(mm) << 1) | 1;
+        int p = x;
+        for (uint32_t mm = m; mm; mm &= mm - 1) {
+            const int n = __builtin_ctz(mm);
+            const int cp = x_prev + __builtin_popcount(m_prev & ((1u << n) - 1u));
+            wmap[p++] = (cp << 16) | (lane << 8) | (n << 1) | 1;
+        }
         wmap[rows + lane] = 0;  // padding rows of the last tile
     }
+    m_prev = m;
+    x_prev = x;
     return (rows + 15) >> 4;
 }
 
@@ -1211,6 +1242,86 @@ __device__ inline void ph_fc1_g8(const AgentLayout& L, const RolloutLds2& lay, f
             }
         }
     }
+}
+
+// v7 A for the static plan shapes: the wave's NU (tile, chunk j) units of ph_fc1_g8 as one straight-line block
+// (identical arithmetic per unit). ph_fc1_g8 walks its units one after another, each a chain of dependent LDS
+// round trips (row map -> previous action -> last-action column) feeding a 9-deep MFMA chain, then the split and
+// the x-plane stores: at full occupancy (3 units per wave) fc1 took 4.7 k cycles per step against ~0.4 k of
+// MFMA work. Here every LDS read of all units issues first, the chunk's W1 operands are read once (they do not
+// depend on the tile), and the units' MFMA chains interleave.
+template <int H, int KK, int NU>
+__device__ __forceinline__ void fc1_g8_units(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* rmap,
+                                             const int* prev, int j, int ti0, int dt, int t, int lane) {
+    const int col = lane & 15, g = lane >> 4, N = L.N, ldo = lay.ldo, ldh = lay.ldh;
+    int zero = 0;
+    asm volatile("" : "+s"(zero));
+    const float* lobs = fm + lay.obs;
+    int cr[NU], er[NU], n[NU];
+    bool valid[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        cr[u] = (ti0 + u * dt) * 16 + col;
+        const int rm = rmap[cr[u]];
+        valid[u] = rm & 1;
+        n[u] = (rm >> 1) & 127;
+        er[u] = rmap_er(rm, N);
+    }
+    const bf16x8* orow[NU];
+    int pa[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        orow[u] = reinterpret_cast<const bf16x8*>(lobs + er[u] * ldo) + g;
+        pa[u] = (valid[u] && t > 0) ? prev[er[u]] : -1;
+    }
+    const bf16x8* wrow = reinterpret_cast<const bf16x8*>(fm + lay.w1o + zero + (j * 16 + col) * ldo) + g;
+    const int pl = L.H * ldo / 4;  // plane stride in bf16x8 units
+    const floatx4 b1 = ld4(fm + lay.b1 + zero + j * 16 + 4 * g);
+    floatx4 acc[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        acc[u] = b1;
+        if (L.last_action && pa[u] >= 0) acc[u] += ld4(fm + lay.w1a + pa[u] * ldh + j * 16 + 4 * g);
+        if (L.agent_id) acc[u] += ld4(fm + lay.w1n + n[u] * ldh + j * 16 + 4 * g);
+    }
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {  // operands per K step (register budget: the kernel runs at 2 waves / SIMD)
+        bf16x8 w[3], b[NU];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) w[p] = wrow[p * pl + 4 * kk];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) b[u] = orow[u][4 * kk];
+#pragma unroll
+        for (int p = 2; p >= 0; --p)
+#pragma unroll
+            for (int u = 0; u < NU; ++u) acc[u] = mfma_bf16(w[p], b[u], acc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        unsigned int* xr = reinterpret_cast<unsigned int*>(fm + lay.xb + cr[u] * XPL_STRIDE) + (j * 16 + 4 * g) / 2;
+        float v[4] = {fmaxf(acc[u][0], 0.f), fmaxf(acc[u][1], 0.f), fmaxf(acc[u][2], 0.f), fmaxf(acc[u][3], 0.f)};
+#pragma unroll
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            const unsigned int a = cvt_pk_bf16(v[0], v[1]), c = cvt_pk_bf16(v[2], v[3]);
+            *reinterpret_cast<uint2*>(xr + lvl * 32) = make_uint2(a, c);
+            if (lvl < 2) {
+                v[0] -= __uint_as_float(a << 16);
+                v[1] -= __uint_as_float(a & 0xFFFF0000u);
+                v[2] -= __uint_as_float(c << 16);
+                v[3] -= __uint_as_float(c & 0xFFFF0000u);
+            }
+        }
+    }
+}
+
+// nu (wave-uniform, 0..MU) units of fc1_g8_units: tiles ti0, ti0 + dt, ...
+template <int H, int KK, int MU>
+__device__ __forceinline__ void fc1_g8_static(const AgentLayout& L, const RolloutLds2& lay, float* fm, const int* rmap,
+                                              const int* prev, int nu, int j, int ti0, int dt, int t, int lane) {
+    if (nu == MU)
+        fc1_g8_units<H, KK, MU>(L, lay, fm, rmap, prev, j, ti0, dt, t, lane);
+    else if constexpr (MU > 1)
+        fc1_g8_static<H, KK, MU - 1>(L, lay, fm, rmap, prev, nu, j, ti0, dt, t, lane);
 }
 
 // ---- v7 GRU: fp32 products emulated on the bf16 matrix cores (split-bf16 "bf16x6") -------------------------
@@ -1263,8 +1374,8 @@ __device__ inline void load_gru_g8(GruG8& W, const float* __restrict__ P, const 
 // B: GRU cell of every tile for the wave's 8 features -> h' (env-row hidden state). x comes as bf16 planes from
 // fc1 (split once), h is split here; the compact-row -> env-row map was stored by fc1.
 template <int H>
-__device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* fm, const int* rmap, const float* hc,
-                                 float* hn, int tiles, int N, int w, int lane) {
+__device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* fm, const int* rmap, float* hb,
+                                 int tiles, int N, int w, int lane) {
     const int col = lane & 15, g = lane >> 4, ldh = lay.ldh;
     const bool upper = lane >= 32;
     // this lane's two output features after the exchange: lower lanes 8w+4g+{0,1}, upper 8w+4(g-2)+2+{0,1}
@@ -1275,7 +1386,8 @@ __device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* 
         const bool valid = rm & 1;
         const int er = rmap_er(rm, N);
         const bf16x8* xp = reinterpret_cast<const bf16x8*>(fm + lay.xb + (int64_t)cr * XPL_STRIDE) + g;
-        const float* hr = hc + (int64_t)er * ldh + 8 * g;
+        // h of the previous step, split once by that step's fc2 phase (HPL row = the row's previous compact index)
+        const bf16x8* hp = reinterpret_cast<const bf16x8*>(fm + lay.hpl + (int64_t)rmap_prev(rm) * XPL_STRIDE) + g;
         floatx4 arz = ld4(fm + W.rz_bias), arzh = floatx4{0.f, 0.f, 0.f, 0.f};
         floatx4 anx = ld4(fm + W.in_bias), anh = ld4(fm + W.hn_bias);
 #pragma unroll
@@ -1283,7 +1395,9 @@ __device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* 
             Split3 xs;
 #pragma unroll
             for (int p = 0; p < 3; ++p) xs.p[p] = xp[p * 8 + 4 * kk];  // plane p: +128 B; K step kk: +64 B
-            const Split3 hs = split3(ld4(hr + 32 * kk), ld4(hr + 32 * kk + 4));
+            Split3 hs;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) hs.p[p] = hp[p * 8 + 4 * kk];
             arz = mfma_x6(W.rzi[kk], xs, arz);
             anx = mfma_x6(W.n[kk], xs, anx);
             arzh = mfma_x6(W.rzh[kk], hs, arzh);
@@ -1311,7 +1425,7 @@ __device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* 
             nh0 = upper ? anh[2] : __uint_as_float(s0[1]);
             nh1 = upper ? anh[3] : __uint_as_float(s1[1]);
         }
-        const float2 ho = *reinterpret_cast<const float2*>(hc + (int64_t)er * ldh + fo);
+        const float2 ho = *reinterpret_cast<const float2*>(hb + (int64_t)er * ldh + fo);
         float2 hv;
         {
             const float rg = fast_sigmoid(r0), zg = fast_sigmoid(z0);
@@ -1323,7 +1437,7 @@ __device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* 
             const float ng = fast_tanh(ni1 + rg * nh1);
             hv.y = ng + zg * (ho.y - ng);
         }
-        if (valid) *reinterpret_cast<float2*>(hn + (int64_t)er * ldh + fo) = hv;
+        if (valid) *reinterpret_cast<float2*>(hb + (int64_t)er * ldh + fo) = hv;  // in place: own features only
     }
 }
 
@@ -1396,7 +1510,7 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
 __device__ __forceinline__ int eps_coin(const MlgEnvSpec& spec, const RoEnv& R, const int* rmap, int ti, int e0, int t,
                                         float eps, int test_mode, int lane) {
     const int rm = rmap[ti * 16 + (lane & 15)];
-    const int e = rm >> 8, n = (rm >> 1) & 127;
+    const int e = rmap_env(rm), n = (rm >> 1) & 127;
     const uint64_t key = mlg_env_key(spec.seed, e0 + e);
     return !test_mode && eps > 0.f &&
            mlg_u01(mlg_rng(key, mlg_ctr(R.episode[e], (uint32_t)t, MLG_PURPOSE_EPS, (uint32_t)n))) < eps;
@@ -1418,9 +1532,32 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
         const int cr = ti * 16 + col;
         const int rm = rmap[cr];
         const bool valid = rm & 1;
-        const int e = rm >> 8, n = (rm >> 1) & 127, er = e * N + n;
+        const int e = rmap_env(rm), n = (rm >> 1) & 127, er = e * N + n;
         const uint64_t avm = lavm[er];
         const float* hr = hn + er * ldh + 4 * g;
+        if (valid) {  // h' as three bf16 planes at this compact row: the GRU's h operand of the next step (HPL)
+            unsigned int* hq = reinterpret_cast<unsigned int*>(fm + lay.hpl + cr * XPL_STRIDE) + 2 * g;
+#pragma unroll
+            for (int kc = 0; kc < HC; ++kc) {  // features 16 kc + 4 g .. + 3
+                float v[4];
+                const floatx4 hv = ld4(hr + kc * 16);
+                v[0] = hv[0];
+                v[1] = hv[1];
+                v[2] = hv[2];
+                v[3] = hv[3];
+#pragma unroll
+                for (int lvl = 0; lvl < 3; ++lvl) {  // split3's pieces (round to nearest, exact remainders)
+                    const unsigned int a = cvt_pk_bf16(v[0], v[1]), c = cvt_pk_bf16(v[2], v[3]);
+                    *reinterpret_cast<uint2*>(hq + lvl * 32 + 8 * kc) = make_uint2(a, c);
+                    if (lvl < 2) {
+                        v[0] -= __uint_as_float(a << 16);
+                        v[1] -= __uint_as_float(a & 0xFFFF0000u);
+                        v[2] -= __uint_as_float(c << 16);
+                        v[3] -= __uint_as_float(c & 0xFFFF0000u);
+                    }
+                }
+            }
+        }
         ArgmaxState as{-INFINITY, 1 << 30};
         // epsilon-greedy coin (action_selectors.py:44-62, counter RNG of spec §3.7): computed by every lane with no
         // branch, so it issues between the fc2 MFMAs; only the rare exploring lanes take the branch below
@@ -1779,7 +1916,7 @@ __device__ __forceinline__ MlgBatch split_batch_sgprs(MlgBatch b) {
     return b;
 }
 
-template <int H, bool G8>
+template <int H, bool G8, int SN = 0, int SU = 0>
 __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const MlgEnvState& st, const AgentLayout& L,
                                                 const float* __restrict__ P, const MlgBatch& bt_arg, const MlgRunInfo& info,
                                                 float eps, int test_mode, const RolloutLds2& lay, int DU, int DN,
@@ -1788,7 +1925,7 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
     constexpr int HC = H / 16, NW = 8, REW = 16, G = NW / HC;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     float* fm = reinterpret_cast<float*>(smem);
-    const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
+    const int N = spec.n_agents, lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hl = lane & 31;
     const int e0 = blockIdx.x * REW, T1 = bt.T1;
     v2_prologue(spec, L, P, lay, smem, REW * N);
     const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info, DU, DN, DA, SD);
@@ -1802,21 +1939,33 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
     else
         load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
     __syncthreads();
+#ifdef MLG_PRIO  // A/B: static priority for the second-dispatched half of the workgroup (MI355X_MICROARCH.md)
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     Stamps sp;
     sp.init();
     uint64_t rows_issued = 0;  // agent rows issued to the MFMA cell (incl. tile padding)
+    uint32_t m_prev = 0u;      // v7 row map of the previous step (make_rmap)
+    int x_prev = 0;
     for (int t = 0; t < T1; ++t) {
         const uint32_t run = (uint32_t)__ballot(lane < REW && C.R.status[lane & (REW - 1)] < 2);
         sp.step(t, __popc(run));
         if (run == 0) break;
-        const float* hc = fm + lay.hb + (t & 1) * lay.hsz;
-        float* hn = fm + lay.hb + ((t & 1) ^ 1) * lay.hsz;
+        // v7: one in-place buffer (nhb = 1); v2: double buffered by step parity
+        const float* hc = fm + lay.hb + (t & 1) * (lay.nhb - 1) * lay.hsz;
+        float* hn = fm + lay.hb + ((t & 1) ^ 1) * (lay.nhb - 1) * lay.hsz;
         StepRows SR;
         int tiles;
         int* wmap = smem + lay.rmap + wave * lay.rms;
         if constexpr (G8) {
-            tiles = make_rmap(C.amask, wmap, lane);
-            ph_fc1_g8<H>(L, lay, fm, wmap, C.R.prev, tiles, j, gi, G, t, lane);
+            tiles = make_rmap(C.amask[lane & 15], wmap, lane, m_prev, x_prev);
+#ifndef MLG_FC1_SERIAL  // A/B: the tile-by-tile fc1
+            if constexpr (SN > 0) {
+                const int nu = tiles > gi ? (tiles - gi + G - 1) / G : 0;
+                fc1_g8_static<H, (8 * SU + 31) / 32, (SN + G - 1) / G>(L, lay, fm, wmap, C.R.prev, nu, j, gi, G, t, lane);
+            } else
+#endif
+                ph_fc1_g8<H>(L, lay, fm, wmap, C.R.prev, tiles, j, gi, G, t, lane);
 #ifdef MLG_DUP_FC1  // timing ablation only: the phase twice (idempotent)
             ph_fc1_g8<H>(L, lay, fm, wmap, C.R.prev, tiles, j, gi, G, t, lane);
 #endif
@@ -1836,14 +1985,11 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         if constexpr (G8)
             if (wave < tiles) pre = eps_coin(spec, C.R, wmap, wave, e0, t, eps, test_mode, lane);
         if constexpr (G8)
-            ph_gru_g8<H>(W8, lay, fm, wmap, hc, hn, tiles, N, wave, lane);
+            ph_gru_g8<H>(W8, lay, fm, wmap, hn, tiles, N, wave, lane);
         else
             ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
-#ifdef MLG_DUP_GRU
-        if constexpr (G8)
-            ph_gru_g8<H>(W8, lay, fm, wmap, hc, hn, tiles, N, wave, lane);
-        else
-            ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
+#ifdef MLG_DUP_GRU  // v2 only (v7 updates h in place: a second pass would not be idempotent)
+        if constexpr (!G8) ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
 #endif
         sp.mark(1);
         lds_barrier();
@@ -1884,10 +2030,10 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
                                                            float eps, int test_mode, RolloutLds2 lay) {
     using S = StaticShape<H, G8, SN, SU>;
     if constexpr (S::on)
-        rollout_v2_body<H, G8>(spec, st, S::L, P, bt, info, eps, test_mode, S::lay, SU, SN, 5 + SU, true);
+        rollout_v2_body<H, G8, SN, SU>(spec, st, S::L, P, bt, info, eps, test_mode, S::lay, SU, SN, 5 + SU, true);
     else
         rollout_v2_body<H, G8>(spec, st, L, P, bt, info, eps, test_mode, lay, spec.U, spec.n_agents, spec.n_actions,
-                               false);
+                               G8);  // v7 layouts hold no index tables (arithmetic indices)
 }
 
 // ================================================================================================

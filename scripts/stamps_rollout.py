@@ -77,6 +77,12 @@ for g in range(grid):
 print("step cycles by running envs in the WG (mean, count):")
 for k in sorted(by):
     print(f"  nrun={k:2d} mean={np.mean(by[k]):8.0f} n={len(by[k])}")
+mr = int(os.environ.get("MINRUN", "0"))
+if mr:  # libmaleague built with -DMLG_STAMPS_MINRUN=mr: phase slots per counted step
+    nfull = (nrun >= mr).sum(1).mean()
+    print(f"steps with >= {mr} running envs per WG: {nfull:.1f}; per-step phase cycles (mean over waves):")
+    for k, n in enumerate(names):
+        print(f"  {n:22s} {a[:, :, k][valid].mean() / nfull:8.0f}")
 tot_wg = cyc[:, 1:].sum(1)
 slow = int(np.argmax(tot_wg))
 print("slowest WG", slow, "total", tot_wg[slow], "mean WG", tot_wg.mean())
