@@ -1373,42 +1373,58 @@ __device__ inline void load_gru_g8(GruG8& W, const float* __restrict__ P, const 
 
 // B: GRU cell of every tile for the wave's 8 features -> h' (env-row hidden state). x comes as bf16 planes from
 // fc1 (split once), h is split here; the compact-row -> env-row map was stored by fc1.
-template <int H>
-__device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* fm, const int* rmap, float* hb,
-                                 int tiles, int N, int w, int lane) {
+// NT (1 or 2) consecutive tiles of ph_gru_g8 with their MFMA chains interleaved (8 independent accumulators for
+// two tiles): one tile's operand loads and gate epilogue overlap the other's matrix work. Per tile the same
+// operations in the same order as the one-tile loop.
+template <int NT>
+__device__ __forceinline__ void gru_g8_tiles(const GruG8& W, const RolloutLds2& lay, float* fm, const int* rmap, float* hb,
+                                             int ti0, int N, int fo, int lane) {
     const int col = lane & 15, g = lane >> 4, ldh = lay.ldh;
     const bool upper = lane >= 32;
-    // this lane's two output features after the exchange: lower lanes 8w+4g+{0,1}, upper 8w+4(g-2)+2+{0,1}
-    const int fo = 8 * w + 4 * (g & 1) + (upper ? 2 : 0);
-    for (int ti = 0; ti < tiles; ++ti) {
-        const int cr = ti * 16 + col;
+    int er[NT];
+    bool valid[NT];
+    const bf16x8 *xp[NT], *hp[NT];
+    floatx4 arz[NT], arzh[NT], anx[NT], anh[NT];
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const int cr = (ti0 + u) * 16 + col;
         const int rm = rmap[cr];
-        const bool valid = rm & 1;
-        const int er = rmap_er(rm, N);
-        const bf16x8* xp = reinterpret_cast<const bf16x8*>(fm + lay.xb + (int64_t)cr * XPL_STRIDE) + g;
-        // h of the previous step, split once by that step's fc2 phase (HPL row = the row's previous compact index)
-        const bf16x8* hp = reinterpret_cast<const bf16x8*>(fm + lay.hpl + (int64_t)rmap_prev(rm) * XPL_STRIDE) + g;
-        floatx4 arz = ld4(fm + W.rz_bias), arzh = floatx4{0.f, 0.f, 0.f, 0.f};
-        floatx4 anx = ld4(fm + W.in_bias), anh = ld4(fm + W.hn_bias);
+        valid[u] = rm & 1;
+        er[u] = rmap_er(rm, N);
+        xp[u] = reinterpret_cast<const bf16x8*>(fm + lay.xb + (int64_t)cr * XPL_STRIDE) + g;
+        // h of the previous step, split once per step (hpl_split_tile; HPL row = the row's previous compact index)
+        hp[u] = reinterpret_cast<const bf16x8*>(fm + lay.hpl + (int64_t)rmap_prev(rm) * XPL_STRIDE) + g;
+        arz[u] = ld4(fm + W.rz_bias);
+        arzh[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+        anx[u] = ld4(fm + W.in_bias);
+        anh[u] = ld4(fm + W.hn_bias);
+    }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            Split3 xs;
+    for (int kk = 0; kk < 2; ++kk) {
+        Split3 xs[NT], hs[NT];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) xs.p[p] = xp[p * 8 + 4 * kk];  // plane p: +128 B; K step kk: +64 B
-            Split3 hs;
+        for (int u = 0; u < NT; ++u)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) hs.p[p] = hp[p * 8 + 4 * kk];
-            arz = mfma_x6(W.rzi[kk], xs, arz);
-            anx = mfma_x6(W.n[kk], xs, anx);
-            arzh = mfma_x6(W.rzh[kk], hs, arzh);
-            anh = mfma_x6(W.n[kk], hs, anh);
+            for (int p = 0; p < 3; ++p) {
+                xs[u].p[p] = xp[u][p * 8 + 4 * kk];  // plane p: +128 B; K step kk: +64 B
+                hs[u].p[p] = hp[u][p * 8 + 4 * kk];
+            }
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+            arz[u] = mfma_x6(W.rzi[kk], xs[u], arz[u]);
+            anx[u] = mfma_x6(W.n[kk], xs[u], anx[u]);
+            arzh[u] = mfma_x6(W.rzh[kk], hs[u], arzh[u]);
+            anh[u] = mfma_x6(W.n[kk], hs[u], anh[u]);
         }
-        arz += arzh;
+    }
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const floatx4 az = arz[u] + arzh[u];
         // lanes l < 32 hold r (rows 4g..) and W_in x; lanes l + 32 hold z and W_hn h of the same features
         float r0, r1, z0, z1;
         {
-            auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(arz[0]), __float_as_uint(arz[2]), false, false);
-            auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(arz[1]), __float_as_uint(arz[3]), false, false);
+            auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(az[0]), __float_as_uint(az[2]), false, false);
+            auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(az[1]), __float_as_uint(az[3]), false, false);
             r0 = __uint_as_float(s0[0]);
             z0 = __uint_as_float(s0[1]);
             r1 = __uint_as_float(s1[0]);
@@ -1416,16 +1432,16 @@ __device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* 
         }
         float ni0, ni1, nh0, nh1;
         {
-            auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(anh[0]), __float_as_uint(anx[2]), false, false);
-            auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(anh[1]), __float_as_uint(anx[3]), false, false);
+            auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(anh[u][0]), __float_as_uint(anx[u][2]), false, false);
+            auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(anh[u][1]), __float_as_uint(anx[u][3]), false, false);
             // lower: own anx[0..1] = W_in x, received (in the anx[2..3] slot) W_hn h; upper: received W_in x in the
             // anh[0..1] slot, own anh[2..3] = W_hn h
-            ni0 = upper ? __uint_as_float(s0[0]) : anx[0];
-            ni1 = upper ? __uint_as_float(s1[0]) : anx[1];
-            nh0 = upper ? anh[2] : __uint_as_float(s0[1]);
-            nh1 = upper ? anh[3] : __uint_as_float(s1[1]);
+            ni0 = upper ? __uint_as_float(s0[0]) : anx[u][0];
+            ni1 = upper ? __uint_as_float(s1[0]) : anx[u][1];
+            nh0 = upper ? anh[u][2] : __uint_as_float(s0[1]);
+            nh1 = upper ? anh[u][3] : __uint_as_float(s1[1]);
         }
-        const float2 ho = *reinterpret_cast<const float2*>(hb + (int64_t)er * ldh + fo);
+        const float2 ho = *reinterpret_cast<const float2*>(hb + (int64_t)er[u] * ldh + fo);
         float2 hv;
         {
             const float rg = fast_sigmoid(r0), zg = fast_sigmoid(z0);
@@ -1437,8 +1453,20 @@ __device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* 
             const float ng = fast_tanh(ni1 + rg * nh1);
             hv.y = ng + zg * (ho.y - ng);
         }
-        if (valid) *reinterpret_cast<float2*>(hb + (int64_t)er * ldh + fo) = hv;  // in place: own features only
+        if (valid[u]) *reinterpret_cast<float2*>(hb + (int64_t)er[u] * ldh + fo) = hv;  // in place: own features only
     }
+}
+
+template <int H>
+__device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* fm, const int* rmap, float* hb,
+                                 int tiles, int N, int w, int lane) {
+    // this lane's two output features after the exchange: lower lanes 8w+4g+{0,1}, upper 8w+4(g-2)+2+{0,1}
+    const int fo = 8 * w + 4 * ((lane >> 4) & 1) + (lane >= 32 ? 2 : 0);
+    int ti = 0;
+#ifndef MLG_GRU_SERIAL  // A/B: one tile at a time
+    for (; ti + 1 < tiles; ti += 2) gru_g8_tiles<2>(W, lay, fm, rmap, hb, ti, N, fo, lane);
+#endif
+    for (; ti < tiles; ++ti) gru_g8_tiles<1>(W, lay, fm, rmap, hb, ti, N, fo, lane);
 }
 
 // C: fc2 + masked argmax + epsilon-greedy per tile; records the actions (batch + LDS pending actions).
@@ -1535,29 +1563,6 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
         const int e = rmap_env(rm), n = (rm >> 1) & 127, er = e * N + n;
         const uint64_t avm = lavm[er];
         const float* hr = hn + er * ldh + 4 * g;
-        if (valid) {  // h' as three bf16 planes at this compact row: the GRU's h operand of the next step (HPL)
-            unsigned int* hq = reinterpret_cast<unsigned int*>(fm + lay.hpl + cr * XPL_STRIDE) + 2 * g;
-#pragma unroll
-            for (int kc = 0; kc < HC; ++kc) {  // features 16 kc + 4 g .. + 3
-                float v[4];
-                const floatx4 hv = ld4(hr + kc * 16);
-                v[0] = hv[0];
-                v[1] = hv[1];
-                v[2] = hv[2];
-                v[3] = hv[3];
-#pragma unroll
-                for (int lvl = 0; lvl < 3; ++lvl) {  // split3's pieces (round to nearest, exact remainders)
-                    const unsigned int a = cvt_pk_bf16(v[0], v[1]), c = cvt_pk_bf16(v[2], v[3]);
-                    *reinterpret_cast<uint2*>(hq + lvl * 32 + 8 * kc) = make_uint2(a, c);
-                    if (lvl < 2) {
-                        v[0] -= __uint_as_float(a << 16);
-                        v[1] -= __uint_as_float(a & 0xFFFF0000u);
-                        v[2] -= __uint_as_float(c << 16);
-                        v[3] -= __uint_as_float(c & 0xFFFF0000u);
-                    }
-                }
-            }
-        }
         ArgmaxState as{-INFINITY, 1 << 30};
         // epsilon-greedy coin (action_selectors.py:44-62, counter RNG of spec §3.7): computed by every lane with no
         // branch, so it issues between the fc2 MFMAs; only the rare exploring lanes take the branch below
@@ -1617,6 +1622,35 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
             bt.actions[bt_off] = act;
             if (!bt.full_write) bt.actions_onehot[bt_off * A + act] = 1.0f;
 #endif
+        }
+    }
+}
+
+// v7: h' of compact tile ti as three bf16 planes (split3's pieces: round to nearest, exact remainders) at its compact
+// rows (HPL), the GRU's h operand of the next step. Run between barrier C and the end of the step (HPL is read by the
+// next step's GRU after two more barriers; the fp32 h' it reads was written before barrier B).
+template <int H>
+__device__ inline void hpl_split_tile(const RolloutLds2& lay, float* fm, const int* rmap, const float* hb, int ti, int N,
+                                      int lane) {
+    constexpr int HC = H / 16;
+    const int col = lane & 15, g = lane >> 4, cr = ti * 16 + col, rm = rmap[cr];
+    if (!(rm & 1)) return;
+    const float* hr = hb + rmap_er(rm, N) * lay.ldh + 4 * g;
+    unsigned int* hq = reinterpret_cast<unsigned int*>(fm + lay.hpl + cr * XPL_STRIDE) + 2 * g;
+#pragma unroll
+    for (int kc = 0; kc < HC; ++kc) {  // features 16 kc + 4 g .. + 3
+        const floatx4 hv = ld4(hr + kc * 16);
+        float v[4] = {hv[0], hv[1], hv[2], hv[3]};
+#pragma unroll
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            const unsigned int a = cvt_pk_bf16(v[0], v[1]), c = cvt_pk_bf16(v[2], v[3]);
+            *reinterpret_cast<uint2*>(hq + lvl * 32 + 8 * kc) = make_uint2(a, c);
+            if (lvl < 2) {
+                v[0] -= __uint_as_float(a << 16);
+                v[1] -= __uint_as_float(a & 0xFFFF0000u);
+                v[2] -= __uint_as_float(c << 16);
+                v[3] -= __uint_as_float(c & 0xFFFF0000u);
+            }
         }
     }
 }
@@ -2006,6 +2040,8 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
 #endif
         sp.mark(2);
         lds_barrier();
+        if constexpr (G8)  // h' planes of tile ti by wave NW - 1 - ti (off the fc2 -> barrier C path)
+            for (int ti = NW - 1 - wave; ti < tiles; ti += NW) hpl_split_tile<H>(lay, fm, wmap, hn, ti, N, lane);
         sp.mark(3);
         const EnvCtx Ce = env_ctx_step(C);
         env_lane_step1(Ce, E, t, hl);
