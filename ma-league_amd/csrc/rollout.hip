@@ -21,19 +21,19 @@
 
 #ifdef MLG_STAMPS
 // Diagnostic build only (-DMLG_STAMPS, libmaleague_stamps.so): per-wave cycle counts of the rollout phases,
-// written to g_mlg_stamps[block][wave][16] (slots 0..13 phases, 14 total, 15 = 1).
+// written to g_mlg_stamps[block][wave][32] (slots 0..29 phases, 30 total, 31 = 1).
 __device__ unsigned long long* g_mlg_stamps = nullptr;
 struct Stamps {
-    unsigned long long acc[14], last, begin, tstep;
+    unsigned long long acc[30], last, begin, tstep;
     __device__ void init() {
-        for (int k = 0; k < 14; ++k) acc[k] = 0;
+        for (int k = 0; k < 30; ++k) acc[k] = 0;
         last = begin = tstep = __builtin_amdgcn_s_memtime();
     }
     // step trace (wave 0): cycles of step t-1 and running envs of step t, after the phase slots of the grid
     __device__ void step(int t, int nrun) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         if (g_mlg_stamps && threadIdx.x == 0 && t < 128)
-            g_mlg_stamps[(int64_t)gridDim.x * 8 * 16 + (int64_t)blockIdx.x * 128 + t] = ((now - tstep) << 8) | (unsigned)nrun;
+            g_mlg_stamps[(int64_t)gridDim.x * 8 * 32 + (int64_t)blockIdx.x * 128 + t] = ((now - tstep) << 8) | (unsigned)nrun;
         tstep = now;
 #ifdef MLG_STAMPS_LOWRUN
         on = nrun <= MLG_STAMPS_LOWRUN;
@@ -59,10 +59,10 @@ struct Stamps {
     }
     __device__ void flush() {
         if ((threadIdx.x & 63) || !g_mlg_stamps) return;
-        unsigned long long* o = g_mlg_stamps + ((int64_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 16;
-        for (int k = 0; k < 14; ++k) o[k] = acc[k];
-        o[14] = __builtin_amdgcn_s_memtime() - begin;
-        o[15] = 1;
+        unsigned long long* o = g_mlg_stamps + ((int64_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 32;
+        for (int k = 0; k < 30; ++k) o[k] = acc[k];
+        o[30] = __builtin_amdgcn_s_memtime() - begin;
+        o[31] = 1;
     }
 };
 #else
@@ -1181,7 +1181,6 @@ __device__ __forceinline__ int rmap_prev(int rm) { return (rm >> 16) & 255; }
 // (agents die, envs end), so a row's previous compact index is x_prev + the number of its env's earlier agents
 // in m_prev.
 __device__ inline int make_rmap(uint32_t m, int* wmap, int lane, uint32_t& m_prev, int& x_prev) {
-    const int l16 = lane & 15;
     int c = group_incl_scan<16>(__builtin_popcount(m), lane);
     const int rows = __builtin_amdgcn_readlane(c, 15);
     const int x = c - __builtin_popcount(m);
@@ -1992,7 +1991,9 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         int tiles;
         int* wmap = smem + lay.rmap + wave * lay.rms;
         if constexpr (G8) {
+            // rebuilt every step (skipping unchanged maps measured slower: the extra live registers spill)
             tiles = make_rmap(C.amask[lane & 15], wmap, lane, m_prev, x_prev);
+            sp.mark(14);  // v7 stamps: row map (incl. the step's status ballot) in slot 14
 #ifndef MLG_FC1_SERIAL  // A/B: the tile-by-tile fc1
             if constexpr (SN > 0) {
                 const int nu = tiles > gi ? (tiles - gi + G - 1) / G : 0;
@@ -2038,10 +2039,16 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         else
             ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
 #endif
+        // v7: h' planes (hpl_split_tile) by the waves that have no fc2 tile, beside the fc2 phase (when every wave has
+        // one -- tiles >= 8, generic shapes -- by the fc2 waves after their tiles)
+        if constexpr (G8) {
+            const bool idle = tiles < NW;
+            const int step = idle ? NW - tiles : NW;
+            for (int ti = idle ? wave - tiles : wave; ti >= 0 && ti < tiles; ti += step)
+                hpl_split_tile<H>(lay, fm, wmap, hn, ti, N, lane);
+        }
         sp.mark(2);
         lds_barrier();
-        if constexpr (G8)  // h' planes of tile ti by wave NW - 1 - ti (off the fc2 -> barrier C path)
-            for (int ti = NW - 1 - wave; ti < tiles; ti += NW) hpl_split_tile<H>(lay, fm, wmap, hn, ti, N, lane);
         sp.mark(3);
         const EnvCtx Ce = env_ctx_step(C);
         env_lane_step1(Ce, E, t, hl);

@@ -20,42 +20,42 @@ exp._init_stepper()
 st = exp.stepper
 st.t_env = 10 ** 6
 grid = (B + 15) // 16
-buf = torch.zeros(grid * 8 * 16 + grid * 128, dtype=torch.int64, device="cuda")  # phase slots + step trace
+buf = torch.zeros(grid * 8 * 32 + grid * 128, dtype=torch.int64, device="cuda")  # phase slots + step trace
 _native.call("mlg_debug_set_stamps", _native.ptr(buf))
 for it in range(3):
     buf.zero_()
     exp._train_episode(it * B)
 torch.cuda.synchronize()
 allb = buf.cpu().numpy()
-a = allb[:grid * 128].reshape(grid, 8, 16).astype(np.float64)
-tr = allb[grid * 128:].reshape(grid, 128)
-valid = a[:, :, 15] == 1
+a = allb[:grid * 256].reshape(grid, 8, 32).astype(np.float64)
+tr = allb[grid * 256:].reshape(grid, 128)
+valid = a[:, :, 31] == 1
 if os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v1":
     names = ["agent", "barrier_after_agent", "-", "-"]
     names += ["E1_exec_actions", "E2_resolve(+bar)", "E3_reduce(+bar)", "obs(+bar)", "state", "avail",
               "zero+list+barrier"]
 elif os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v7":
     names = ["A_fc1", "B_gru", "C_fc2_select", "barrier_after_C", "E1_exec(+E2)", "barrier_A",
-             "E3_reduce", "pair_pass", "status/tail-zero", "obs", "barrier_end", "avail", "state", "barrier_B"]
+             "E3_reduce", "pair_pass", "status/tail-zero", "obs", "barrier_end", "avail", "state", "barrier_B", "rowmap"]
 else:
     names = ["A_fc1", "B_gru(+barrier A)", "C_fc2_select(+barrier B)", "barrier_after_C", "E1_exec", "E2_resolve",
              "E3_reduce", "pair_pass", "status/tail-zero", "obs", "barrier_end", "avail", "state"]
 if os.environ.get("MLG_ROLLOUT_KERNEL", "v4") == "v4":
     for role, ws in (("agent waves 0-3", slice(0, 4)), ("env waves 4-7", slice(4, 8))):
         sub = a[:, ws, :]
-        vv = sub[:, :, 15] == 1
-        tt = sub[:, :, 14][vv].mean()
+        vv = sub[:, :, 31] == 1
+        tt = sub[:, :, 30][vv].mean()
         print(f"-- {role}: mean total {tt:.0f}")
         for k in range(14):
             m = sub[:, :, k][vv].mean()
             if m > 0:
                 print(f"   slot {k:2d} mean={m:12.0f} share={m / tt * 100:6.1f}%")
-tot = a[:, :, 14][valid].mean()
+tot = a[:, :, 30][valid].mean()
 print(f"rollout waves={valid.sum()} mean total cycles/wave={tot:.0f} (~{tot / 2.1e3:.1f} us at 2.1GHz)")
 for k, n in enumerate(names):
     v = a[:, :, k][valid]
     print(f"{n:22s} mean={v.mean():12.0f} share={v.mean() / tot * 100:6.1f}%  max={v.max():.0f}")
-tw = a[:, 0, 14][valid[:, 0]]
+tw = a[:, 0, 30][valid[:, 0]]
 print("per-WG total cycles: min %.0f p10 %.0f p50 %.0f p90 %.0f max %.0f" % tuple(np.percentile(tw, [0, 10, 50, 90, 100])))
 lens = st.last_run["ep_len"].numpy()
 wmax = np.array([lens[i:i + 16].max() + 1 for i in range(0, B, 16)])
@@ -95,9 +95,9 @@ if int(os.environ.get("TIMELINE", "0")):
     envw, oth = [], []
     for g in range(grid):
         for w in range(8):
-            if a[g, w, 15] != 1 or a[g, w, 10] == 0:
+            if a[g, w, 31] != 1 or a[g, w, 10] == 0:
                 continue
-            (envw if a[g, w, 7] > 0 else oth).append(a[g, w, :14])
+            (envw if a[g, w, 7] > 0 else oth).append(a[g, w, :15])
     for nm, rows in (("env wave", envw), ("other waves", oth)):
         if not rows:
             continue

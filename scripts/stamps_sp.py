@@ -31,24 +31,24 @@ home, away = BasicMAC(proto.scheme, groups, args), BasicMAC(proto.scheme, groups
 stepper.initialize(scheme, groups, preprocess, home, away)
 stepper.t_env = 10 ** 6
 grid = (B + RS - 1) // RS
-buf = torch.zeros(grid * 8 * 16 + grid * 128, dtype=torch.int64, device="cuda")
+buf = torch.zeros(grid * 8 * 32 + grid * 128, dtype=torch.int64, device="cuda")
 _native.call("mlg_debug_set_stamps", _native.ptr(buf))
 for it in range(3):
     buf.zero_()
     stepper.run(test_mode=False)
 torch.cuda.synchronize()
 allb = buf.cpu().numpy()
-a = allb[:grid * 128].reshape(grid, 8, 16).astype(np.float64)
-tr = allb[grid * 128:].reshape(grid, 128)
-valid = a[:, :, 15] == 1
+a = allb[:grid * 256].reshape(grid, 8, 32).astype(np.float64)
+tr = allb[grid * 256:].reshape(grid, 128)
+valid = a[:, :, 31] == 1
 names = os.environ.get("SP_SLOTS", "fc1,barrier_A,gru,barrier_B,fc2_select,barrier_C,E1_E2,E3_pair_obs,tail,barrier_end")
 names = names.split(",")
-tot = a[:, :, 14][valid].mean()
+tot = a[:, :, 30][valid].mean()
 print(f"waves={valid.sum()} mean total cycles/wave={tot:.0f}")
 for role, ws in (("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
     sub = a[:, ws, :]
-    vv = sub[:, :, 15] == 1
-    tt = sub[:, :, 14][vv].mean()
+    vv = sub[:, :, 31] == 1
+    tt = sub[:, :, 30][vv].mean()
     print(f"-- {role}: mean total {tt:.0f}")
     for k, n in enumerate(names):
         m = sub[:, :, k][vv].mean()
