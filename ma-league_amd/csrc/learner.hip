@@ -14,7 +14,6 @@
 //               (deterministic slab reduction; MFMA with the row index as K)
 //   finish      loss/stat reduction, clip_grad_norm_(10), RMSprop step                       (:104-105, learner.py:25-31)
 // Tensors saved for backward are t-major: [T][R][F] with R = B * N agent rows (r = b * N + n).
-#include <mutex>
 #include <algorithm>
 
 #include "agent_device.h"
@@ -495,20 +494,20 @@ __global__ void __launch_bounds__(512) agent_rec_kernel(LCfg c, AgentLayout L, c
 // gives every lane the three gates of one (feature 16w + 4fg + g, row): all 64 lanes finish one GRU cell each.
 // grid (2 * ntiles4): blockIdx < ntiles4 online (saves gates), else target. H/16 waves.
 template <int H>
-__global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
-                                                         const float* __restrict__ Ptg, const float* __restrict__ gi_on,
-                                                         const float* __restrict__ gi_tg, float* __restrict__ hs_on,
-                                                         float* __restrict__ hs_tg, float* __restrict__ ws_gr,
-                                                         float* __restrict__ ws_gz, float* __restrict__ ws_gn,
-                                                         float* __restrict__ ws_ghn, const float* __restrict__ msum) {
+__device__ __forceinline__ void agent_rec4_body(const LCfg& c, const AgentLayout& L, const float* __restrict__ Pon,
+                                                const float* __restrict__ Ptg, const float* __restrict__ gi_on,
+                                                const float* __restrict__ gi_tg, float* __restrict__ hs_on,
+                                                float* __restrict__ hs_tg, float* __restrict__ ws_gr,
+                                                float* __restrict__ ws_gz, float* __restrict__ ws_gn,
+                                                float* __restrict__ ws_ghn, const float* __restrict__ msum, int bid) {
     constexpr int LDA = H + 4;
     __shared__ __attribute__((aligned(16))) float hs[2][4 * LDA];
     LStamps lst;
     lst.init();
     const int Te = t_eff(msum);
     const int nt4 = (c.R + 3) / 4;
-    const bool online = blockIdx.x < nt4;
-    const int tile = online ? blockIdx.x : blockIdx.x - nt4;
+    const bool online = bid < nt4;
+    const int tile = online ? bid : bid - nt4;
     const float* P = online ? Pon : Ptg;
     const float* gi = online ? gi_on : gi_tg;
     float* hsg = online ? hs_on : hs_tg;
@@ -608,6 +607,16 @@ __global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, 
         }
     }
     lst.flush(0);
+}
+
+template <int H>
+__global__ void __launch_bounds__(512) agent_rec4_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
+                                                         const float* __restrict__ Ptg, const float* __restrict__ gi_on,
+                                                         const float* __restrict__ gi_tg, float* __restrict__ hs_on,
+                                                         float* __restrict__ hs_tg, float* __restrict__ ws_gr,
+                                                         float* __restrict__ ws_gz, float* __restrict__ ws_gn,
+                                                         float* __restrict__ ws_ghn, const float* __restrict__ msum) {
+    agent_rec4_body<H>(c, L, Pon, Ptg, gi_on, gi_tg, hs_on, hs_tg, ws_gr, ws_gz, ws_gn, ws_ghn, msum, blockIdx.x);
 }
 
 // grid (ntiles, T, 2), Ap/16 waves: wave = action tile. q = b2 + W2 . h_t (h_t = HS[t + 1]).
@@ -1214,7 +1223,7 @@ __global__ void __launch_bounds__(128) mix_td_kernel(LCfg c, MlgBatch bt, MixPtr
 // ================================================================================================
 // Split mixer (default for the FAST shapes): the QMixer's hypernetworks read only the state (qmix.py:41-52: hyper_w_1,
 // hyper_b_1, hyper_w_final, V), not the agent network, so their forward -- about two thirds of mix_td's matrix work --
-// runs in mix_pre_kernel on a second stream while the agent recurrence runs (run_train). Per (b, t) row it stores the
+// runs beside the agent recurrence, in the same launch (rec4_mixpre_kernel) on the CUs the recurrence leaves idle. Per (b, t) row it stores the
 // pre-abs hyper_w_1 outputs of every agent, the pre-abs hyper_w_final outputs, hyper_b_1 and V: online on s_t, target
 // on s_{t+1}; the online net also stores its layer-1 activations and the state row for the weight gradients.
 // mix_td2_kernel then gathers the Qs, mixes (MixerPF::mix), forms the TD error and runs the mixer backward exactly as
@@ -1225,14 +1234,15 @@ struct HypOut {
     int hs;
 };
 
+// One 16-row tile by a pair of waves: wv 0 the target net on s_{t+1}, wv 1 the online net on s_t.
 template <int HE, int E>
-__global__ void __launch_bounds__(128) mix_pre_kernel(LCfg c, MlgBatch bt, MixPtrs Mon, MixPtrs Mtg, MixPack mp,
-                                                      HypOut o) {
+__device__ __forceinline__ void mix_pre_tile(const LCfg& c, const MlgBatch& bt, const MixPtrs& Mon, const MixPtrs& Mtg,
+                                             const MixPack& mp, const HypOut& o, int tile, int wv, int lane) {
     using Mx = Mixer<HE, E>;
     using MP = MixerPF<HE, E, 4, MIXPF_N>;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, g = lane >> 4;
-    const bool tgt = wv == 0;  // wave 0: target net on s_{t+1}; wave 1: online net on s_t
-    const int rm = blockIdx.x * 16 + col;
+    const int col = lane & 15, g = lane >> 4;
+    const bool tgt = wv == 0;
+    const int rm = tile * 16 + col;
     const int Tm = c.T - 1;
     const bool valid = rm < c.RM;
     const int b = valid ? rm / Tm : 0, t = valid ? rm % Tm : 0;
@@ -1262,6 +1272,28 @@ __global__ void __launch_bounds__(128) mix_pre_kernel(LCfg c, MlgBatch bt, MixPt
         if (g == 0)
             for (int k = 0; k < S; ++k) o.srow[(int64_t)rm * S + k] = s[k];
     }
+}
+
+// The agent recurrence (agent_rec4_kernel, blocks < 2 * ntiles4) and the mixer's hypernetwork forward (mix_pre_tile,
+// blockDim / 128 tiles per block after them) in one launch: the recurrence occupies (R / 4) * 2 CUs for its whole
+// sequential T loop, the hypernet tiles run on the idle ones, with no cross-stream fork / join.
+template <int H>
+__global__ void __launch_bounds__(512) rec4_mixpre_kernel(LCfg c, AgentLayout L, const float* __restrict__ Pon,
+                                                          const float* __restrict__ Ptg, const float* __restrict__ gi_on,
+                                                          const float* __restrict__ gi_tg, float* __restrict__ hs_on,
+                                                          float* __restrict__ hs_tg, float* __restrict__ ws_gr,
+                                                          float* __restrict__ ws_gz, float* __restrict__ ws_gn,
+                                                          float* __restrict__ ws_ghn, const float* __restrict__ msum,
+                                                          MlgBatch bt, MixPtrs Mon, MixPtrs Mtg, MixPack mp, HypOut o) {
+    const int nrec = 2 * ((c.R + 3) / 4);
+    if ((int)blockIdx.x < nrec) {
+        agent_rec4_body<H>(c, L, Pon, Ptg, gi_on, gi_tg, hs_on, hs_tg, ws_gr, ws_gz, ws_gn, ws_ghn, msum, blockIdx.x);
+        return;
+    }
+    const int w = threadIdx.x >> 6, per = blockDim.x / 128;
+    const int tile = ((int)blockIdx.x - nrec) * per + (w >> 1);
+    if (tile * 16 >= c.RM) return;  // whole pair of waves past the last tile (block-uniform per wave pair)
+    mix_pre_tile<64, 32>(c, bt, Mon, Mtg, mp, o, tile, w & 1, threadIdx.x & 63);
 }
 
 template <int HE, int E>
@@ -1383,7 +1415,7 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
         dwfh[mt] = acc;
     }
     if (valid) {
-        // layer-1 activations (stored by mix_pre_kernel) for the ReLU masks
+        // layer-1 activations (stored by mix_pre_tile) for the ReLU masks
         const float* la = hy.la + (int64_t)rm * L1;
         float* d1 = o.d1 + (int64_t)rm * L1;
 #pragma unroll
@@ -1849,7 +1881,7 @@ Plan make_plan(const MlgLearnerCfg* cfg, int T1) {
     w.da2 = take(RM * c.N * c.E);
     w.df2 = take(RM * c.E);
     w.dv2 = take(RM);
-    w.hyp_stride = c.mixer == 2 ? (int)a4((int64_t)c.N * c.E + 2 * c.E + 1) : 0;  // mix_pre_kernel rows (HypOut)
+    w.hyp_stride = c.mixer == 2 ? (int)a4((int64_t)c.N * c.E + 2 * c.E + 1) : 0;  // mix_pre_tile rows (HypOut)
     w.hyp_on = take(RM * w.hyp_stride);
     w.hyp_tg = take(RM * w.hyp_stride);
     w.n_mix_tiles = (int)((RM + 15) / 16);
@@ -1898,27 +1930,6 @@ WJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     *slab_floats = mlg::layout_bjobs(J, n_tasks, n_red, &slab_part);  // slab partials + per-block norm partials
     p.w.nrm = p.w.slab + slab_part;
     return J;
-}
-
-// Second stream of the learner (one per device, created on first use, process lifetime) with the two events that
-// fork it from and join it back into the caller's stream.
-struct AuxStream {
-    hipStream_t s = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-};
-AuxStream* aux_stream() {
-    static std::mutex mu;
-    static AuxStream per_dev[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    AuxStream& a = per_dev[dev];
-    if (!a.s) {
-        if (hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        for (auto& e : a.ev)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    }
-    return &a;
 }
 
 template <int H>
@@ -1997,27 +2008,22 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     }
     const int ntiles = (c.R + 15) / 16;
     const int threads = (c.H / 16) * 64;
-    // split mixer: the hypernetwork forward on a second stream, concurrent with the agent network (mix_pre_kernel)
+    // split mixer (default for the FAST shapes): the hypernetwork forward rides in the recurrence launch
+    // (rec4_mixpre_kernel), mix_td2_kernel does the rest; MLG_MIX_FUSED=1: the one-kernel mix_td
+    static const bool rec16 = getenv("MLG_LEARNER_REC16") != nullptr;  // A/B switch: the 16-row tile recurrence
     const bool fast_mix = p.mp.Sp <= 64 && c.N <= MIXPF_N && c.A <= MIXPF_A && !getenv("MLG_MIX_GENERIC");
-    // opt-in (MLG_MIX_SPLIT=1): measured slower in the full bench (1.57-1.62 vs 1.33 ms per iteration: the
-    // cross-stream fork / join stalls the pipelined host loop), so the one-kernel mix_td stays the default
-    static const bool split_env = getenv("MLG_MIX_SPLIT") != nullptr;
-    const bool split_mix = c.mixer == 2 && fast_mix && split_env;
+    static const bool fused_env = getenv("MLG_MIX_FUSED") != nullptr;
+    const bool split_mix = c.mixer == 2 && fast_mix && !fused_env && !rec16 && threads % 128 == 0;
     HypOut hy{ws + p.w.hyp_on, ws + p.w.hyp_tg, ws + p.w.l1act, ws + p.w.srow, p.w.hyp_stride};
-    AuxStream* aux = nullptr;
-    if (split_mix) {
-        aux = aux_stream();
-        if (!aux) return mlg::fail("qlearner_train: auxiliary stream: %s", hipGetErrorString(hipGetLastError()));
-        (void)hipEventRecord(aux->ev[0], s);
-        (void)hipStreamWaitEvent(aux->s, aux->ev[0], 0);
-        hipLaunchKernelGGL((mix_pre_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, aux->s, c, bt, Mon, Mtg, p.mp,
-                           hy);
-        (void)hipEventRecord(aux->ev[1], aux->s);
-    }
     hipLaunchKernelGGL((agent_in_kernel<H>), dim3(ntiles, c.T, 2), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                        ws + p.w.p_tg, ws + p.w.in, ws + p.w.x, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.msum);
-    static const bool rec16 = getenv("MLG_LEARNER_REC16") != nullptr;  // A/B switch: the 16-row tile recurrence
-    if (rec16)
+    if (split_mix) {
+        const int nrec = 2 * ((c.R + 3) / 4), per = threads / 128;
+        hipLaunchKernelGGL((rec4_mixpre_kernel<H>), dim3(nrec + (p.w.n_mix_tiles + per - 1) / per), dim3(threads), 0, s,
+                           c, p.L, ws + p.w.p_on, ws + p.w.p_tg, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.hs,
+                           ws + p.w.hs_tg, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.msum, bt, Mon,
+                           Mtg, p.mp, hy);
+    } else if (rec16)
         hipLaunchKernelGGL((agent_rec_kernel<H>), dim3(2 * ntiles), dim3(threads), 0, s, c, p.L, ws + p.w.p_on,
                            ws + p.w.p_tg, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.hs, ws + p.w.hs_tg, ws + p.w.gr,
                            ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.msum);
@@ -2030,7 +2036,6 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     MixOut mo{ws + p.w.srow, ws + p.w.l1act, ws + p.w.d1, ws + p.w.da2, ws + p.w.df2, ws + p.w.dv2,
               ws + p.w.dq, ws + p.w.d2, ws + p.w.part};
     if (split_mix) {
-        (void)hipStreamWaitEvent(s, aux->ev[1], 0);
         hipLaunchKernelGGL((mix_td2_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, ws + p.w.mac,
                            ws + p.w.tmac, ws + p.w.msum, hy, mo);
     } else if (fast_mix)
