@@ -363,11 +363,11 @@ __global__ void __launch_bounds__(512) agent_in_kernel(LCfg c, MlgBatch bt, Agen
         floatx4 acc = ld4(P + L.b1 + w * 16 + 4 * g);
         if (valid) {
             if (L.last_action && t > 0) {
-                const float* oh = bt.actions_onehot + (boff - N) * A;
-                for (int a = 0; a < A; ++a) {
-                    const float v = oh[a];
-                    if (v != 0.f) acc += v * ld4(P + L.w1a + (int64_t)a * H + w * 16 + 4 * g);
-                }
+                // the one-hot row's only possible nonzero is at the recorded action (actions_onehot = OneHot(actions),
+                // zero rows past an episode's end): one load of that element instead of a scan of the A columns
+                const int a = (int)bt.actions[boff - N];
+                const float v = (a >= 0 && a < A) ? bt.actions_onehot[(boff - N) * A + a] : 0.f;
+                if (v != 0.f) acc += v * ld4(P + L.w1a + (int64_t)a * H + w * 16 + 4 * g);
             }
             if (L.agent_id) acc += ld4(P + L.w1n + (int64_t)n * H + w * 16 + 4 * g);
         }
@@ -380,17 +380,19 @@ __global__ void __launch_bounds__(512) agent_in_kernel(LCfg c, MlgBatch bt, Agen
         *reinterpret_cast<floatx4*>(xs + col * LDA + w * 16 + 4 * g) = acc;
         if (online && valid) *reinterpret_cast<floatx4*>(ws_x + ((int64_t)t * R + r) * H + w * 16 + 4 * g) = acc;
     }
-    if (online) {  // dense input row for dW1 (basic_controller.py:80-92 layout)
-        for (int i = tid; i < 16 * c.d_in; i += blockDim.x) {
-            const int rr = tile * 16 + i / c.d_in, k = i % c.d_in;
-            if (rr >= R) continue;
-            const int bb = rr / N, nn = rr % N;
+    if (online) {  // dense input row for dW1 (basic_controller.py:80-92 layout): 16 threads per row, one division per row
+        const int l = tid & 15, oa = c.d_obs + (L.last_action ? A : 0);
+        for (int i = tid >> 4; i < 16; i += blockDim.x >> 4) {
+            const int rr = tile * 16 + i;
+            if (rr >= R) break;
+            const int bb = rr / N, nn = rr - bb * N;
             const int64_t bo = (bslot(bt, bb) * bt.T1 + t) * N + nn;
-            float v;
-            if (k < c.d_obs) v = bt.obs[bo * c.d_obs + k];
-            else if (L.last_action && k < c.d_obs + A) v = t > 0 ? bt.actions_onehot[(bo - N) * A + (k - c.d_obs)] : 0.f;
-            else v = (k - c.d_obs - (L.last_action ? A : 0)) == nn ? 1.f : 0.f;
-            ws_in[((int64_t)t * R + rr) * c.d_in + k] = v;
+            float* dst = ws_in + ((int64_t)t * R + rr) * c.d_in;
+            const float* src = bt.obs + bo * c.d_obs;
+            for (int k = l; k < c.d_obs; k += 16) dst[k] = src[k];
+            if (L.last_action)
+                for (int k = l; k < A; k += 16) dst[c.d_obs + k] = t > 0 ? bt.actions_onehot[(bo - N) * A + k] : 0.f;
+            for (int k = l; k < c.d_in - oa; k += 16) dst[oa + k] = k == nn ? 1.f : 0.f;
         }
     }
     __syncthreads();
