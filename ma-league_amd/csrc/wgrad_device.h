@@ -373,7 +373,19 @@ __global__ void __launch_bounds__(256) wgrad_block_reduce_kernel(BJobsT<MJ> J, c
             float s = 0.f;
             const float* base = slab + jb.slab0 + (int64_t)blk * jb.chunks * BSLAB + e;
             int ch = 0;
-            for (; ch + 8 <= jb.chunks; ch += 8) {  // 8 loads in flight, summed in chunk order
+#ifndef MLG_WRED_DEPTH
+#define MLG_WRED_DEPTH 64
+#endif
+            // MLG_WRED_DEPTH loads in flight (the slab partials were just written by other CUs: each round trip is an
+            // L2 / MALL miss), summed in chunk order
+            for (; ch + MLG_WRED_DEPTH <= jb.chunks; ch += MLG_WRED_DEPTH) {
+                float v[MLG_WRED_DEPTH];
+#pragma unroll
+                for (int u = 0; u < MLG_WRED_DEPTH; ++u) v[u] = base[(int64_t)(ch + u) * BSLAB];
+#pragma unroll
+                for (int u = 0; u < MLG_WRED_DEPTH; ++u) s += v[u];
+            }
+            for (; ch + 8 <= jb.chunks; ch += 8) {
                 float v[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(ch + u) * BSLAB];
