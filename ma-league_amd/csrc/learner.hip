@@ -1014,6 +1014,81 @@ __device__ __forceinline__ void gather_q_pf(const LCfg& c, const MlgBatch& bt, c
 
 constexpr int MAXN = 32;
 
+// gather_q_pf with the agents spread over the four 16-lane rows (row g takes agents g, g + 4, ...: the rows of a D
+// layout hold the same (b, t) row, so gather_q_pf loaded everything four times) and the values all-gathered back by
+// rows_transpose4 (VALU lane swaps). Same selection rule per agent; N <= 8.
+template <int AMAX>
+__device__ __forceinline__ void gather_q_rows(const LCfg& c, const MlgBatch& bt, const float* mac, const float* tmac, int b,
+                                              int t, bool valid, int g, float* cq, float* tq) {
+    const int N = c.N, A = c.A, R = c.R;
+    const int64_t row0 = (bslot(bt, b) * bt.T1 + t) * N;
+    float cv[2], tv[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int n = g + 4 * i;
+        cv[i] = tv[i] = 0.f;
+        if (!valid || n >= N) continue;
+        const int r = b * N + n;
+        const int a = (int)bt.actions[row0 + n];
+        const int32_t* av = bt.avail + (bslot(bt, b) * bt.T1 + t + 1) * N * A + (int64_t)n * A;
+        const float* qn = mac + ((int64_t)(t + 1) * R + r) * A;
+        const float* tn = tmac + ((int64_t)(t + 1) * R + r) * A;
+        int avv[AMAX];
+        float qv[AMAX], tvv[AMAX];
+#pragma unroll
+        for (int k = 0; k < AMAX; ++k) {
+            const bool in = k < A;
+            avv[k] = in ? av[k] : 0;
+            qv[k] = in ? qn[k] : 0.f;
+            tvv[k] = in ? tn[k] : 0.f;
+        }
+        cv[i] = mac[((int64_t)t * R + r) * A + a];
+        if (c.double_q) {
+            float bv = 0.f;
+            int bi = 0;
+#pragma unroll
+            for (int k = 0; k < AMAX; ++k) {
+                if (k >= A) break;
+                const float v = avv[k] ? qv[k] : -9999999.f;
+                const bool take = k == 0 || v > bv;
+                bv = take ? v : bv;
+                bi = take ? k : bi;
+            }
+            float tb = 0.f;
+            int ab = 0;
+#pragma unroll
+            for (int k = 0; k < AMAX; ++k) {
+                tb = k == bi ? tvv[k] : tb;
+                ab = k == bi ? avv[k] : ab;
+            }
+            tv[i] = ab ? tb : -9999999.f;
+        } else {
+            float bv = 0.f;
+#pragma unroll
+            for (int k = 0; k < AMAX; ++k) {
+                if (k >= A) break;
+                const float v = avv[k] ? tvv[k] : -9999999.f;
+                bv = (k == 0 || v > bv) ? v : bv;
+            }
+            tv[i] = bv;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // row p's value of agent p + 4 i to every row
+        float c0 = cv[i], c1 = cv[i], c2 = cv[i], c3 = cv[i];
+        float t0 = tv[i], t1 = tv[i], t2 = tv[i], t3 = tv[i];
+        rows_transpose4(c0, c1, c2, c3);
+        rows_transpose4(t0, t1, t2, t3);
+        const float cs[4] = {c0, c1, c2, c3}, ts[4] = {t0, t1, t2, t3};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            if (4 * i + p >= MIXPF_N) break;
+            cq[4 * i + p] = cs[p];
+            tq[4 * i + p] = ts[p];
+        }
+    }
+}
+
 struct MixOut {
     float *srow, *l1act, *d1, *da2, *df2, *dv2, *dq, *d2, *part;
 };
@@ -1329,7 +1404,7 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
     const float vv = h[NE + 2 * E];
     float cq[MAXN], tq[MAXN];
     for (int n = 0; n < N; ++n) cq[n] = tq[n] = 0.f;
-    if (valid) gather_q_pf<MIXPF_A>(c, bt, mac, tmac, b, t, cq, tq);
+    gather_q_rows<MIXPF_A>(c, bt, mac, tmac, b, t, valid, g, cq, tq);
     floatx4 pre[TE], hid[TE];
     if (wv == 0) {
         const float tv = MP::mix(N, tq, b1, w1c, wfp, vv, pre, hid);
