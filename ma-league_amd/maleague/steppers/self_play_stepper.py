@@ -21,6 +21,8 @@ from .parallel_stepper import LazyEnvInfos, ParallelStepper
 
 
 class SelfPlayParallelStepper(ParallelStepper):
+    _ZERO_COPY = False  # the league reads each run's wins on the device (LeagueInstance.play)
+
     def __init__(self, args, logger, log_start_t=0):
         super().__init__(args, logger, log_start_t)
         if self.spec.n_policy_teams != 2 or self.spec.n_agents % 2:
