@@ -249,16 +249,72 @@ def roofline(mode, stepper, r, steps, B):
     return out
 
 
-def cpu_baselines(mode, a):
+def cpu_baselines(legs, a):
     """The CPU legs on the host cores, in a child process that never touches the GPU (it also forks the
-    process-model leg's env workers): oracle/cpu_baseline.py."""
+    process-model leg's env workers): oracle/cpu_baseline.py. ``legs``: "vector", "process", "refil"."""
     cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--json", "--seconds",
-           str(a.cpu_seconds), "--episode-limit", str(a.episode_limit), "--legs",
-           "refil" if mode == "refil" else "vector,process"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=max(300, 8 * a.cpu_seconds))
+           str(a.cpu_seconds), "--episode-limit", str(a.episode_limit), "--legs", ",".join(legs)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=max(300, 8 * len(legs) * a.cpu_seconds))
     if p.returncode != 0:
         return {"error": p.stderr[-400:]}
     return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def cpu_entry(c, leg_names):
+    """The cpu_baseline object of one bench leg from the CPU run's legs (the first named leg is ``value``)."""
+    if "error" in c:
+        return {"value": None, "unit": "env-steps/s", "error": c["error"]}
+    legs = [x for x in c["legs"] if x["leg"] in leg_names]
+    main_leg = legs[0]
+    return {"value": main_leg["value"], "unit": "env-steps/s", "cores": main_leg["cores"], "kind": "port",
+            "sample": main_leg["sample"], "cpu_model": c.get("cpu_model"), "host_cpus": c.get("host_cpus"),
+            "legs": legs}
+
+
+# ---- N > 1 without an outer launcher: start the ranks ourselves -----------------------------------------------
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv, out_fd) -> int:
+    """``bench.py --gpus N`` (N > 1) run directly, without torch.distributed.run around it: start
+    ``python -m torch.distributed.run --nproc-per-node N bench.py <same args>`` as a CHILD process (this process has
+    made no GPU call -- only ``import torch`` -- so nothing is exec'd from a GPU-initialised process), one rank per
+    GPU over RCCL, and relay rank 0's single JSON line. Any rank failing fails the bench (non-zero exit).
+    Replaces the reference's league topology launch, src/league/processes/central_worker.py:84-97."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL peer buffers)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or len(lines) != 1:
+        sys.stderr.write(f"bench: {a.gpus}-rank launch failed (exit {p.returncode}, {len(lines)} result lines)\n"
+                         + p.stdout[-2000:] + "\n")
+        return p.returncode or 1
+    os.write(out_fd, (lines[0] + "\n").encode())
+    return 0
+
+
+def leg_summary(L, a):
+    """A non-head leg's object in the JSON line."""
+    out = {"value": L["value"], "unit": "env-steps/s", "ms_per_step": L["ms_per_step"],
+           "represents": L["represents"], "workload": L["workload"], "parallelism": L["parallelism"],
+           "per_rank_value": L["per_rank"], "env_steps": L["env_steps"], "mean_episode_len": L["mean_episode_len"],
+           "rollout_kernel": L["roofline"]["kernel"], "avg_kernel_ms": L["avg_kernel_ms"],
+           "roofline_frac": L["roofline"]["frac"], "roofline": L["roofline"]}
+    if "league_iterations" in L:
+        out.update({"match_len": a.match_len,
+                    **{k: L[k] for k in ("league_iterations", "exchange_ms_mean", "exchange_ms_max", "exchange_frac",
+                                         "collective_backend", "world_size", "opponents_rank0",
+                                         "historical_snapshots", "evictions", "payoff_games")},
+                    "note": "league scaling = league.value at N / league.value at N = 1 (same leg, same per-GPU "
+                            "workload: weak scaling)"})
+    return out
 
 
 def main():
@@ -273,9 +329,12 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--episode-limit", type=int, default=100)
     ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    a = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch / process-group plumbing only: init the group, report the world, run no leg")
+    argv = sys.argv[1:]
+    a = ap.parse_args(argv)
     # stdout carries exactly one line, the JSON result: native libraries (RCCL prints a version banner on its first
     # communicator) write to fd 1, so fd 1 is pointed at stderr and the result goes to a saved copy of stdout
     out_fd = os.dup(1)
@@ -283,25 +342,56 @@ def main():
     os.dup2(2, 1)
 
     launched = "WORLD_SIZE" in os.environ  # torch.distributed.run (any nproc) -> a process group, RCCL
+    if a.gpus > 1 and not launched:
+        sys.exit(launch_ranks(a, argv, out_fd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench: --gpus {a.gpus} but the launcher started {world} ranks")
     local_rank = a.device if a.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    use_gpu = not a.dry_run
     if launched:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        if a.backend == "nccl":
+        if use_gpu:
+            torch.cuda.set_device(local_rank)
+        if a.backend == "nccl" and use_gpu:
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
         else:
             dist.init_process_group(a.backend)
-    dev = torch.device(f"cuda:{local_rank}")
-    torch.cuda.set_device(dev)
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
+    dev = torch.device(f"cuda:{local_rank}") if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(dev)
     ctx = Ctx(dist, dev)
+
+    if a.dry_run:
+        # the league exchange's collectives once over the launched group (payoff all_reduce, parameter all_gather,
+        # barrier), with a parameter vector = the rank id, so the line shows every rank took part
+        from maleague.league import DistributedLeague
+        from maleague.league.payoff import PayoffEntry
+        lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=world)
+        lg.record(rank, (rank + 1) % world, PayoffEntry.WIN, n=rank + 1)
+        lg.sync_payoff()
+        lg.exchange(torch.full((8,), float(rank), device=dev), 100 * rank, checkpoint=True)
+        lg.barrier()
+        ranks = ctx.gather(float(rank))
+        if rank == 0:
+            out = {"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": ctx.world, "steps": 0,
+                   "warmup": 0, "dry_run": True, "ranks": [int(r) for r in ranks],
+                   "league": {"world_size": ctx.world, "collective_backend": lg.backend,
+                              "params_of": [float(lg.params_of(p)[0]) for p in range(world)],
+                              "payoff_wins": float(lg.payoff.tensor[..., PayoffEntry.WIN].sum()),
+                              "historical_snapshots": len(lg.historical_meta)}}
+            os.write(out_fd, (json.dumps(out) + "\n").encode())
+        if dist:
+            dist.destroy_process_group()
+        return
 
     from maleague.custom_logging import MainLogger
     from maleague.runs import MultiAgentExperiment
 
-    legs = {"auto": ["ai", "league"], "ai": ["ai"], "league": ["league"], "refil": ["refil"]}[a.mode]
+    legs = {"auto": ["ai", "league", "refil"], "ai": ["ai"], "league": ["league"], "refil": ["refil"]}[a.mode]
     results = {}
     for leg in legs:
         args, plan = make_args(leg, a, rank, local_rank)
@@ -335,9 +425,10 @@ def main():
         if inst is None:
             ep = [0]
 
-            def iteration(i, exp=exp, B=B, ep=ep):
-                exp._train_episode(ep[0])
-                ep[0] += B
+            def iteration(i, exp=exp, ep=ep):
+                # one iteration of MultiAgentExperiment.start's loop (train-mode run, insert, train, the
+                # interval checks), exactly as the product loop runs it
+                ep[0] = exp._iteration(ep[0])
 
             r = timed_loop(ctx, iteration, stepper, a.steps, a.warmup)
         else:
@@ -351,16 +442,13 @@ def main():
 
     head = legs[0]
     h = results[head]
-    cpu = None
+    cpu, cpu_refil = None, None
     if rank == 0 and world == 1 and head in ("ai", "refil") and not a.no_cpu_baseline:
-        c = cpu_baselines(head, a)
-        if "error" in c:
-            cpu = {"value": None, "unit": "env-steps/s", "error": c["error"]}
-        else:
-            main_leg = c["legs"][0]
-            cpu = {"value": main_leg["value"], "unit": "env-steps/s", "cores": main_leg["cores"], "kind": "port",
-                   "sample": main_leg["sample"], "cpu_model": c.get("cpu_model"), "host_cpus": c.get("host_cpus"),
-                   "legs": c["legs"]}
+        names = (["vector", "process"] if head == "ai" else []) + (["refil"] if "refil" in results else [])
+        c = cpu_baselines(names, a)
+        cpu = cpu_entry(c, ["refil"] if head == "refil" else ["vector", "process"])
+        if head != "refil" and "refil" in results:
+            cpu_refil = cpu_entry(c, ["refil"])
     if rank == 0:
         out = {"metric": METRIC, "value": h["value"], "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
                "warmup": a.warmup, "ms_per_step": h["ms_per_step"], "higher_is_better": True, "scaling": "weak",
@@ -378,20 +466,12 @@ def main():
                                                "exchange_frac", "collective_backend", "world_size",
                                                "opponents_rank0", "historical_snapshots", "evictions")}
         if "league" in results and head != "league":
-            L = results["league"]
-            out["league"] = {"value": L["value"], "unit": "env-steps/s", "ms_per_step": L["ms_per_step"],
-                             "represents": L["represents"], "workload": L["workload"],
-                             "parallelism": L["parallelism"], "per_rank_value": L["per_rank"],
-                             "env_steps": L["env_steps"], "mean_episode_len": L["mean_episode_len"],
-                             "match_len": a.match_len,
-                             **{k: L[k] for k in ("league_iterations", "exchange_ms_mean", "exchange_ms_max",
-                                                  "exchange_frac", "collective_backend", "world_size",
-                                                  "opponents_rank0", "historical_snapshots", "evictions",
-                                                  "payoff_games")},
-                             "rollout_kernel": L["roofline"]["kernel"], "avg_kernel_ms": L["avg_kernel_ms"],
-                             "roofline_frac": L["roofline"]["frac"],
-                             "note": "league scaling = league.value at N / league.value at N = 1 (same leg, "
-                                     "same per-GPU workload: weak scaling)"}
+            out["league"] = leg_summary(results["league"], a)
+        if "refil" in results and head != "refil":
+            out["refil"] = leg_summary(results["refil"], a)
+            out["refil"]["cpu_baseline"] = cpu_refil
+            out["refil"]["note"] = ("BASELINE config 5 at the same N (replicas: one REFIL learner per GPU vs the "
+                                    "scripted AI)")
         sys.stdout.flush()
         os.write(out_fd, (json.dumps(out) + "\n").encode())
     if dist:

@@ -200,6 +200,8 @@ typedef struct {
 
 int64_t mlg_qlearner_param_counts(const MlgLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);
 int64_t mlg_qlearner_workspace_floats(const MlgLearnerCfg *c);
+/* Largest batch (episodes) whose slot map may travel as MlgLearnerBufs.host_rows (a kernel argument). */
+int mlg_qlearner_inline_rows(void);
 int mlg_qlearner_train(const MlgLearnerCfg *c, const MlgLearnerBufs *b, void *stream);
 
 

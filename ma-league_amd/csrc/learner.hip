@@ -2168,6 +2168,8 @@ extern "C" int64_t mlg_qlearner_param_counts(const MlgLearnerCfg* c, int64_t* n_
     return p.n_agent + p.n_mixer;
 }
 
+extern "C" int mlg_qlearner_inline_rows(void) { return MLG_INLINE_ROWS; }
+
 extern "C" int64_t mlg_qlearner_workspace_floats(const MlgLearnerCfg* c) {
     if (check_cfg(c)) return -1;
     Plan p = make_plan(c, c->T);

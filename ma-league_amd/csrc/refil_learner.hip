@@ -70,6 +70,11 @@ int check_cfg(const MlgRefilLearnerCfg* c) {
     MLG_REQUIRE(D0 <= KMAX && c->n_actions >= 1 && c->n_actions <= 32, "refil learner: entity input %d / actions %d",
                 D0, c->n_actions);
     MLG_REQUIRE(c->imagine == 1, "refil learner: the imagine agent (REFIL) is the built path");
+    // the recurrences store hs / gates / dGI / dGH through buffer resources (32-bit byte offsets): the largest of
+    // them, (T + 1) x 3B*NA rows x 3*EMB floats, must stay under 2 GiB or its stores would be silently dropped
+    MLG_REQUIRE((int64_t)(c->T + 1) * 3 * c->B * c->n_agents * 3 * EMB < (int64_t)1 << 29,
+                "refil learner: (T+1)*3B*NA*3*EMB=%lld floats exceeds the 2 GB buffer-store range",
+                (long long)(c->T + 1) * 3 * c->B * c->n_agents * 3 * EMB);
     return 0;
 }
 

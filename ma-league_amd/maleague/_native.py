@@ -123,6 +123,7 @@ SIGNATURES = {
     "mlg_qmix_forward": (ctypes.c_int, [_P, _P, _P, _P, _I, _P]),
     "mlg_qlearner_param_counts": (ctypes.c_int64, [_P, _P, _P]),
     "mlg_qlearner_workspace_floats": (ctypes.c_int64, [_P]),
+    "mlg_qlearner_inline_rows": (ctypes.c_int, []),
     "mlg_qlearner_train": (ctypes.c_int, [_P, _P, _P]),
     "mlg_zero_slots_bytes": (ctypes.c_int, [_P, _P, _I, _I, _I, _P]),
     "mlg_refil_packed_agent_size": (ctypes.c_int64, [_P]),

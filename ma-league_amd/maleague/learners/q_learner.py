@@ -148,7 +148,8 @@ class QLearner(Learner):
             self._ws = torch.zeros(int(need * 1.25) + 1024, dtype=torch.float32, device=self.device)
         # a sampled view of the device buffer hands its slot map over as a kernel argument (no H2D copy)
         host_rows = getattr(batch, "host_rows", None)
-        if host_rows is not None and (batch.batch_size > 64 or getattr(batch, "_data", None) is not None):
+        if host_rows is not None and (batch.batch_size > lib.mlg_qlearner_inline_rows()
+                                      or getattr(batch, "_data", None) is not None):
             host_rows = None
         mb, keep = mlg_batch(batch, device_rows=host_rows is None)
         # the target update due after this step (q_learner.py:127-128) is written by the optimizer launch itself

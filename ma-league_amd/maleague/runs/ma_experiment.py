@@ -124,9 +124,22 @@ class MultiAgentExperiment:
             if getattr(self.args, "zero_copy_insert", True) and hasattr(self.stepper, "attach_replay"):
                 self.stepper.attach_replay(self.home_buffer)
 
+    def _t_env_reached(self, threshold) -> bool:
+        """t_env >= threshold. The interval checks of the loop (t_max, test, save, log) resolve the runs in flight
+        only when the bounds of t_env straddle the threshold, so the host keeps running ahead of the device; the
+        answer is always the one the exact t_env gives."""
+        bounds = getattr(self.stepper, "t_env_bounds", None)
+        if bounds is not None:
+            lo, hi = bounds()
+            if hi < threshold:
+                return False
+            if lo >= threshold:
+                return True
+        return self.stepper.t_env >= threshold
+
     @property
     def _has_not_reached_t_max(self):
-        return self._play_time is None and self.stepper.t_env <= self.args.t_max
+        return self._play_time is None and not self._t_env_reached(self.args.t_max + 1)
 
     @property
     def _has_not_reached_time_limit(self):
@@ -146,19 +159,7 @@ class MultiAgentExperiment:
         it = 0
         self._start_time = self._end_time = time.time()
         while self._has_not_reached_time_limit or self._has_not_reached_t_max:
-            self._train_episode(episode_num=episode)
-            n_test_runs = max(1, self.args.test_nepisode // self.stepper.batch_size)
-            if (self.stepper.t_env - self.last_test_T) / self.args.test_interval >= 1.0:
-                self._test(n_test_runs)
-            save_due = (self.stepper.t_env - self.model_save_time) >= self.args.save_model_interval
-            if self.args.save_model and (save_due or self.model_save_time == 0):
-                self.save_models()
-            episode += self.args.batch_size_run
-            if (self.stepper.t_env - self.last_log_T) >= self.args.log_interval:
-                self.logger.log_stat("episode", episode, self.stepper.t_env)
-                if hasattr(self.logger, "log_report"):
-                    self.logger.log_report()
-                self.last_log_T = self.stepper.t_env
+            episode = self._iteration(episode)
             self._end_time = time.time()
             it += 1
             if max_iterations is not None and it >= max_iterations:
@@ -167,6 +168,23 @@ class MultiAgentExperiment:
         self.logger.log_stat("episode", episode, self.stepper.t_env)
         self.stepper.close_env()
         return self.stepper.log_t
+
+    def _iteration(self, episode: int) -> int:
+        """One iteration of the training loop (ma_experiment.py:151-175): a train-mode run + at most one train,
+        then the test / save / log interval checks. Returns the next episode number."""
+        self._train_episode(episode_num=episode)
+        if self._t_env_reached(self.last_test_T + self.args.test_interval):
+            self._test(max(1, self.args.test_nepisode // self.stepper.batch_size))
+        if self.args.save_model and (self.model_save_time == 0
+                                     or self._t_env_reached(self.model_save_time + self.args.save_model_interval)):
+            self.save_models()
+        episode += self.args.batch_size_run
+        if self._t_env_reached(self.last_log_T + self.args.log_interval):
+            self.logger.log_stat("episode", episode, self.stepper.t_env)
+            if hasattr(self.logger, "log_report"):
+                self.logger.log_report()
+            self.last_log_T = self.stepper.t_env
+        return episode
 
     def _train_episode(self, episode_num):
         episode_batch, env_info = self.stepper.run(test_mode=False)

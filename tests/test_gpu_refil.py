@@ -92,13 +92,21 @@ def test_rollout_teacher_forced_vs_oracle(device, rollout_variant, eps, test_mod
     """Teacher-forced: the oracle env replays the recorded actions; every greedy pick is an oracle argmax within Q_TOL,
     every epsilon draw bit-exact. The 64-env case runs config 5's episode limit (100) with partial workgroups."""
     spec, ag, a, nb, summ, _ = _rollout(device, B, T, seed, eps, test_mode)
+    _teacher_check(spec, ag, a, nb, summ, B, T, seed, eps, test_mode)
+
+
+def _teacher_check(spec, ag, a, nb, summ, B, T, seed, eps, test_mode, envs=None):
+    """Replay the recorded actions of ``envs`` (default: all) through the oracle entity env; every greedy pick an
+    oracle argmax within Q_TOL, every epsilon draw bit-exact, bookkeeping and summary exact."""
+    envs = list(range(B)) if envs is None else [int(e) for e in envs]
     refs = ref_entity_envs_for(spec, B, seed=seed)
     NA, A = spec.n_agents, spec.n_actions
     p = {k: v.detach().cpu() for k, v in ag.state_dict().items()}
-    qref, _ = RR.mac_forward(p, {k: torch.from_numpy(v) for k, v in nb.items()}, a)
-    qref = qref.numpy()
+    qref, _ = RR.mac_forward(p, {k: torch.from_numpy(v[envs]) for k, v in nb.items()}, a)
+    qref = dict(zip(envs, qref.numpy()))
     n_rand = n_greedy = 0
-    for b, r in enumerate(refs):
+    for b in envs:
+        r = refs[b]
         r.reset()
         L = int(summ["len"][b])
         assert 1 <= L <= T
@@ -120,7 +128,7 @@ def test_rollout_teacher_forced_vs_oracle(device, rollout_variant, eps, test_mod
                     assert acts[n] == want
                     n_rand += 1
                 else:
-                    qm = np.where(av[n] != 0, qref[b, t, n], -np.inf)
+                    qm = np.where(av[n] != 0, qref[b][t, n], -np.inf)
                     assert av[n, acts[n]] != 0 and qm[acts[n]] >= qm.max() - Q_TOL, (b, t, n)
                     n_greedy += 1
             oh = np.zeros((NA, A), np.float32)
@@ -137,6 +145,37 @@ def test_rollout_teacher_forced_vs_oracle(device, rollout_variant, eps, test_mod
         assert abs(summ["ret"][b] - ret) <= 1e-3
         assert nb["filled"][b, L + 1:].sum() == 0 and nb["reward"][b, L:].sum() == 0
     assert n_greedy > 0 and (test_mode or n_rand > 0)
+    return n_greedy, n_rand
+
+
+def test_rollout_config5_full_shape(device):
+    """BASELINE config 5 at its launch shape (4096 envs, episode limit 100, 3-8 agents per env, train mode at the
+    steady-state epsilon 0.05; 256 workgroups of the four-env kernel in one round): size-independent invariants,
+    determinism (same episode counters -> bit-identical batch and summary), and 64 envs spread over the launch
+    teacher-forced against the oracle env + oracle EntityMAC."""
+    from maleague.envs.teams_env import VecEnvState
+    B, T, seed, eps = 4096, 100, 0, 0.05
+    spec, ag, a, nb, summ, st = _rollout(device, B, T, seed, eps, test_mode=False)
+    L = summ["len"]
+    assert (L >= 1).all() and (L <= T).all()
+    assert nb["filled"].sum() == (L + 1).sum() and nb["terminated"].sum() == B
+    filled = nb["filled"][:, :, 0] == 1
+    assert (nb["actions_onehot"].sum(-1)[filled] == 1).all()
+    av_taken = np.take_along_axis(nb["avail_actions"], nb["actions"].astype(np.int64), axis=-1)[..., 0]
+    assert (av_taken[filled] == 1).all(), "every recorded action is available"
+    assert (np.mod(nb["reward"] * 16, 1) == 0).all()
+    # agents per env: the active slots of the policy team are the first k entities, k in [3, 8]
+    alive0 = (nb["entity_mask"][:, 0, :8] == 0).sum(-1)
+    assert alive0.min() >= 3 and alive0.max() <= 8 and len(np.unique(alive0)) == 6
+    # determinism
+    spec2, ag2, a2, nb2, summ2, _ = _rollout(device, B, T, seed, eps, test_mode=False, st=VecEnvState(spec, B, device))
+    for k in nb:
+        np.testing.assert_array_equal(nb[k], nb2[k], err_msg=k)
+    for k in summ:
+        np.testing.assert_array_equal(summ[k], summ2[k], err_msg=k)
+    sub = np.linspace(0, B - 1, 64).astype(int)
+    n_greedy, n_rand = _teacher_check(spec, ag, a, nb, summ, B, T, seed, eps, False, envs=sub)
+    assert n_greedy > 1000 and n_rand > 0
 
 
 def test_rollout_ring_full_write_equals_zeroed(device, rollout_variant):

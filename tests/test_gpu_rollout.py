@@ -159,9 +159,12 @@ def _build_stepper(device, plan="medium_1h_4t", B=48, episode_limit=40, seed=5, 
     return stepper, mac, args
 
 
-def _check_run(stepper, mac, args, batch, infos, episode, test_mode, eps):
+def _check_run(stepper, mac, args, batch, infos, episode, test_mode, eps, envs=None):
+    """Teacher-forced env replay + oracle agent check of a run; ``envs``: the env indices to check (all by
+    default; a subset for the 4096-env headline shape)."""
     spec = stepper.spec
     B, N, A, T1 = stepper.batch_size, spec.n_agents, spec.n_actions, stepper.episode_limit + 1
+    sub = list(range(B)) if envs is None else [int(e) for e in envs]
     nb = np_batch(batch)
     ep_len = stepper.last_run["ep_len"].numpy()
     rets = stepper.last_run["returns"].numpy()
@@ -169,7 +172,8 @@ def _check_run(stepper, mac, args, batch, infos, episode, test_mode, eps):
     assert stepper.t == ep_len.max()
     # --- env side, teacher forced: replay the recorded actions through the C oracle ---
     refs = ref_envs_for(spec, B, seed=args.seed)
-    for b, r in enumerate(refs):
+    for b in sub:
+        r = refs[b]
         r.episode = episode
         r.reset()
         L = int(ep_len[b])
@@ -198,13 +202,13 @@ def _check_run(stepper, mac, args, batch, infos, episode, test_mode, eps):
     assert len(infos) == B
     # --- agent side: oracle Q on the recorded batch; greedy / epsilon picks bit-exact ---
     params = {k: v.detach().cpu() for k, v in mac.agent.state_dict().items()}
-    tb = {k: torch.from_numpy(v) for k, v in nb.items()}
-    Tm = int(ep_len.max()) + 1
+    tb = {k: torch.from_numpy(v[sub]) for k, v in nb.items()}
+    Tm = int(ep_len[sub].max()) + 1
     with torch.no_grad():
         q, _ = LR.mac_unroll(params, tb, N, T=Tm)
-    q = q.numpy()
+    q = dict(zip(sub, q.numpy()))
     n_checked = n_random = 0
-    for b in range(B):
+    for b in sub:
         for t in range(int(ep_len[b]) + 1):
             for n in range(N):
                 a = int(nb["actions"][b, t, n, 0])
@@ -217,7 +221,7 @@ def _check_run(stepper, mac, args, batch, infos, episode, test_mode, eps):
                         assert a == envref.random_available(av.tolist(), r2)
                         n_random += 1
                         continue
-                m = np.where(av == 0, -np.inf, q[b, t, n])
+                m = np.where(av == 0, -np.inf, q[b][t, n])
                 g = int(np.argmax(m))
                 srt = np.sort(m)
                 if srt[-1] - srt[-2] > Q_TOL:
@@ -280,6 +284,55 @@ def test_rollout_headline_config_properties(device):
             rew, done, _ = r.step(nb["actions"][b, t, :, 0])
             assert nb["reward"][b, t, 0] == np.float32(rew[0])
             np.testing.assert_array_equal(nb["obs"][b, t + 1], r.obs())
+
+
+def test_rollout_headline_config_agent_parity(device):
+    """BASELINE config 2 at its full shape (5v5, 4096 envs, episode_limit 100, train mode at the steady-state
+    epsilon 0.05, the v7 kernel): 64 envs spread over the launch replayed through the C env and the fp32 oracle
+    DRQN -- every epsilon draw bit-exact vs the oracle counter RNG, every greedy pick the oracle's argmax (near
+    ties within Q_TOL), env transitions bit-exact."""
+    stepper, mac, args = _build_stepper(device, plan="medium_1h_4t", B=4096, episode_limit=100, seed=0)
+    stepper.t_env = 10 ** 6
+    eps = max(0.05, 1.0 - 0.95 / 50000 * 10 ** 6)
+    batch, infos = stepper.run(test_mode=False)
+    sub = np.linspace(0, 4095, 64).astype(int)
+    _check_run(stepper, mac, args, batch, infos, episode=0, test_mode=False, eps=eps, envs=sub)
+
+
+def test_stepper_summary_ring_runahead_matches_resolved(device):
+    """the host runs up to _HOST_RING train-mode runs ahead of the device (run summaries written by the
+    kernel into a ring of pinned buffers, t_env unresolved). Ten runs across the end of the epsilon anneal, never
+    reading t_env, must equal the same runs stepped with a resolve after each run: same epsilon per run (=
+    schedule.eval of the exact t_env), same episodes, same final t_env; the ring fills up (oldest run resolved
+    first) once the schedule is flat."""
+    from maleague.envs.teams_env import VecEnvState
+    runs = {}
+    for mode in ("ahead", "resolved"):
+        stepper, mac, args = _build_stepper(device, plan="medium_1h_4t", B=64, episode_limit=60, seed=4,
+                                            epsilon_anneal_time=6000)
+        stepper.envs = VecEnvState(stepper.spec, 64, device)
+        stepper.t_env = 0
+        eps, batches, pend, exact = [], [], [], []
+        for _ in range(10):
+            b, infos = stepper.run(test_mode=False)
+            eps.append(float(mac.action_selector.epsilon))
+            pend.append(len(stepper._pendings))
+            batches.append({k: b[k].clone() for k in b.data.transition_data})
+            if mode == "resolved":
+                exact.append(stepper.t_env)
+        runs[mode] = (eps, batches, pend, stepper.t_env, exact, [bool(i["battle_won"][0]) for i in infos])
+    ea, ba, pa, ta, _, wa = runs["ahead"]
+    er, br, _, tr, exact, wr = runs["resolved"]
+    assert ta == tr and wa == wr
+    assert ea == er
+    sched = _build_stepper(device, B=64, epsilon_anneal_time=6000)[1].action_selector.schedule
+    t_before = [0] + exact[:-1]
+    assert ea == [float(sched.eval(t)) for t in t_before]
+    assert ea[0] > ea[-1] == 0.05 and ea[1] > 0.05, ea  # annealing at first, flat at the end
+    assert max(pa) == stepper._HOST_RING, pa  # ring full: the oldest run was resolved to make room
+    for i, (x, y) in enumerate(zip(ba, br)):
+        for k in x:
+            assert torch.equal(x[k], y[k]), (i, k)
 
 
 @pytest.mark.parametrize("kernel", ["v7", "v6", "v5", "v4", "v2", "v1"])
