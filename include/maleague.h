@@ -82,6 +82,11 @@ typedef struct {
     /* Sampled view (learner entry points only): episode b lives in slot rows[b] of tensors holding more
      * slots (the replay buffer itself -- no gather copy); nullptr = identity. */
     const int32_t *rows;
+    /* Full-write mode, optional [ring_size] (or [B] without a ring): per slot, the exclusive end of the rows
+     * that may hold non-zero data (>= T1 = unknown, e.g. a fresh or externally written buffer). The rollout
+     * zeroes only rows [L + 1, slot_extent) of a slot whose new episode has length L instead of [L + 1, T1),
+     * and stores slot_extent = L + 1. nullptr = zero every tail row. */
+    int32_t *slot_extent;
 } MlgBatch;
 
 /* Per-run episode summary written by mlg_rollout. */
@@ -226,6 +231,7 @@ typedef struct {
     int64_t *filled;       /* [B][T1][1] */
     int32_t B, T1, ring_slot0, ring_size, full_write; /* as MlgBatch */
     const int32_t *rows;   /* sampled view (learner): episode b lives in slot rows[b]; nullptr = identity */
+    int32_t *slot_extent;  /* as MlgBatch */
 } MlgEntityBatch;
 
 typedef struct {

@@ -498,10 +498,18 @@ __device__ inline void zero_bytes(void* base, int64_t b0, int64_t b1, int lane) 
     for (int64_t i = (m1 > b0 ? m1 : b0) + lane; i < b1; i += 64) p[i] = 0;
 }
 
-// zero slots [t0, T1) of every key for env e (full-write ring mode), all 64 lanes
+// zero rows [t0, end) of every key of slot `slot` (full-write ring mode), all 64 lanes; end = T1, or the slot's
+// extent (MlgEntityBatch.slot_extent: the rows of its previous episode that may be non-zero), which then becomes t0
 __device__ inline void ro_zero_tail(const MlgEntityBatch& bt, const RoArgs& a, int64_t slot, int t0, int lane) {
-    if (t0 >= bt.T1) return;
-    const int64_t r0 = slot * bt.T1 + t0, r1 = (slot + 1) * (int64_t)bt.T1;
+    int end = bt.T1;
+    if (bt.slot_extent) {
+        const int x = bt.slot_extent[slot];
+        end = x < 0 ? 0 : (x < bt.T1 ? x : bt.T1);
+    }
+    // the new extent is stored once `end` is known (the old value has been read by every lane)
+    if (bt.slot_extent && lane == 0) bt.slot_extent[slot] = t0;
+    if (t0 >= end) return;
+    const int64_t r0 = slot * bt.T1 + t0, r1 = slot * (int64_t)bt.T1 + end;
     auto z = [&](void* p, int64_t row_bytes) { zero_bytes(p, r0 * row_bytes, r1 * row_bytes, lane); };
     z(bt.entities, (int64_t)a.U * a.ED * 4);
     z(bt.actions_onehot, (int64_t)a.NA * a.A * 4);

@@ -440,7 +440,8 @@ __device__ void zero_slots(const Sides& sd, const RoEnv& R, int e0, int t0, int 
 }
 
 // Per-env summary + env state write-back.
-__device__ void ro_finish(const MlgEnvState& st, const RoEnv& R, const MlgRunInfo& info, int e0, int B, int U) {
+__device__ void ro_finish(const MlgEnvState& st, const RoEnv& R, const Sides& sd, const MlgRunInfo& info, int e0, int B,
+                          int U) {
     const int tid = threadIdx.x, nthr = blockDim.x;
     for (int e = tid; e < RE; e += nthr) {
         const int b = e0 + e;
@@ -449,6 +450,10 @@ __device__ void ro_finish(const MlgEnvState& st, const RoEnv& R, const MlgRunInf
         info.ret[b] = R.ret[e];
         if (info.ret_away) info.ret_away[b] = R.ret2[e];
         st.t[b] = R.len[e];
+        for (int side = 0; side < sd.ns; ++side) {  // v1 zeroes every tail row: the slot's extent is L + 1
+            const MlgBatch bt = side_batch(sd, side);
+            if (bt.full_write && bt.slot_extent) bt.slot_extent[side_slot(R, side, e)] = R.len[e] + 1;
+        }
     }
     for (int i = tid; i < RE * U; i += nthr) {
         const int e = i / U, u = i % U;
@@ -592,8 +597,21 @@ __global__ void __launch_bounds__(512) rollout_kernel(MlgEnvSpec spec, MlgEnvSta
     for (int e = tid; e < RE; e += nthr) R.stepped[e] = 0;
     __syncthreads();
     if (any_full_write && last_t + 2 < T1) zero_slots(sd, R, e0, last_t + 2, T1, A, S, DO);
-    ro_finish(st, R, info, e0, sd.bt[0].B, U);
+    ro_finish(st, R, sd, info, e0, sd.bt[0].B, U);
 }
+
+// Full-write tail bookkeeping of one env lane, packed in one register: next row to zero (bits 0-15) and the
+// exclusive end of the rows that may still hold data of the slot's previous episode (bits 16-30: the slot's
+// extent, T1 when unknown). Before the episode ends the next row is T1 (nothing to zero).
+__device__ inline int tail_init(const MlgBatch& bt, int slot) {
+    int zend = bt.T1;
+    if (bt.full_write && bt.slot_extent) {
+        const int x = bt.slot_extent[slot];
+        zend = x < 0 ? 0 : (x < bt.T1 ? x : bt.T1);
+    }
+    return bt.T1 | (zend << 16);
+}
+__device__ inline int tail_start(int zc, int row) { return (zc & ~0xFFFF) | row; }
 
 // Full-write (ring) mode: zero timesteps [z0, z1) of every key of batch slot `slot`.
 __device__ inline void zero_slot_steps(const MlgBatch& bt, int slot, int z0, int z1, int N, int A, int S, int DO,
@@ -1657,7 +1675,8 @@ __device__ inline void hpl_split_tile(const RolloutLds2& lay, float* fm, const i
 // ---- env lanes (half-wave per env; shared by v2 and v4) -------------------------------------------
 struct EnvLane {
     UnitLane u;
-    int e, b, st, slot, len, zcur, h0, act;
+    int e, b, st, slot, len, h0, act;
+    int zcur;  // full-write tail: next row to zero (bits 0-15), exclusive end of the rows to zero (bits 16-30)
     uint32_t ep;
     float ret;
     bool stepped;
@@ -1709,6 +1728,7 @@ __device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, En
         E.ep = st.episode[E.b];
         E.st = 0;
         E.slot = C.bt.ring_size > 0 ? (C.bt.ring_slot0 + E.b) % C.bt.ring_size : E.b;
+        E.zcur = tail_init(C.bt, E.slot);
         if (hl < C.U) {
             const int tm = C.SS->team[hl];
             env_spawn_xyh(make_tables(spec, *C.SS), mlg_env_key(spec.seed, E.b), E.ep, hl, C.SS->team_first[tm],
@@ -1761,7 +1781,7 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     }
     if (E.st == 1) {  // final action recorded; env done (parallel_stepper.py:153)
         E.st = 2;
-        E.zcur = t + 1;
+        E.zcur = tail_start(E.zcur, t + 1);
         if (hl == 0) C.amask[E.e] = 0u;
         if (C.bt.full_write && hl == 0) {
             C.bt.reward[(int64_t)E.slot * T1 + t] = 0.f;
@@ -1858,11 +1878,11 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
 
 // Full-write mode: a finished env's half-wave zeroes a few more steps of its slot's tail.
 __device__ inline void env_lane_tail(const EnvCtx& C, EnvLane& E, int steps, int hl) {
-    if (!C.bt.full_write || E.st != 2 || E.zcur >= C.bt.T1 || E.b >= C.B) return;
-    const MlgEnvSpec& spec = *C.spec;
-    const int z1 = E.zcur + steps < C.bt.T1 ? E.zcur + steps : C.bt.T1;
-    zero_slot_steps(C.bt, E.slot, E.zcur, z1, C.N, C.A, 6 * C.U, 8 * C.U, hl, 32);
-    E.zcur = z1;
+    const int z0 = E.zcur & 0xFFFF, zend = E.zcur >> 16;
+    if (!C.bt.full_write || E.st != 2 || z0 >= zend || E.b >= C.B) return;
+    const int z1 = z0 + steps < zend ? z0 + steps : zend;
+    zero_slot_steps(C.bt, E.slot, z0, z1, C.N, C.A, 6 * C.U, 8 * C.U, hl, 32);
+    E.zcur = (E.zcur & ~0xFFFF) | z1;
 }
 
 // Per-env summary + env state write-back (+ the rest of the tail in full-write mode).
@@ -1871,6 +1891,7 @@ __device__ inline void env_lane_finish(const EnvCtx& C, const MlgEnvState& st, E
     const int U = C.U;
     if (C.bt.full_write) env_lane_tail(C, E, C.bt.T1, hl);
     if (hl == 0) {
+        if (C.bt.full_write && C.bt.slot_extent) C.bt.slot_extent[E.slot] = E.len + 1;
         C.info.ep_len[E.b] = E.len;
         C.info.ret[E.b] = E.ret;
         st.t[E.b] = E.len;
@@ -2055,7 +2076,7 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         sp.mark(4);
         env_lane_step2(Ce, E, t, hl, sp);
 #ifdef MLG_DUP_TAIL  // timing ablation: the tail zeroing twice over the same steps
-        if (!E.stepped && (t & 1)) { const int z0 = E.zcur; env_lane_tail(Ce, E, 8, hl); E.zcur = z0; }
+        if (!E.stepped && (t & 1)) { const int z0 = E.zcur; env_lane_tail(Ce, E, 8, hl); E.zcur = z0; }  // packed
 #endif
         if (!E.stepped && (t & 1)) env_lane_tail(Ce, E, 8, hl);
         sp.mark(8);

@@ -39,7 +39,7 @@ class MlgBatch(ctypes.Structure):
                 ("avail", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
                 ("actions_onehot", ctypes.c_void_p), ("filled", ctypes.c_void_p), ("B", ctypes.c_int32),
                 ("T1", ctypes.c_int32), ("ring_slot0", ctypes.c_int32), ("ring_size", ctypes.c_int32),
-                ("full_write", ctypes.c_int32), ("rows", ctypes.c_void_p)]
+                ("full_write", ctypes.c_int32), ("rows", ctypes.c_void_p), ("slot_extent", ctypes.c_void_p)]
 
 
 class MlgRunInfo(ctypes.Structure):
@@ -83,7 +83,7 @@ class MlgEntityBatch(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ["entities", "obs_mask", "entity_mask", "actions", "avail", "reward",
                                               "terminated", "actions_onehot", "filled"]] + \
                [(n, ctypes.c_int32) for n in ["B", "T1", "ring_slot0", "ring_size", "full_write"]] + \
-               [("rows", ctypes.c_void_p)]
+               [("rows", ctypes.c_void_p), ("slot_extent", ctypes.c_void_p)]
 
 
 class MlgRefilDims(ctypes.Structure):

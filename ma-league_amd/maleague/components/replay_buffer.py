@@ -20,6 +20,28 @@ class ReplayBuffer(EpisodeBatch):
         self.buffer_index = 0
         self.episodes_in_buffer = 0
         self._outstanding = []  # weakrefs to RingEpisodeBatches written into the ring but not inserted yet
+        # per slot: exclusive end of the rows that may hold non-zero data (max_seq_length = unknown). Rollouts in
+        # full-write ring mode zero only [L + 1, extent) of a slot they rewrite and record L + 1 (MlgBatch.slot_extent);
+        # every other write into the buffer (insert by copy) marks its slots unknown again.
+        self.slot_extent = (torch.full((buffer_size,), max_seq_length, dtype=torch.int32, device=device)
+                            if torch.device(device).type == "cuda" else None)
+
+    def update(self, data, bs=slice(None), ts=slice(None), mark_filled=True):
+        super().update(data, bs, ts, mark_filled)
+        self.invalidate_extents(bs)
+
+    def extent_ptr(self):
+        """Device pointer of the slot extents (None without them)."""
+        ext = getattr(self, "slot_extent", None)
+        return None if ext is None else ext.data_ptr()
+
+    def invalidate_extents(self, slots=None):
+        """Slots written by anything but a full-write rollout: their rows past any episode end are unknown."""
+        if getattr(self, "slot_extent", None) is not None:
+            if slots is None:
+                self.slot_extent.fill_(self.max_seq_length)
+            else:
+                self.slot_extent[slots] = self.max_seq_length
 
     def has_outstanding(self) -> bool:
         """True while a rollout's episodes sit in the ring's next slots uncommitted (written in place, not yet
@@ -57,6 +79,7 @@ class ReplayBuffer(EpisodeBatch):
             return
         dst = slice(self.buffer_index, self.buffer_index + ep_batch.batch_size)
         self._copy_in(ep_batch, dst)
+        self.invalidate_extents(dst)
         self.buffer_index += ep_batch.batch_size
         self.episodes_in_buffer = max(self.episodes_in_buffer, self.buffer_index)
         self.buffer_index %= self.buffer_size

@@ -348,6 +348,7 @@ class ParallelStepper(EnvStepper):
             # full-write mode: the kernel writes every byte of the B ring slots (zeros past each episode's end,
             # by the idle lanes of finished envs), so nothing is zero-initialised or copied
             mb.B, mb.ring_slot0, mb.ring_size, mb.full_write = self.batch_size, slot0, ring.buffer_size, 1
+            mb.slot_extent = ring.extent_ptr()
             self._launch_mb(mb, eps, test_mode)
             del keep
             self.home_batch = RingEpisodeBatch(ring, slot0, self.batch_size)

@@ -66,6 +66,7 @@ class SelfPlayParallelStepper(ParallelStepper):
             mb_h, k = mlg_batch(ring)
             keep.append(k)
             mb_h.B, mb_h.ring_slot0, mb_h.ring_size, mb_h.full_write = self.batch_size, slot0, ring.buffer_size, 1
+            mb_h.slot_extent = ring.extent_ptr()
             self.home_batch = RingEpisodeBatch(ring, slot0, self.batch_size)
         else:
             self.home_batch = self.new_batch_fn()
@@ -78,9 +79,14 @@ class SelfPlayParallelStepper(ParallelStepper):
             # batch per run (self_play_parallel_stepper.py:95).
             if self._away_buf is None:
                 self._away_buf = self.new_batch_fn()
+                # rows of each slot that may be non-zero (T1 = unknown): later runs zero only what the slot's
+                # previous episode wrote past the new episode's end
+                self._away_extent = torch.full((self.batch_size,), self.episode_limit + 1, dtype=torch.int32,
+                                               device=self.device)
             self.away_batch = self._away_buf
             mb_a, k = mlg_batch(self.away_batch)
             mb_a.full_write = 1
+            mb_a.slot_extent = self._away_extent.data_ptr()
         else:
             self.away_batch = self.new_batch_fn()
             mb_a, k = mlg_batch(self.away_batch)

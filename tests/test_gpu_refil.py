@@ -46,7 +46,8 @@ def test_agent_forward_matches_golden(device, golden):
     np.testing.assert_array_equal(Im.cpu().numpy(), d["imagine.Imask"])
 
 
-def _rollout(device, B=12, T=40, seed=5, eps=0.0, test_mode=True, ring=None, agent_seed=1, st=None, kmin=3, kmax=8):
+def _rollout(device, B=12, T=40, seed=5, eps=0.0, test_mode=True, ring=None, agent_seed=1, st=None, kmin=3, kmax=8,
+             batch=None, extent=None):
     from maleague import _native
     from maleague.components.episode_batch import EpisodeBatch
     from maleague.components.batch_view import mlg_entity_batch
@@ -59,13 +60,16 @@ def _rollout(device, B=12, T=40, seed=5, eps=0.0, test_mode=True, ring=None, age
     scheme, groups, pre = entity_scheme_for(info, torch)
     if st is None:
         st = VecEnvState(spec, B, device)
-    batch = EpisodeBatch(scheme, groups, B, T + 1, preprocess=pre, device=device)
-    if ring is not None:
-        for v in batch.data.transition_data.values():
-            v.fill_(7)
+    if batch is None:
+        batch = EpisodeBatch(scheme, groups, B, T + 1, preprocess=pre, device=device)
+        if ring is not None:
+            for v in batch.data.transition_data.values():
+                v.fill_(7)
     mb, keep = mlg_entity_batch(batch)
     if ring is not None:
         mb.full_write = 1
+    if extent is not None:
+        mb.slot_extent = extent.data_ptr()
     run = torch.zeros(6 * B, dtype=torch.int32, device=device)
     ri = _native.MlgRunInfo(run[0:B].data_ptr(), run[4 * B:5 * B].data_ptr(), run[B:3 * B].data_ptr(),
                             run[3 * B:4 * B].data_ptr(), None, None)
@@ -76,6 +80,8 @@ def _rollout(device, B=12, T=40, seed=5, eps=0.0, test_mode=True, ring=None, age
     r = run.cpu().numpy()
     summary = {"len": r[0:B], "won": r[B:3 * B].reshape(B, 2), "draw": r[3 * B:4 * B],
                "ret": r[4 * B:5 * B].view(np.float32)}
+    if extent is not None:
+        _rollout.last_batch = batch
     return spec, ag, a, np_batch(batch), summary, st
 
 
@@ -186,6 +192,23 @@ def test_rollout_ring_full_write_equals_zeroed(device, rollout_variant):
     for k in nb0:
         np.testing.assert_array_equal(nb0[k], nb1[k], err_msg=k)
     np.testing.assert_array_equal(s0["len"], s1["len"])
+
+
+def test_rollout_full_write_slot_extents(device, rollout_variant):
+    """full-write mode with slot extents (MlgEntityBatch.slot_extent): one batch rewritten by successive runs of
+    different episodes; each run zeroes only the rows past its episodes' ends that the previous episode in the slot
+    wrote, records L + 1, and the batch equals a zero-initialised one every time."""
+    B, T = 10, 30
+    ext = torch.full((B,), T + 1, dtype=torch.int32, device=device)  # rows unknown: a fresh garbage-filled batch
+    batch = None
+    for it, (seed, eps) in enumerate([(9, 0.2), (3, 0.6), (9, 0.0), (5, 0.3)]):
+        *_, nb0, s0, _ = _rollout(device, B=B, T=T, seed=seed, eps=eps, test_mode=False)  # zero-initialised
+        *_, nb1, s1, _ = _rollout(device, B=B, T=T, seed=seed, eps=eps, test_mode=False, ring=True, batch=batch,
+                                  extent=ext)
+        batch = _rollout.last_batch
+        for k in nb0:
+            np.testing.assert_array_equal(nb0[k], nb1[k], err_msg=f"{it} {k}")
+        np.testing.assert_array_equal(ext.cpu().numpy(), s1["len"] + 1)
 
 
 def test_rollout_fixed_team_sizes(device, rollout_variant):

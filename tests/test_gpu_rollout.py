@@ -368,6 +368,10 @@ def test_rollout_ring_mode_zero_copy_insert(device, kernel, monkeypatch):
         ring.insert_episode_batch(b_ring)
         ref.insert_episode_batch(b_plain)
         assert (ring.buffer_index, ring.episodes_in_buffer) == (ref.buffer_index, ref.episodes_in_buffer)
+        # slot extents (MlgBatch.slot_extent): the run's slots now hold rows [0, L] of their episodes
+        slots = (torch.arange(48) + b_ring.slot0) % 100
+        want = (stepper.last_run["ep_len"] + 1).to(torch.int32)
+        assert torch.equal(ring.slot_extent.cpu()[slots], want), (it, kernel)
     for k in ref.data.transition_data:
         n = ref.episodes_in_buffer
         assert torch.equal(ring[k][:n], ref[k][:n]), k

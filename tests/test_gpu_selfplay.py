@@ -132,7 +132,9 @@ def test_selfplay_identical_policies_symmetric(device):
 
 def test_selfplay_ring_mode_equals_plain(device):
     """Home episodes written straight into the replay ring, and away episodes written in full-write mode into the
-    reused away batch (pre-filled with garbage), equal the zero-initialised EpisodeBatches."""
+    reused away batch, equal the zero-initialised EpisodeBatches. Run 0 writes over garbage (extents unknown);
+    later runs reuse slots holding the previous run's episodes (only the rows past the new end that the old
+    episode wrote are zeroed: MlgBatch.slot_extent)."""
     from maleague.components.replay_buffer import ReplayBuffer
     from maleague.envs.teams_env import VecEnvState
     stepper, home, away, args = _build(device, B=48, episode_limit=30, seed=2)
@@ -155,10 +157,13 @@ def test_selfplay_ring_mode_equals_plain(device):
         stepper.envs = st1
         assert stepper.attach_replay(ring)
         stepper.args.reuse_away_batch = True
-        if stepper._away_buf is not None:
+        if stepper._away_buf is not None and it == 1:
             for v in stepper._away_buf.data.transition_data.values():
                 v.fill_(7)
+            stepper._away_extent.fill_(31)  # written from outside: rows unknown
         hr, ar, _ = stepper.run(test_mode=False)
+        L = stepper.last_run["ep_len"]
+        assert torch.equal(stepper._away_extent.cpu(), (L + 1).to(torch.int32))
         assert ar is not ap
         for k in hp.data.transition_data:
             assert torch.equal(hp[k], hr[k]), (it, k)
