@@ -40,6 +40,7 @@ import torch  # noqa: E402
 
 FP32_MFMA_PEAK = 157.3e12  # MI355X dense fp32 (MFMA == VALU rate), MI355X_MICROARCH.md chip table
 HBM_PEAK = 8.0e12
+TIMING_EVERY = 1  # HIP-event pair around every k-th rollout launch of the timed region (--timing-every)
 METRIC = "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X"
 COUNTERS_JSON = os.path.join(ROOT, "profiles", "counters.json")
 
@@ -101,6 +102,7 @@ def timed_loop(ctx: Ctx, iteration, stepper, steps: int, warmup: int) -> dict:
     ctx.barrier()
     timing_ok = ctx.dev.type == "cuda"
     stepper.timing = [] if timing_ok else None
+    stepper.timing_every = TIMING_EVERY
     t0_env = stepper.t_env
     rows0 = int(stepper.agent_rows.item())
     ctx.sync()
@@ -227,6 +229,9 @@ def roofline(mode, stepper, r, steps, B):
         fl = sides * agent_flops_per_forward(N, info["obs_shape"] + A + N, 64, A)
     # agent forwards per launch: every env steps len times and records one final action (len + 1 forwards)
     forwards = (r["local_env_steps"] + steps * B) / steps
+    if r["avg_kernel_ms"] is None:  # --timing-every 0 (A/B runs): no kernel timing
+        return {"bound": "mfma", "achieved": None, "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": None,
+                "traffic": None, "kernel": kernel_names(mode, N, A), "avg_kernel_ms": None}
     avg_s = r["avg_kernel_ms"] / 1e3
     achieved = fl * forwards / avg_s
     kernel = kernel_names(mode, N, A, kc1)
@@ -331,10 +336,14 @@ def main():
     ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timing-every", type=int, default=1,
+                    help="HIP events around every k-th rollout launch of the timed region (0: none, A/B only)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / process-group plumbing only: init the group, report the world, run no leg")
     argv = sys.argv[1:]
     a = ap.parse_args(argv)
+    global TIMING_EVERY
+    TIMING_EVERY = a.timing_every
     # stdout carries exactly one line, the JSON result: native libraries (RCCL prints a version banner on its first
     # communicator) write to fd 1, so fd 1 is pointed at stderr and the result goes to a saved copy of stdout
     out_fd = os.dup(1)

@@ -114,7 +114,9 @@ class ParallelStepper(EnvStepper):
         self.home_mac = None
         self.home_batch = None
         self.away_mac = None  # self-play only (SelfPlayParallelStepper)
-        self.timing = None  # list -> (start, end) HIP events around every rollout launch (bench.py)
+        self.timing = None  # list -> (start, end) HIP events around rollout launches (bench.py)
+        self.timing_every = 1  # time every k-th launch only (an event pair costs a few us of GPU queue time)
+        self._launches = 0
         self._ring = None   # ReplayBuffer written in place (zero-copy insert), see attach_replay()
 
     _batch_keys = ("state", "obs", "actions", "avail_actions", "reward", "terminated", "actions_onehot", "filled")
@@ -319,10 +321,14 @@ class ParallelStepper(EnvStepper):
                                   info[3 * B:4 * B].data_ptr(), self.agent_rows.data_ptr(),
                                   info[5 * B:6 * B].data_ptr())
 
+    def _timed_launch(self) -> bool:
+        self._launches += 1
+        return self.timing is not None and self.timing_every > 0 and self._launches % self.timing_every == 0
+
     def _launch_mb(self, mb, epsilon: float, test_mode: bool):
         run_info = self._run_info()
         ev = None
-        if self.timing is not None:
+        if self._timed_launch():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         self._rollout(mb, run_info, epsilon, test_mode)

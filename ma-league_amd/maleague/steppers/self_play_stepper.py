@@ -98,7 +98,7 @@ class SelfPlayParallelStepper(ParallelStepper):
         st = self.envs.to_c()
         run_info = self._run_info()
         ev = None
-        if self.timing is not None:
+        if self._timed_launch():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         _native.call("mlg_rollout_selfplay", _native.byref(self._cspec), _native.byref(st), _native.byref(d),

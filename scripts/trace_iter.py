@@ -6,6 +6,11 @@ import sys
 from collections import defaultdict
 
 
+def short(name):
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "").replace("at::native::", "")
+    return n.split("(")[0][:90]
+
+
 def main():
     path, key = sys.argv[1], sys.argv[2]
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 4
@@ -25,7 +30,7 @@ def main():
         span += (rows[b][0] - rows[a][0]) / 1e3
         prev_end = None
         for r in rows[a:b]:
-            nm = r[2].split("(")[0][-70:]
+            nm = short(r[2])
             tot[nm] += (r[1] - r[0]) / 1e3
             cnt[nm] += 1
             if prev_end is not None:
@@ -42,7 +47,7 @@ def main():
     prev_end = None
     for r in rows[a:b]:
         gap = (r[0] - prev_end) / 1e3 if prev_end is not None else 0.0
-        print(f"  {(r[0] - t0) / 1e3:9.1f} {(r[1] - r[0]) / 1e3:8.1f} {gap:7.1f}  {r[2].split('(')[0][-80:]}")
+        print(f"  {(r[0] - t0) / 1e3:9.1f} {(r[1] - r[0]) / 1e3:8.1f} {gap:7.1f}  {short(r[2])}")
         prev_end = max(prev_end or 0, r[1])
 
 
