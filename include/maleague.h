@@ -300,11 +300,15 @@ typedef struct {
     float *workspace;            /* mlg_refil_workspace_floats() floats */
     float *stats;                /* [8] out: loss, im_loss, grad_norm, td_error_abs, q_taken_mean, target_mean,
                                     mask_sum, 0 */
+    double *trained_steps;       /* optional [1] += mask_sum (Agent.trained_steps, refil_learner.py:176) */
 } MlgRefilLearnerBufs;
 
 int64_t mlg_refil_param_counts(const MlgRefilLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);
 int64_t mlg_refil_workspace_floats(const MlgRefilLearnerCfg *c);
 int mlg_refil_train(const MlgRefilLearnerCfg *c, const MlgRefilLearnerBufs *b, void *stream);
+/* The imagine group draw of a train call (entity_rnn_agent.py:95-97: p_b = rand per episode, groupA[b][j] =
+ * bernoulli(p_b)) on the device, counter-based from (seed, draw): one launch into groupA [B][NE]. */
+int mlg_refil_draw_groups(int32_t B, int32_t NE, uint64_t seed, uint32_t draw, uint8_t *groupA, void *stream);
 
 /* Diagnostic builds only (-DMLG_STAMPS): device buffer [grid][8 waves][16] u64 of per-phase cycle counts
  * of mlg_rollout. Returns nonzero in normal builds. */
@@ -312,6 +316,13 @@ int mlg_debug_set_stamps(void *ptr);
 /* Diagnostic builds only (-DMLG_STAMPS): per-wave phase cycle counters of the learner recurrences. */
 int mlg_debug_set_learner_stamps(void *ptr);
 int mlg_refil_debug_set_stamps(void *ptr); /* same for mlg_refil_rollout: [grid][16] u64 */
+
+/* League payoff bookkeeping of one batched self-play run (league_experiment_process.py:85-105, _extract_result +
+ * _update_payoff per env): entry = the league's local payoff delta [GAMES, WIN, LOSS, DRAW, ...] of (home, away);
+ * won [B][2] (policy team first), draw [B] as written by mlg_rollout_selfplay. DRAW if draw or both / no team won,
+ * else WIN / LOSS by won[b][0]; GAMES += B when count_games (the reference never counts GAMES). One launch. */
+int mlg_league_record_runs(const int32_t *won, const int32_t *draw, int32_t B, float *entry, int32_t count_games,
+                           void *stream);
 
 const char *mlg_last_error(void);
 const char *mlg_version(void);

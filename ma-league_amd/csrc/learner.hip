@@ -1524,12 +1524,19 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
         }
         if (g == 0) o.dv2[rm] = dy;
     }
-    if (valid && g == 0) {  // dQ per agent row (t-major) and its one-hot expansion for dW2
+    if (valid && g == 0) {  // dQ per agent row (t-major) and its one-hot expansion for dW2: whole rows (no memset
+                            // pass); the lane of t = T - 2 also zeroes the rows of t = T - 1, which no lane owns
         for (int n = 0; n < N; ++n) {
             const int r = b * N + n;
             o.dq[(int64_t)t * c.R + r] = dq[n];
             const int a = (int)bt.actions[(bslot(bt, b) * bt.T1 + t) * N + n];
-            o.d2[((int64_t)t * c.R + r) * c.A + a] = dq[n];
+            float* d2r = o.d2 + ((int64_t)t * c.R + r) * c.A;
+            for (int a2 = 0; a2 < c.A; ++a2) d2r[a2] = a2 == a ? dq[n] : 0.f;
+            if (t == Tm - 1) {
+                o.dq[(int64_t)(t + 1) * c.R + r] = 0.f;
+                float* d2z = o.d2 + ((int64_t)(t + 1) * c.R + r) * c.A;
+                for (int a2 = 0; a2 < c.A; ++a2) d2z[a2] = 0.f;
+            }
         }
     }
 }
@@ -2044,10 +2051,17 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     pj.E = c.E;
     pj.HE = c.HE;
     pj.mixer = c.mixer;
-    pj.d2 = ws + p.w.d2;  // d2 is sparse: zero it (and dq) every call
+    // split mixer (default for the FAST shapes): the hypernetwork forward rides in the recurrence launch
+    // (rec4_mixpre_kernel), mix_td2_kernel does the rest; MLG_MIX_FUSED=1: the one-kernel mix_td
+    static const bool rec16 = getenv("MLG_LEARNER_REC16") != nullptr;  // A/B switch: the 16-row tile recurrence
+    const bool fast_mix = p.mp.Sp <= 64 && c.N <= MIXPF_N && c.A <= MIXPF_A && !getenv("MLG_MIX_GENERIC");
+    static const bool fused_env = getenv("MLG_MIX_FUSED") != nullptr;
+    const int threads = (c.H / 16) * 64;
+    const bool split_mix = c.mixer == 2 && fast_mix && !fused_env && !rec16 && threads % 128 == 0;
+    pj.d2 = ws + p.w.d2;  // d2 is sparse: zeroed (with dq) here unless mix_td2 writes whole rows (split mixer)
     pj.dq = ws + p.w.dq;
-    pj.n_d2 = (int64_t)c.T * c.R * c.A;
-    pj.n_dq = (int64_t)c.T * c.R;
+    pj.n_d2 = split_mix ? 0 : (int64_t)c.T * c.R * c.A;
+    pj.n_dq = split_mix ? 0 : (int64_t)c.T * c.R;
     pj.bt = bt;
     pj.B = c.B;
     pj.T = c.T;
@@ -2084,13 +2098,6 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
         Mtg = ptrs(tparams, ws + p.w.mix_tg);
     }
     const int ntiles = (c.R + 15) / 16;
-    const int threads = (c.H / 16) * 64;
-    // split mixer (default for the FAST shapes): the hypernetwork forward rides in the recurrence launch
-    // (rec4_mixpre_kernel), mix_td2_kernel does the rest; MLG_MIX_FUSED=1: the one-kernel mix_td
-    static const bool rec16 = getenv("MLG_LEARNER_REC16") != nullptr;  // A/B switch: the 16-row tile recurrence
-    const bool fast_mix = p.mp.Sp <= 64 && c.N <= MIXPF_N && c.A <= MIXPF_A && !getenv("MLG_MIX_GENERIC");
-    static const bool fused_env = getenv("MLG_MIX_FUSED") != nullptr;
-    const bool split_mix = c.mixer == 2 && fast_mix && !fused_env && !rec16 && threads % 128 == 0;
     HypOut hy{ws + p.w.hyp_on, ws + p.w.hyp_tg, ws + p.w.l1act, ws + p.w.srow, p.w.hyp_stride};
     hipLaunchKernelGGL((agent_in_kernel<H>), dim3(ntiles, c.T, 2), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                        ws + p.w.p_tg, ws + p.w.in, ws + p.w.x, ws + p.w.gi_on, ws + p.w.gi_tg, ws + p.w.msum);

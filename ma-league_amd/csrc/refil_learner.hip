@@ -861,6 +861,13 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, M
     float* part = io.part + (int64_t)i * 8;
     if (t >= Te - 1) {  // t = T - 1, or past max_t_filled (mask 0): no loss, zero deltas
         if (lane < 8) part[lane] = 0.f;
+        // dQ / d2 rows of the item's (copy, agent) rows: zeros (the item owns them; no memset pass)
+        for (int q = lane; q < 3 * c.NA * (c.A + 1); q += 64) {
+            const int cc = q / (c.NA * (c.A + 1)), rem = q % (c.NA * (c.A + 1)), n = rem / (c.A + 1), a2 = rem % (c.A + 1);
+            const int64_t row = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * c.NA + n;
+            if (a2 == c.A) io.dq[row] = 0.f;
+            else io.d2[row * c.A + a2] = 0.f;
+        }
         for (int k = 0; k < 4; ++k)
             for (int v = 0; v < nvar(k); ++v)
                 for (int q = lane; q < NAS * EM; q += 64) io.dX[k][((int64_t)v * c.I + i) * NAS * EM + q] = 0.f;
@@ -1007,7 +1014,7 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, M
             const int64_t row = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * NA + n;
             const float v = live ? dd[cc] : 0.f;
             io.dq[row] = v;
-            io.d2[row * c.A + act[n]] = v;
+            for (int a2 = 0; a2 < c.A; ++a2) io.d2[row * c.A + a2] = a2 == act[n] ? v : 0.f;  // whole row: no memset
         }
     }
 }
@@ -1321,7 +1328,8 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
                                                       float* __restrict__ grads, float* __restrict__ sq, int64_t n_params,
                                                       float lr, float alpha, float eps, float max_norm, int NA,
                                                       float lmbda, float* __restrict__ stats,
-                                                      const float* __restrict__ nrm_part, int n_nrm) {
+                                                      const float* __restrict__ nrm_part, int n_nrm,
+                                                      double* __restrict__ trained) {
     __shared__ float red[1024];
     const int tid = threadIdx.x;
     float s = 0.f;
@@ -1354,6 +1362,7 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
             stats[5] = s5[4] / (ms * NA);
             stats[6] = ms;
             stats[7] = 0.f;
+            if (trained) trained[0] += (double)ms;
         }
     }
 }
@@ -1454,8 +1463,6 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     hipLaunchKernelGGL(hyper_splitT_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 5), dim3(256), 0, s, hsT);
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((3 * EMB * EMB + 255) / 256), (unsigned)tj.n), dim3(256), 0, s,
                        tj);
-    (void)hipMemsetAsync(ws + w.d2, 0, sizeof(float) * (size_t)c.T * c.Ron * c.A, s);
-    (void)hipMemsetAsync(ws + w.dq, 0, sizeof(float) * (size_t)c.T * c.Ron, s);
     hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + w.msum);
     const int64_t n_ein = (int64_t)c.I * NE * c.K1;
     hipLaunchKernelGGL(ein_kernel, dim3((unsigned)((n_ein + 255) / 256)), dim3(256), 0, s, c, bt, ws + w.ein);
@@ -1533,7 +1540,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     const int64_t n_par = p.n_agent + p.n_mixer;
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + w.part, c.I,
                        ws + w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr, cfg->optim_alpha,
-                       cfg->optim_eps, cfg->grad_norm_clip, c.NA, c.lmbda, bufs->stats, ws + p.w.nrm, n_red_blocks);
+                       cfg->optim_eps, cfg->grad_norm_clip, c.NA, c.lmbda, bufs->stats, ws + p.w.nrm, n_red_blocks,
+                       bufs->trained_steps);
     return mlg::check_launch("refil_train");
 }
 
@@ -1554,6 +1562,27 @@ extern "C" int64_t mlg_refil_workspace_floats(const MlgRefilLearnerCfg* c) {
     int tasks;
     make_jobs(p, nullptr, nullptr, &slab, &tasks, &n_red);
     return p.w.total + slab;
+}
+
+namespace {
+// ---- the imagine group draw (entity_rnn_agent.py:95-97) on the device: p_b ~ U(0, 1) per episode, then entity j of
+// episode b in group A with probability p_b. Counter-based (mlg_rng: key = seed, counter = (draw, b, purpose 5,
+// j + 1)); like the reference's th.rand / th.bernoulli it is a random draw, not a bit-reproduction of torch's stream.
+__global__ void refil_groups_kernel(int B, int NE, uint64_t seed, uint32_t draw, uint8_t* __restrict__ groupA) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= B * NE) return;
+    const int b = k / NE, j = k % NE;
+    const float p = mlg_u01(mlg_rng(seed, mlg_ctr(draw, (uint32_t)b, 5u, 0u)));
+    groupA[k] = (uint8_t)(mlg_u01(mlg_rng(seed, mlg_ctr(draw, (uint32_t)b, 5u, (uint32_t)j + 1u))) < p);
+}
+}  // namespace
+
+extern "C" int mlg_refil_draw_groups(int32_t B, int32_t NE, uint64_t seed, uint32_t draw, uint8_t* groupA,
+                                     void* stream) {
+    MLG_REQUIRE(groupA && B >= 1 && NE >= 1 && NE <= 4096, "refil_draw_groups: B=%d NE=%d", B, NE);
+    hipLaunchKernelGGL(refil_groups_kernel, dim3((unsigned)((B * NE + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       B, NE, seed, draw, groupA);
+    return mlg::check_launch("refil_draw_groups");
 }
 
 extern "C" int mlg_refil_train(const MlgRefilLearnerCfg* c, const MlgRefilLearnerBufs* b, void* stream) {

@@ -103,7 +103,8 @@ class MlgRefilLearnerCfg(ctypes.Structure):
 
 class MlgRefilLearnerBufs(ctypes.Structure):
     _fields_ = [("batch", MlgEntityBatch)] + [(n, ctypes.c_void_p) for n in ["groupA", "params", "grads", "square_avg",
-                                                                           "target_params", "workspace", "stats"]]
+                                                                           "target_params", "workspace", "stats",
+                                                                           "trained_steps"]]
 
 
 _P = ctypes.c_void_p
@@ -140,6 +141,8 @@ SIGNATURES = {
     "mlg_debug_set_stamps": (ctypes.c_int, [_P]),
     "mlg_debug_set_learner_stamps": (ctypes.c_int, [_P]),
     "mlg_refil_debug_set_stamps": (ctypes.c_int, [_P]),
+    "mlg_league_record_runs": (ctypes.c_int, [_P, _P, _I, _P, _I, _P]),
+    "mlg_refil_draw_groups": (ctypes.c_int, [_I, _I, ctypes.c_uint64, ctypes.c_uint32, _P, _P]),
     "mlg_last_error": (ctypes.c_char_p, []),
     "mlg_version": (ctypes.c_char_p, []),
 }

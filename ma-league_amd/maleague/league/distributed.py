@@ -65,7 +65,15 @@ class DistributedLeague:
     def record_runs(self, home: int, away: int, won: torch.Tensor, draw: torch.Tensor):
         """Episode results of one batched run, on the device (no host sync): _extract_result +
         _update_payoff (league_experiment_process.py:85-105) for every env. won [B, 2] (policy team first),
-        draw [B]; DRAW if the env says so or if both / no team won, else WIN / LOSS by won[:, 0]."""
+        draw [B]; DRAW if the env says so or if both / no team won, else WIN / LOSS by won[:, 0]. Device tensors: one
+        mlg_league_record_runs launch; host tensors (CPU rehearsals / tests): the same reduction in torch."""
+        if self._delta.is_cuda:
+            from .. import _native
+            entry = self._delta[home, away]
+            _native.call("mlg_league_record_runs", _native.ptr(won.contiguous()), _native.ptr(draw.contiguous()),
+                         int(won.shape[0]), entry.data_ptr(), int(not self.payoff.reference_compat),
+                         _native.stream_ptr(self.device))
+            return
         w0, w1 = won[:, 0] != 0, won[:, 1] != 0
         d = (draw != 0) | (w0 == w1)
         win = ~d & w0

@@ -45,6 +45,8 @@ class REFILLearner(Learner):
         self._last_stats = None
         self._stats_fresh = False
         self.train_calls = 0
+        self._groups = None  # device buffer of the imagine group draw
+        self._group_seed = (int(getattr(args, "seed", 0)) << 32) ^ 0x5EF11  # key of the draw's counter-based RNG
 
     def parameters(self):
         return list(self.mac.parameters()) + list(self.mixer.parameters())
@@ -105,14 +107,19 @@ class REFILLearner(Learner):
         if self._ws is None or self._ws.numel() < need:
             self._ws = None
             self._ws = torch.zeros(int(need * 1.1) + 1024, dtype=torch.float32, device=self.device)
-        if groupA is None:
-            p = torch.rand(B, 1, device=self.device).expand(B, NE)
-            groupA = torch.bernoulli(p).to(torch.uint8)
+        if groupA is None:  # drawn on the device: one launch (mlg_refil_draw_groups), counter = train call
+            if self._groups is None or self._groups.shape != (B, NE):
+                self._groups = torch.empty(B, NE, dtype=torch.uint8, device=self.device)
+            groupA = self._groups
+            _native.call("mlg_refil_draw_groups", B, NE, self._group_seed, self.train_calls & 0xFFFFFFFF,
+                         groupA.data_ptr(), _native.stream_ptr(self.device))
         groupA = groupA.reshape(B, NE).to(device=self.device, dtype=torch.uint8).contiguous()
         mb, keep = mlg_entity_batch(batch)
+        # trained steps accumulate on the device inside the optimizer launch (no separate add)
+        counter = self.mac.agent.trained_counter(self.device)
         bufs = _native.MlgRefilLearnerBufs(mb, groupA.data_ptr(), self._flat.flat.data_ptr(), self._grads.data_ptr(),
                                            self._sq.data_ptr(), self._tflat.flat.data_ptr(), self._ws.data_ptr(),
-                                           self._stats.data_ptr())
+                                           self._stats.data_ptr(), counter.data_ptr())
         _native.call("mlg_refil_train", _native.byref(cfg), _native.byref(bufs), _native.stream_ptr(self.device))
         del keep
         self._groupA = groupA
@@ -122,7 +129,6 @@ class REFILLearner(Learner):
         if (episode_num - self.last_target_update_episode) / self.args.target_update_interval >= 1.0:
             self.update_targets()
             self.last_target_update_episode = episode_num
-        self.mac.update_trained_steps(self._stats[6])
         self._stats_fresh = True
         if callable(t_env):  # lazily resolved t_env: the kernels above are already queued
             up = getattr(t_env, "upper", None)

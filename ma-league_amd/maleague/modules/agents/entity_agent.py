@@ -45,9 +45,22 @@ class EntityAttentionRNNAgent(AgentNetwork):
         self._dirty += 1
 
     def flat_parameters(self) -> torch.Tensor:
-        """named_parameters() concatenated (the canonical order the C ABI documents)."""
+        """named_parameters() concatenated (the canonical order the C ABI documents). When the parameters already are
+        consecutive views of one fp32 buffer (a learner's FlatParams), that buffer itself: no copy, no launch."""
+        params = list(self.parameters())
+        p0 = params[0]
+        if all(p.dtype == torch.float32 and p.is_contiguous() for p in params):
+            off, ok = p0.data_ptr(), True
+            for p in params:
+                if p.data_ptr() != off or p.untyped_storage().data_ptr() != p0.untyped_storage().data_ptr():
+                    ok = False
+                    break
+                off += 4 * p.numel()
+            if ok:
+                n = sum(p.numel() for p in params)
+                return p0.detach().new_empty(0).set_(p0.untyped_storage(), p0.storage_offset(), (n,), (1,))
         with torch.no_grad():
-            return torch.cat([p.detach().float().reshape(-1) for p in self.parameters()])
+            return torch.cat([p.detach().float().reshape(-1) for p in params])
 
     def packed(self) -> torch.Tensor:
         params = list(self.parameters())
@@ -73,7 +86,12 @@ class EntityAttentionRNNAgent(AgentNetwork):
 
     # ---- reference API -------------------------------------------------------------------------
     def init_hidden(self):
-        return self.fc1.weight.new(1, self.args.rnn_hidden_dim).zero_()
+        """A zero [1, H] state, cached per device (callers expand it and never write into it): no fill per run."""
+        w = self.fc1.weight
+        h0 = getattr(self, "_h0", None)
+        if h0 is None or h0.device != w.device or h0.dtype != w.dtype:
+            self._h0 = h0 = w.new_zeros(1, self.args.rnn_hidden_dim)
+        return h0
 
     def forward(self, inputs, hidden_state, ret_attn_logits=None):
         """inputs = (entities [bs, ts, ne, ed], obs_mask [bs, ts, ne, ne], entity_mask [bs, ts, ne]);

@@ -76,6 +76,27 @@ def test_refil_learner_two_calls_match_golden(device, golden):
                                        err_msg=f"call {call} mixer {k}")
     # the reference REFIL learner logs unprefixed keys (refil_learner.py:185-195), im_loss for imagine agents
     assert set(log.stats) == {"loss", "im_loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"}
+    # Agent.trained_steps += mask.sum() per call (refil_learner.py:176), counted by the optimizer launch
+    assert L.mac.agent.trained_steps == 2 * int(round(float(L._stats[6].item())))
+
+
+def test_refil_device_group_draw(device):
+    """The imagine group draw on the device (mlg_refil_draw_groups, entity_rnn_agent.py:95-97: p_b ~ U(0,1) per
+    episode, entities in group A with probability p_b): deterministic per (seed, draw), fresh per draw, and
+    distributed like the reference's draw (overall rate 1/2, per-episode rates spread like U(0,1))."""
+    from maleague import _native
+    B, NE = 4096, 16
+    out = [torch.empty(B, NE, dtype=torch.uint8, device=device) for _ in range(3)]
+    for o, draw in zip(out, (7, 7, 8)):
+        _native.call("mlg_refil_draw_groups", B, NE, 1234, draw, o.data_ptr(), _native.stream_ptr())
+    g = [o.cpu().numpy() for o in out]
+    assert np.array_equal(g[0], g[1]) and not np.array_equal(g[0], g[2])
+    assert set(np.unique(g[0])) <= {0, 1}
+    rate = g[0].mean(axis=1)
+    assert abs(rate.mean() - 0.5) < 0.02
+    # per-episode rate ~ p_b: variance = Var(p) + E[p(1-p)] / NE = 1/12 + 1/(6 NE)
+    assert abs(rate.var() - (1 / 12 + 1 / (6 * NE))) < 0.01
+    assert (rate == 0).mean() > 0.01 and (rate == 1).mean() > 0.01
 
 
 @pytest.mark.parametrize("softmax,double_q", [(False, True), (True, False)])

@@ -329,3 +329,21 @@ def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, monkeypatch):
     assert worst <= 1e-5, worst
     n_diff = assert_near_tie_divergence(out["sp2"][0], nbs, qs, B)  # only near-tie flips diverge
     assert n_diff <= B // 10, n_diff
+
+
+@pytest.mark.parametrize("compat", [False, True])
+def test_league_record_runs_device_kernel(device, compat):
+    """DistributedLeague.record_runs on device tensors (one mlg_league_record_runs launch) == the host-side reduction
+    (league_experiment_process.py:85-105): wins / losses / draws (incl. both- and no-team-won) and GAMES."""
+    from maleague.league import DistributedLeague
+    rng = np.random.RandomState(3)
+    B = 4096
+    won = rng.randint(0, 2, size=(B, 2)).astype(np.int32)
+    draw = (rng.rand(B) < 0.2).astype(np.int32)
+    lg_d = DistributedLeague(n_players=3, device=device, reference_compat=compat)
+    lg_h = DistributedLeague(n_players=3, device="cpu", reference_compat=compat)
+    for home, away in ((0, 2), (1, 1), (0, 2)):
+        lg_d.record_runs(home, away, torch.from_numpy(won).to(device), torch.from_numpy(draw).to(device))
+        lg_h.record_runs(home, away, torch.from_numpy(won), torch.from_numpy(draw))
+    np.testing.assert_array_equal(lg_d._delta.cpu().numpy(), lg_h._delta.numpy())
+    assert lg_h._delta[0, 2, 1:4].sum() == 2 * B
