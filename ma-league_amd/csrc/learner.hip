@@ -1524,19 +1524,13 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
         }
         if (g == 0) o.dv2[rm] = dy;
     }
-    if (valid && g == 0) {  // dQ per agent row (t-major) and its one-hot expansion for dW2: whole rows (no memset
-                            // pass); the lane of t = T - 2 also zeroes the rows of t = T - 1, which no lane owns
+    if (valid && g == 0) {  // dQ per agent row (t-major) and its one-hot expansion for dW2 (d2 zeroed by prep_kernel:
+                            // whole-row writes here measured 3.7 us slower, and the zeroing is off prep's critical path)
         for (int n = 0; n < N; ++n) {
             const int r = b * N + n;
             o.dq[(int64_t)t * c.R + r] = dq[n];
             const int a = (int)bt.actions[(bslot(bt, b) * bt.T1 + t) * N + n];
-            float* d2r = o.d2 + ((int64_t)t * c.R + r) * c.A;
-            for (int a2 = 0; a2 < c.A; ++a2) d2r[a2] = a2 == a ? dq[n] : 0.f;
-            if (t == Tm - 1) {
-                o.dq[(int64_t)(t + 1) * c.R + r] = 0.f;
-                float* d2z = o.d2 + ((int64_t)(t + 1) * c.R + r) * c.A;
-                for (int a2 = 0; a2 < c.A; ++a2) d2z[a2] = 0.f;
-            }
+            o.d2[((int64_t)t * c.R + r) * c.A + a] = dq[n];
         }
     }
 }
@@ -2058,10 +2052,10 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     static const bool fused_env = getenv("MLG_MIX_FUSED") != nullptr;
     const int threads = (c.H / 16) * 64;
     const bool split_mix = c.mixer == 2 && fast_mix && !fused_env && !rec16 && threads % 128 == 0;
-    pj.d2 = ws + p.w.d2;  // d2 is sparse: zeroed (with dq) here unless mix_td2 writes whole rows (split mixer)
+    pj.d2 = ws + p.w.d2;  // d2 is sparse: zero it (and dq) every call
     pj.dq = ws + p.w.dq;
-    pj.n_d2 = split_mix ? 0 : (int64_t)c.T * c.R * c.A;
-    pj.n_dq = split_mix ? 0 : (int64_t)c.T * c.R;
+    pj.n_d2 = (int64_t)c.T * c.R * c.A;
+    pj.n_dq = (int64_t)c.T * c.R;
     pj.bt = bt;
     pj.B = c.B;
     pj.T = c.T;
