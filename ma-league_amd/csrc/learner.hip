@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "agent_device.h"
+#include "gru4_device.h"
 #include "mlg_host.h"
 #include "wgrad_device.h"
 
@@ -310,13 +311,6 @@ __device__ __forceinline__ int t_eff(const float* msum) { return min((int)msum[1
 __device__ __forceinline__ int t_eff(const float* msum) { return (int)msum[1]; }
 #endif
 
-// prefetch depth (steps) of the recurrences' per-step operand rings (even: the LDS double buffer alternates)
-#ifndef MLG_REC_PD
-#define MLG_REC_PD 4
-#endif
-#ifndef MLG_BWD_PD
-#define MLG_BWD_PD 4
-#endif
 
 // ================================================================================================
 // 16-row x 16-feature tile product with the activation operand in LDS, row-major [16][lda]:
@@ -502,112 +496,14 @@ __device__ __forceinline__ void agent_rec4_body(const LCfg& c, const AgentLayout
                                                 float* __restrict__ hs_tg, float* __restrict__ ws_gr,
                                                 float* __restrict__ ws_gz, float* __restrict__ ws_gn,
                                                 float* __restrict__ ws_ghn, const float* __restrict__ msum, int bid) {
-    constexpr int LDA = H + 4;
-    __shared__ __attribute__((aligned(16))) float hs[2][4 * LDA];
     LStamps lst;
     lst.init();
-    const int Te = t_eff(msum);
     const int nt4 = (c.R + 3) / 4;
     const bool online = bid < nt4;
-    const int tile = online ? bid : bid - nt4;
     const float* P = online ? Pon : Ptg;
-    const float* gi = online ? gi_on : gi_tg;
-    float* hsg = online ? hs_on : hs_tg;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int b = lane >> 2, q = lane & 3;  // block, and i (A / D register) or j (B / D column = row)
-    const int g = b >> 2, fg = b & 3;
-    const int R = c.R;
-    const int r = tile * 4 + q;  // this lane's row as a B / D column
-    const bool valid = r < R;
-    const int rr = valid ? r : 0;
-    const int fA = 16 * w + 4 * fg + q;  // A operand: feature row of W_hh for this lane (i = q)
-    const int fD = 16 * w + 4 * fg;      // D: features fD..fD+3 of gate g at row r
-    const int f = fD + g;                // after the transpose: the lane's cell is (feature f, row r)
-    float wa[H];
-#pragma unroll
-    for (int k4 = 0; k4 < H / 4; ++k4) {
-        const floatx4 v = g < 3 ? ld4(P + L.whh + (int64_t)(g * H + fA) * H + 4 * k4) : floatx4{0.f, 0.f, 0.f, 0.f};
-        wa[4 * k4] = v.x;
-        wa[4 * k4 + 1] = v.y;
-        wa[4 * k4 + 2] = v.z;
-        wa[4 * k4 + 3] = v.w;
-    }
-    const floatx4 bhn = ld4(P + L.bhh + 2 * H + fD);
-    for (int i = tid; i < 4 * LDA; i += blockDim.x) hs[0][i] = 0.f;
-    const __amdgpu_buffer_rsrc_t rs_gi = mlg_rsrc(gi), rs_h = mlg_rsrc(hsg), rs_r = mlg_rsrc(ws_gr),
-                                 rs_z = mlg_rsrc(ws_gz), rs_n = mlg_rsrc(ws_gn), rs_hn = mlg_rsrc(ws_ghn);
-    st1_rs(rs_h, valid ? (rr * H + f) * 4 : (int)0x80000000u, 0, 0.f);  // HS[0]
-    // per-step inputs: the MFMA init of rows 0 / 1 (GI r / z part of features fD..) and the lane's GI n element
-    const int gq = g == 1 ? 1 : 0;
-    const int vo_gp = (rr * 3 * H + gq * H + fD) * 4, vo_gn = (rr * 3 * H + 2 * H + f) * 4;
-    struct In {
-        floatx4 gp;
-        float gn;
-    };
-    auto load_in = [&](int t, In& d) {
-        const int so = t * R * 3 * H * 4;
-        d.gp = ld4_rs(rs_gi, vo_gp, so);
-        d.gn = ld1_rs(rs_gi, vo_gn, so);
-    };
-    const int vo_st = valid ? (rr * H + f) * 4 : (int)0x80000000u;
-    float hprev = 0.f;  // h_{t-1} of the lane's cell: its own previous output
-    auto step = [&](int t, const In& in, int cur) {
-        const float* hrow = hs[cur] + q * LDA;
-        floatx4 hv[H / 4];  // the whole h row first: the MFMA chain then never waits on LDS
-#pragma unroll
-        for (int k4 = 0; k4 < H / 4; ++k4) hv[k4] = ld4(hrow + 4 * k4);
-        // two accumulation chains (even / odd k quads) halve the dependent-MFMA latency; summed at the end
-        floatx4 acc0 = g == 2 ? bhn : (g == 3 ? floatx4{0.f, 0.f, 0.f, 0.f} : in.gp), acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k4 = 0; k4 < H / 4; k4 += 2) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                acc0 = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[4 * k4 + e], hv[k4][e], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[4 * k4 + 4 + e], hv[k4 + 1][e], acc1, 0, 0, 0);
-            }
-        }
-        const floatx4 acc = acc0 + acc1;
-        float ar = acc[0], az = acc[1], ahn = acc[2], a3 = acc[3];
-        rows_transpose4(ar, az, ahn, a3);  // gate g of (feature f, row r) now in register g
-        lst.mark(0);
-        const float rg = fast_sigmoid(ar), zg = fast_sigmoid(az);
-        const float ng = fast_tanh(in.gn + rg * ahn);
-        const float hn = ng + zg * (hprev - ng);
-        hs[cur ^ 1][q * LDA + f] = hn;
-        hprev = hn;
-        lst.mark(2);
-        const int vo = t < Te ? vo_st : (int)0x80000000u;  // t >= Te: padding step (see below)
-        const int vg = online ? vo : (int)0x80000000u;
-        const int so = (t < Te ? t : 0) * R * H * 4;
-        st1_rs(rs_h, vo, so + R * H * 4, hn);  // HS[t + 1]
-        st1_rs(rs_r, vg, so, rg);
-        st1_rs(rs_z, vg, so, zg);
-        st1_rs(rs_n, vg, so, ng);
-        st1_rs(rs_hn, vg, so, ahn);
-        lst.mark(3);
-        __syncthreads();
-        lst.mark(4);
-        ++lst.steps;
-    };
-    // GI rows are prefetched MLG_REC_PD steps ahead (clamped, unconditional loads) into a register ring. The step
-    // count is padded to a multiple of MLG_REC_PD (padding steps store nothing): no control flow inside the
-    // unrolled body, so every ring slot keeps its registers and the loads are waited for only where consumed.
-    In ring[MLG_REC_PD];
-#pragma unroll
-    for (int i = 0; i < MLG_REC_PD; ++i) load_in(i < Te ? i : Te - 1, ring[i]);
-    __syncthreads();
-    lst.mark(5);
-    for (int t0 = 0; t0 < Te; t0 += MLG_REC_PD) {
-#pragma unroll
-        for (int i = 0; i < MLG_REC_PD; ++i) {
-            const int t = t0 + i;
-            step(t, ring[i], i & 1);
-            // refill the slot only once the step has consumed it: the load then targets the slot's own registers
-            // (no register rotation at the loop back-edge, which would wait for every load in flight)
-            load_in(t + MLG_REC_PD < Te ? t + MLG_REC_PD : Te - 1, ring[i]);
-            lst.mark(1);
-        }
-    }
+    const mlg::Gru4Fwd a{c.R, P + L.whh, P + L.bhh, online ? gi_on : gi_tg, online ? hs_on : hs_tg,
+                         ws_gr, ws_gz, ws_gn, ws_ghn, online};
+    mlg::gru4_fwd<H>(a, online ? bid : bid - nt4, t_eff(msum), lst);
     lst.flush(0);
 }
 
@@ -1539,7 +1435,6 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
 // reverse-time GRU backward; wave w owns hidden chunk w. W_hh^T rows of the chunk live in VGPRs, the
 // step's gate values are prefetched one step ahead, dGH is exchanged through LDS (double buffered).
 // dh_{t-1} = dh * z + W_hh^T dGH.  dX = W_ih^T dGI does not feed the recurrence: agent_dx_kernel.
-constexpr int MLG_BWD_MAXA = 96;  // fc2 rows staged in LDS by agent_bwd_kernel (host-checked)
 template <int H>
 __global__ void __launch_bounds__(512) agent_bwd_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ P,
                                                         const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
@@ -1653,140 +1548,14 @@ __global__ void __launch_bounds__(512) agent_bwd4_kernel(LCfg c, MlgBatch bt, Ag
                                                          const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
                                                          float* __restrict__ dgi, float* __restrict__ dgh,
                                                          const float* __restrict__ msum) {
-    constexpr int LDG = 3 * H + 4;
-    constexpr int KQ = 3 * H / 4;  // gate rows per K quarter
-    __shared__ __attribute__((aligned(16))) float sgh[2][4 * LDG];
-    __shared__ __attribute__((aligned(16))) float w2s[MLG_BWD_MAXA * H];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int blk = lane >> 2, q = lane & 3, kq = blk >> 2, fg = blk & 3;
-    const int r = blockIdx.x * 4 + q;
-    const bool valid = r < c.R;
-    const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
-    const int R = c.R, N = c.N;
-    const int fD = 16 * w + 4 * fg;
-    const int f = fD + kq;  // the lane's (feature, row) after the reduction
     LStamps lst;
     lst.init();
-    const int Te = t_eff(msum);
-    const int rr = valid ? r : 0;
-    const int64_t abase = bslot(bt, b) * bt.T1 * N + n;
-    struct Raw {  // per-step operands as stored by the forward, for (feature f, row r)
-        float rg, zg, ng, ghn, hp, dq;
-        int a;
-    };
-    // Buffer loads: the lane part of every offset is fixed, the step part is a wave-uniform SGPR offset, so a
-    // step's loads cost no VALU address arithmetic.
-    const __amdgpu_buffer_rsrc_t rs_r = mlg_rsrc(ws_gr), rs_z = mlg_rsrc(ws_gz), rs_n = mlg_rsrc(ws_gn),
-                                 rs_hn = mlg_rsrc(ws_ghn), rs_hs = mlg_rsrc(ws_hs), rs_dq = mlg_rsrc(dqv),
-                                 rs_act = mlg_rsrc(reinterpret_cast<const float*>(bt.actions));
-    const int vo_g = (rr * H + f) * 4, vo_dq = rr * 4, vo_act = (int)(abase * 8);
-    auto load_raw = [&](int t, Raw& s) {
-        const int so = t * R * H * 4;
-        s.rg = ld1_rs(rs_r, vo_g, so);
-        s.zg = ld1_rs(rs_z, vo_g, so);
-        s.ng = ld1_rs(rs_n, vo_g, so);
-        s.ghn = ld1_rs(rs_hn, vo_g, so);
-        s.hp = ld1_rs(rs_hs, vo_g, so);  // HS[t] = h_{t-1}
-        const int tq = t < c.T - 1 ? t : c.T - 2;
-        s.dq = ld1_rs(rs_dq, vo_dq, tq * R * 4);
-        // 32-bit load of the action's low word (little-endian int64), unconditional: no branch around it, and no
-        // dead high half whose pending load would block the reuse of its register
-        const int act = __float_as_int(ld1_rs(rs_act, vo_act, tq * N * 8));
-        s.a = t < c.T - 1 ? act : -1;
-    };
-    // the first steps' operands are requested before anything else is queued on the vector memory path
-    Raw ring[MLG_BWD_PD];
-#pragma unroll
-    for (int i = 0; i < MLG_BWD_PD; ++i) load_raw(Te - 1 - i > 0 ? Te - 1 - i : 0, ring[i]);
-    float wt[KQ];  // A operand: W_hh[kq * KQ + kk][fD + i] (i = q)
-#pragma unroll
-    for (int kk = 0; kk < KQ; ++kk) wt[kk] = P[L.whh + (int64_t)(kq * KQ + kk) * H + fD + q];
-    for (int i = tid; i < c.A * H; i += blockDim.x) w2s[i] = P[L.w2 + i];  // fc2 rows for dh += dq W2[a]
-    {  // steps past max_t_filled: zero deltas (wgrad rows); the tile's rows are contiguous per step
-        const int nv = min(4, R - (int)blockIdx.x * 4) * 3 * H / 4;  // float4s per step and array
-        for (int t = Te; t < c.T; ++t) {
-            float* zi = dgi + ((int64_t)t * R + blockIdx.x * 4) * 3 * H;
-            float* zh = dgh + ((int64_t)t * R + blockIdx.x * 4) * 3 * H;
-            for (int i = tid; i < nv; i += blockDim.x) {
-                reinterpret_cast<floatx4*>(zi)[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-                reinterpret_cast<floatx4*>(zh)[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-            }
-        }
-    }
-    // Every gate delta is dh times a factor of the saved activations (the GRU backward is linear in dh), and the
-    // fc2 term dq W2[a] does not depend on dh either: both are formed one step ahead, off the dh -> dh chain.
-    struct Coef {
-        float cr, cz, cn, chn, ch, dw;
-    };
-    auto coef = [&](const Raw& s, Coef& k) {
-        const bool take = valid && s.a >= 0;
-        const float w2 = w2s[(take ? s.a : 0) * H + f];
-        const float cn = (1.f - s.zg) * (1.f - s.ng * s.ng);  // dn' = dh (1 - z)(1 - n^2)
-        k.cn = cn;
-        k.cr = cn * s.ghn * (s.rg * (1.f - s.rg));      // dr' = dn' (W_hn h + b_hn) r (1 - r)
-        k.cz = (s.hp - s.ng) * (s.zg * (1.f - s.zg));  // dz' = dh (h_{t-1} - n) z (1 - z)
-        k.chn = cn * s.rg;                              // d(W_hn h + b_hn) = dn' r
-        k.ch = s.zg;                                    // direct path dh_{t-1} += dh z
-        k.dw = (take ? s.dq : 0.f) * w2;
-    };
-    float dh = 0.f;
-    const __amdgpu_buffer_rsrc_t rs_gi = mlg_rsrc(dgi), rs_gh = mlg_rsrc(dgh);
-    const int vo_st = valid ? (r * 3 * H + f) * 4 : (int)0x80000000u;
-    auto step = [&](int t, const Coef& k, int cur) {
-        dh += k.dw;
-        const float drp = dh * k.cr, dzp = dh * k.cz, dnp = dh * k.cn, dghn = dh * k.chn, dhd = dh * k.ch;
-        float* gh = sgh[cur] + q * LDG + f;
-        gh[0] = drp;
-        gh[H] = dzp;
-        gh[2 * H] = dghn;
-        lst.mark(2);
-        __syncthreads();
-        lst.mark(4);
-        const float* ghr = sgh[cur] + q * LDG + kq * KQ;
-        floatx4 gv[KQ / 4];
-#pragma unroll
-        for (int k4 = 0; k4 < KQ / 4; ++k4) gv[k4] = ld4(ghr + 4 * k4);
-        // the step's global stores go out behind the barrier, in the shadow of the MFMA chain
-        const int vo = t >= 0 ? vo_st : (int)0x80000000u;  // t < 0: padding step, every lane dropped
-        const int so = (t >= 0 ? t : 0) * R * 3 * H * 4;
-        st1_rs(rs_gi, vo, so, drp);
-        st1_rs(rs_gi, vo, so + H * 4, dzp);
-        st1_rs(rs_gi, vo, so + 2 * H * 4, dnp);
-        st1_rs(rs_gh, vo, so, drp);
-        st1_rs(rs_gh, vo, so + H * 4, dzp);
-        st1_rs(rs_gh, vo, so + 2 * H * 4, dghn);
-        lst.mark(3);
-        floatx4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k4 = 0; k4 < KQ / 4; k4 += 2) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                p0 = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[4 * k4 + e], gv[k4][e], p0, 0, 0, 0);
-                p1 = __builtin_amdgcn_mfma_f32_4x4x1f32(wt[4 * k4 + 4 + e], gv[k4 + 1][e], p1, 0, 0, 0);
-            }
-        }
-        const floatx4 part = p0 + p1;
-        dh = dhd + rows_sum_transpose4(part[0], part[1], part[2], part[3]);  // (q0 + q1) + (q2 + q3)
-        lst.mark(0);
-        ++lst.steps;
-    };
-    __syncthreads();  // w2s staged
-    Coef kc;
-    coef(ring[0], kc);
-    lst.mark(5);
-    // step count padded to a multiple of MLG_BWD_PD (padding steps t < 0 store nothing; see agent_rec4_kernel)
-    for (int t0 = Te - 1; t0 >= 0; t0 -= MLG_BWD_PD) {
-#pragma unroll
-        for (int i = 0; i < MLG_BWD_PD; ++i) {
-            const int t = t0 - i;
-            load_raw(t - MLG_BWD_PD > 0 ? t - MLG_BWD_PD : 0, ring[i]);  // slot i (step t) is consumed
-            Coef kn;
-            coef(ring[(i + 1) % MLG_BWD_PD], kn);  // step t - 1
-            lst.mark(1);
-            step(t, kc, i & 1);
-            kc = kn;
-        }
-    }
+    const int r = blockIdx.x * 4 + ((threadIdx.x & 63) & 3);
+    const bool valid = r < c.R;
+    const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
+    const mlg::Gru4Bwd a{c.R, c.T, c.A, c.N, P + L.whh, P + L.w2, ws_hs, ws_gr, ws_gz, ws_gn, ws_ghn, dqv,
+                         bt.actions, dgi, dgh};
+    mlg::gru4_bwd<H>(a, blockIdx.x, t_eff(msum), bslot(bt, b) * bt.T1 * c.N + n, lst);
     lst.flush(1);
 }
 

@@ -21,6 +21,7 @@
 // Agent rows: r = (c * B + b) * NA + n for copy c (0 plain, 1 within, 2 interact); target rows r = b * NA + n.
 // Items i = b * T + t. Mixer items use t < T - 1 (the other kernels write zeros for t = T - 1).
 #include "mlg_host.h"
+#include "gru4_device.h"
 #include "refil_device.h"
 #include "wgrad_device.h"
 
@@ -666,6 +667,23 @@ __global__ void __launch_bounds__(256) rec_kernel(RCfg c, RAgent L, const float*
     }
 }
 
+// The recurrences on 4-row tiles (gru4_device.h, shared with the QMIX learner): 4x the CUs of the 16-row tiles above
+// on the sequential T loop. grid (ntiles4 online + ntiles4 target), 4 waves; online tiles store the gates.
+__global__ void __launch_bounds__(256) rec4_kernel(RCfg c, RAgent L, const float* __restrict__ Pon,
+                                                   const float* __restrict__ Ptg, const float* __restrict__ gi_on,
+                                                   const float* __restrict__ gi_tg, float* __restrict__ hs_on,
+                                                   float* __restrict__ hs_tg, float* __restrict__ ws_gr,
+                                                   float* __restrict__ ws_gz, float* __restrict__ ws_gn,
+                                                   float* __restrict__ ws_ghn, const float* __restrict__ msum) {
+    const int nt_on = (c.Ron + 3) / 4;
+    const bool online = (int)blockIdx.x < nt_on;
+    const float* P = online ? Pon : Ptg;
+    const mlg::Gru4Fwd a{online ? c.Ron : c.Rtg, P + L.whh, P + L.bhh, online ? gi_on : gi_tg, online ? hs_on : hs_tg,
+                         ws_gr, ws_gz, ws_gn, ws_ghn, online};
+    mlg::NoStamps st;
+    mlg::gru4_fwd<EMB>(a, online ? blockIdx.x : blockIdx.x - nt_on, t_eff(msum), st);
+}
+
 // agent row r of a net -> (b, n); copy = r / (B * NA)
 __device__ __forceinline__ void row_bn(const RCfg& c, int r, int& b, int& n) {
     n = r % c.NA;
@@ -1211,6 +1229,22 @@ __global__ void __launch_bounds__(256) rec_bwd_kernel(RCfg c, MlgEntityBatch bt,
     }
 }
 
+// reverse-time GRU backward of the online rows on 4-row tiles (gru4_device.h); dh += dQ W3[a] (fc3 rows)
+__global__ void __launch_bounds__(256) rec_bwd4_kernel(RCfg c, MlgEntityBatch bt, RAgent L, const float* __restrict__ P,
+                                                       const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
+                                                       const float* __restrict__ ws_gz, const float* __restrict__ ws_gn,
+                                                       const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
+                                                       float* __restrict__ dgi, float* __restrict__ dgh,
+                                                       const float* __restrict__ msum) {
+    const int r = blockIdx.x * 4 + ((threadIdx.x & 63) & 3);
+    int b = 0, n = 0;
+    if (r < c.Ron) row_bn(c, r, b, n);
+    const mlg::Gru4Bwd a{c.Ron, c.T, c.A, c.NA, P + L.whh, P + L.w3, ws_hs, ws_gr, ws_gz, ws_gn, ws_ghn, dqv,
+                         bt.actions, dgi, dgh};
+    mlg::NoStamps st;
+    mlg::gru4_bwd<EMB>(a, blockIdx.x, t_eff(msum), eslot(bt, b) * bt.T1 * c.NA + n, st);
+}
+
 // ---- agent entity block backward: one wave per item pair --------------------------------------------------
 struct EntBwd {
     const float *wihT, *w2T, *woutT, *winT;
@@ -1473,9 +1507,16 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     hipLaunchKernelGGL(ent_fwd_kernel, dim3((unsigned)((c.I + 1) / 2), 2), dim3(64), 0, s, c, bt, bufs->groupA, La,
                        ws + w.ein, on, tg, ws + w.msum);
     const int nt_on = (c.Ron + 15) / 16, nt_tg = (c.Rtg + 15) / 16;
-    hipLaunchKernelGGL(rec_kernel, dim3((unsigned)(nt_on + nt_tg)), dim3(256), 0, s, c, La, ws + w.pa_on, ws + w.pa_tg,
-                       ws + w.gi_on, ws + w.gi_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn,
-                       ws + w.msum);
+    // the recurrences on 4-row tiles (default) or 16-row tiles (MLG_REFIL_REC16, A/B)
+    static const bool rec16 = getenv("MLG_REFIL_REC16") != nullptr;
+    if (rec16)
+        hipLaunchKernelGGL(rec_kernel, dim3((unsigned)(nt_on + nt_tg)), dim3(256), 0, s, c, La, ws + w.pa_on,
+                           ws + w.pa_tg, ws + w.gi_on, ws + w.gi_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.gr, ws + w.gz,
+                           ws + w.gn, ws + w.ghn, ws + w.msum);
+    else
+        hipLaunchKernelGGL(rec4_kernel, dim3((unsigned)((c.Ron + 3) / 4 + (c.Rtg + 3) / 4)), dim3(256), 0, s, c, La,
+                           ws + w.pa_on, ws + w.pa_tg, ws + w.gi_on, ws + w.gi_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.gr,
+                           ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.msum);
     hipLaunchKernelGGL(q_kernel, dim3((unsigned)nt_on, (unsigned)c.T, 2), dim3(64 * (c.Ap / 16)), 0, s, c, bt, La,
                        ws + w.pa_on, ws + w.pa_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.mac, ws + w.tmac, ws + w.msum);
     // ---- mixer ----
@@ -1524,8 +1565,13 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     }
     hipLaunchKernelGGL(hyper_bwd_kernel, dim3((unsigned)c.I, 4), dim3(64), 0, s, c, bt, hb, ws + w.msum);
     // ---- agent backward ----
-    hipLaunchKernelGGL(rec_bwd_kernel, dim3((unsigned)nt_on), dim3(256), 0, s, c, bt, La, ws + w.pa_on, ws + w.hs_on,
-                       ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.dq, ws + w.dgi, ws + w.dgh, ws + w.msum);
+    if (rec16)
+        hipLaunchKernelGGL(rec_bwd_kernel, dim3((unsigned)nt_on), dim3(256), 0, s, c, bt, La, ws + w.pa_on, ws + w.hs_on,
+                           ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.dq, ws + w.dgi, ws + w.dgh, ws + w.msum);
+    else
+        hipLaunchKernelGGL(rec_bwd4_kernel, dim3((unsigned)((c.Ron + 3) / 4)), dim3(256), 0, s, c, bt, La, ws + w.pa_on,
+                           ws + w.hs_on, ws + w.gr, ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.dq, ws + w.dgi, ws + w.dgh,
+                           ws + w.msum);
     EntBwd eb{ws + w.a_wihT, ws + w.a_w2T, ws + w.a_woutT, ws + w.a_winT, ws + w.h_wspT[4], ws + w.x1, ws + w.qkv, ws + w.P, ws + w.x3,
               ws + w.dgi, ws + w.dfc2, ws + w.dout, ws + w.dqkv, ws + w.dfc1};
     hipLaunchKernelGGL(ent_bwd_kernel, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt, eb, ws + w.msum);

@@ -1,5 +1,6 @@
-"""QLearner.train microbenchmark on the bench's shapes: 5v5 medium_1h_4t rollouts (ENVS envs, episode_limit 100)
-fill a device replay ring, then REPS train() calls on batch_size 32 samples read in place (the bench's path).
+"""QLearner.train / REFILLearner.train (MODE=refil) microbenchmark on the bench's shapes: 5v5 medium_1h_4t (refil:
+refil_8, 3-8 agents) rollouts (ENVS envs, episode_limit 100) fill a device replay ring, then REPS train() calls on
+batch_size 32 samples read in place (the bench's path).
 Prints mean ms per train() (HIP events on the learner's stream) and the loss of the last call, so variant libraries
 (MLG_LIB=...) can be A/B-compared; run under rocprofv3 --kernel-trace --stats for the per-kernel split."""
 import json
@@ -21,7 +22,12 @@ overrides = [f"batch_size_run={ENVS}", "runner=parallel", "buffer_cpu_only=False
              "env_args.match_build_plan=medium_1h_4t", "env_args.episode_limit=100", "seed=0",
              "learner_log_interval=1000000000", "log_interval=1000000000", "runner_log_interval=1000000000",
              "test_interval=1000000000000", "t_max=1000000000000", "show_exp_parameters=False"]
-cfg = build_config("qmix", "ma", overrides=overrides, device_index=0)
+MODE = os.environ.get("MODE", "qmix")
+if MODE == "refil":
+    overrides = [o.replace("medium_1h_4t", "refil_8") for o in overrides]
+    cfg = build_config("refil", "ma_entity", overrides=overrides, device_index=0)
+else:
+    cfg = build_config("qmix", "ma", overrides=overrides, device_index=0)
 np.random.seed(0)
 torch.manual_seed(0)
 args = to_args(cfg)
