@@ -49,6 +49,7 @@ class DistributedLeague:
         self.historical = None         # [max_historical, n_params]
         self.historical_meta: List[tuple] = []  # (pid, parent pid, trained_steps), oldest first
         self.evictions = 0  # snapshots evicted to make room for newer ones (pool full)
+        self.payoff_host = None  # host copy of the payoff taken by host_snapshot() (what matchmaking reads)
 
     def player(self) -> int:
         return self.rank % self.n
@@ -101,6 +102,19 @@ class DistributedLeague:
         self.payoff.tensor.add_(self._delta)
         self._delta.zero_()
         return self.payoff.tensor
+
+    def host_snapshot(self, counter: torch.Tensor = None):
+        """ONE device -> host read per league iteration: the (reduced) payoff table, plus ``counter`` (a player's
+        device-side trained-steps count) in the same copy. Matchmaking and the checkpoint decisions then read win
+        rates from ``payoff_host`` with no further device round trips. Returns the counter's value (or None)."""
+        flat = self.payoff.tensor.reshape(-1).to(torch.float64)
+        if counter is not None:
+            flat = torch.cat([flat, counter.reshape(1).to(device=flat.device, dtype=torch.float64)])
+        host = flat.cpu()
+        n = self.payoff.tensor.numel()
+        self.payoff_host = PayoffWrapper(host[:n].to(torch.float32).reshape(self.payoff.tensor.shape),
+                                         self.payoff.reference_compat)
+        return float(host[n]) if counter is not None else None
 
     # ---- agent pool --------------------------------------------------------------------------------------
     def share_params(self, flat: torch.Tensor):
@@ -167,7 +181,7 @@ class DistributedLeague:
         most = max(counts.values())
         idx = next(i for i, (_, parent, _) in enumerate(self.historical_meta) if counts[parent] == most)
         hp = self.historical_meta.pop(idx)[0]
-        for t in (self.payoff.tensor, self._delta):
+        for t in (self.payoff.tensor, self._delta) + ((self.payoff_host.tensor,) if self.payoff_host else ()):
             t[hp, :, :] = 0
             t[:, hp, :] = 0
         self.evictions += 1

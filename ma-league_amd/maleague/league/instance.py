@@ -78,14 +78,20 @@ class LeagueInstance:
 
     def view(self) -> LeagueView:
         hist = [Historical(pid, parent, steps) for pid, parent, steps in self.league.historical_meta]
-        return LeagueView(self.league.payoff, self.players, hist)
+        # the host copy of this league iteration's payoff (DistributedLeague.host_snapshot) when there is one
+        pay = self.league.payoff_host if self.league.payoff_host is not None else self.league.payoff
+        return LeagueView(pay, self.players, hist)
 
     def sync(self):
         """League iteration boundary: payoff all_reduce, parameter / checkpoint all_gather, barrier, next match.
         Returns (opponent pid, historical?) or None when the matchmaker ends the league for this player."""
         home = self.experiment.home_mac
         self.league.sync_payoff()
-        steps = int(home.agent.trained_steps)
+        # payoff + this player's trained steps in one device -> host read (matchmaking then runs on the host copy)
+        agent = home.agent
+        counter = agent.trained_counter(self.league.device) if hasattr(agent, "trained_counter") else None
+        dev_steps = self.league.host_snapshot(counter)
+        steps = agent.trained_steps_with(dev_steps) if counter is not None else int(agent.trained_steps)
         self.me.trained_steps = steps
         ckpt = self.me.ready_to_checkpoint(self.view()) if self.mode == "rolebased" else False
         taken = self.league.exchange(agent_vector(home), steps, ckpt)

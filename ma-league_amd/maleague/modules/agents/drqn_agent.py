@@ -32,6 +32,10 @@ class AgentNetwork(nn.Module):
         self._trained_host = int(value)
         self._trained_dev = None
 
+    def trained_steps_with(self, device_count: float) -> int:
+        """trained_steps given the device counter's value read elsewhere (no extra device round trip)."""
+        return self._trained_host + int(round(float(device_count)))
+
     def trained_counter(self, device) -> torch.Tensor:
         """The device-side float64 running count a learner kernel adds to (created at 0 on first use)."""
         if self._trained_dev is None or self._trained_dev.device != torch.device(device):

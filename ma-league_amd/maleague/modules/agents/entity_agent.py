@@ -12,6 +12,7 @@ import torch
 import torch.nn as nn
 
 from ... import _native
+from ...utils.flat import flat_view
 from ..layers.attention import EntityAttentionLayer
 from .drqn_agent import AgentNetwork
 
@@ -48,17 +49,9 @@ class EntityAttentionRNNAgent(AgentNetwork):
         """named_parameters() concatenated (the canonical order the C ABI documents). When the parameters already are
         consecutive views of one fp32 buffer (a learner's FlatParams), that buffer itself: no copy, no launch."""
         params = list(self.parameters())
-        p0 = params[0]
-        if all(p.dtype == torch.float32 and p.is_contiguous() for p in params):
-            off, ok = p0.data_ptr(), True
-            for p in params:
-                if p.data_ptr() != off or p.untyped_storage().data_ptr() != p0.untyped_storage().data_ptr():
-                    ok = False
-                    break
-                off += 4 * p.numel()
-            if ok:
-                n = sum(p.numel() for p in params)
-                return p0.detach().new_empty(0).set_(p0.untyped_storage(), p0.storage_offset(), (n,), (1,))
+        flat = flat_view(params)
+        if flat is not None:
+            return flat
         with torch.no_grad():
             return torch.cat([p.detach().float().reshape(-1) for p in params])
 

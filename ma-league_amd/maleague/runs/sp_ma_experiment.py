@@ -11,6 +11,8 @@ from typing import OrderedDict
 import torch
 
 from ..controllers import REGISTRY as mac_REGISTRY
+from ..learners.q_learner import FlatParams
+from ..utils.flat import flat_view
 from ..steppers import SELF_REGISTRY as self_steppers_REGISTRY
 from .ma_experiment import MultiAgentExperiment
 
@@ -23,13 +25,20 @@ def agent_vector(mac) -> torch.Tensor:
 @torch.no_grad()
 def load_agent_vector(mac, vec: torch.Tensor):
     """In-place copy (keeps a learner's flat-parameter views valid; bumps versions -> weights repacked)."""
+    params = list(mac.agent.parameters())
+    n = sum(p.numel() for p in params)
+    if n != vec.numel():
+        raise ValueError(f"parameter vector of {vec.numel()} floats for an agent of {n}")
+    flat = flat_view(params)
+    if flat is not None:  # parameters back to back in one buffer: one copy
+        flat.copy_(vec.reshape(-1))
+        mac.agent.mark_dirty()  # writes through the flat view bump no parameter version: repack explicitly
+        return
     off = 0
-    for p in mac.agent.parameters():
+    for p in params:
         k = p.numel()
         p.copy_(vec[off:off + k].view_as(p))
         off += k
-    if off != vec.numel():
-        raise ValueError(f"parameter vector of {vec.numel()} floats for an agent of {off}")
 
 
 class SelfPlayMultiAgentExperiment(MultiAgentExperiment):
@@ -37,6 +46,8 @@ class SelfPlayMultiAgentExperiment(MultiAgentExperiment):
         super().__init__(args, logger, on_episode_end=on_episode_end, log_start_t=log_start_t)
         # the away agent uses the home buffer's scheme (sp_ma_experiment.py:24-25)
         self.away_mac = mac_REGISTRY[self.args.mac](self.home_buffer.scheme, self.groups, self.args)
+        # the frozen opponent's parameters as views of one flat buffer: an opponent swap is one copy
+        FlatParams(self.away_mac.agent.parameters(), self.args.device)
 
     def load_adversary(self, agent: OrderedDict):
         """Frozen opponent parameters (a DRQN state_dict), sp_ma_experiment.py:27-29."""
