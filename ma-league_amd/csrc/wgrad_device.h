@@ -239,7 +239,10 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
     if (task >= last.task0 + last.mb * last.nb * last.chunks) return;
     const BJob jb = J.j[find_bjob(J, task)];
     const int local = task - jb.task0;
-    const int ch = local % jb.chunks, blk = local / jb.chunks;
+    // the output blocks of one row chunk are consecutive tasks (the same workgroup / neighbours): jobs with several
+    // 64-row output blocks (M = 192: in_trans, W_ih, W_hh) then read their x rows from HBM once, the other blocks
+    // hit L2 (block-major order re-read them from HBM per block). Slab positions do not depend on this order.
+    const int ch = local / (jb.mb * jb.nb), blk = local % (jb.mb * jb.nb);
     const int mbi = blk / jb.nb, nbi = blk % jb.nb;
     const int col = lane & 15, g = lane >> 4;
     const int r0 = ch * jb.ch_rows, r1 = min(jb.rows, r0 + jb.ch_rows);
