@@ -26,6 +26,23 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 }
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+// Store through the global address space. A pointer whose provenance the compiler cannot see (kept in VGPRs behind
+// an opaque asm, e.g. the rollout's per-step batch pointers) is otherwise stored through as FLAT: flat stores count
+// on lgkmcnt too, so every later LDS / permute wait would also wait for the step's HBM stores to complete. Batch,
+// run-summary (zero-copy host) and ring pointers are all global memory.
+template <class T>
+__device__ __forceinline__ void gst(T* p, T v) {
+    *(__attribute__((address_space(1))) T*)p = v;
+}
+// HIP's struct vector types have no assignment into another address space: store their native vector form
+__device__ __forceinline__ void gst(uint4* p, uint4 v) {
+    typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+    gst(reinterpret_cast<u32x4_*>(p), u32x4_{v.x, v.y, v.z, v.w});
+}
+__device__ __forceinline__ void gst(float2* p, float2 v) {
+    typedef float f32x2_ __attribute__((ext_vector_type(2)));
+    gst(reinterpret_cast<f32x2_*>(p), f32x2_{v.x, v.y});
+}
 
 // bf16 operands of v_mfma_f32_16x16x32_bf16 (8 per lane) and round-to-nearest packing of two fp32 (low half = lo).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

@@ -624,9 +624,9 @@ __device__ inline void zero_slot_steps(const MlgBatch& bt, int slot, int z0, int
         float* b = p + r0 * per;
         if (per % 4 == 0) {
             uint4* q = reinterpret_cast<uint4*>(b);
-            for (int x = lane; x < n * per / 4; x += nl) q[x] = make_uint4(0u, 0u, 0u, 0u);
+            for (int x = lane; x < n * per / 4; x += nl) gst(q + x, make_uint4(0u, 0u, 0u, 0u));
         } else {
-            for (int x = lane; x < n * per; x += nl) b[x] = 0.f;
+            for (int x = lane; x < n * per; x += nl) gst(b + x, 0.f);
         }
     };
     z16(bt.obs, N * DO);
@@ -634,15 +634,15 @@ __device__ inline void zero_slot_steps(const MlgBatch& bt, int slot, int z0, int
     int* av = bt.avail + r0 * N * A;
     float* oh = bt.actions_onehot + r0 * N * A;
     for (int x = lane; x < n * N * A; x += nl) {
-        av[x] = 0;
-        oh[x] = 0.f;
+        gst(av + x, 0);
+        gst(oh + x, 0.f);
     }
-    auto* ac = bt.actions + r0 * N;
-    for (int x = lane; x < n * N; x += nl) ac[x] = 0;
+    int64_t* ac = bt.actions + r0 * N;
+    for (int x = lane; x < n * N; x += nl) gst(ac + x, (int64_t)0);
     for (int x = lane; x < n; x += nl) {
-        bt.reward[r0 + x] = 0.f;
-        bt.terminated[r0 + x] = 0;
-        bt.filled[r0 + x] = 0;
+        gst(bt.reward + r0 + x, 0.f);
+        gst(bt.terminated + r0 + x, (uint8_t)0);
+        gst(bt.filled + r0 + x, (int64_t)0);
     }
 }
 
@@ -876,8 +876,8 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
         }
         if (valid) {
             float* dst = bt.obs + (st_row * N + a) * DO + j * 8;
-            *reinterpret_cast<floatx4*>(dst) = lo;
-            *reinterpret_cast<floatx4*>(dst + 4) = hi;
+            gst(reinterpret_cast<floatx4*>(dst), lo);
+            gst(reinterpret_cast<floatx4*>(dst + 4), hi);
             if (obf) {  // v7: bf16 rows (every obs feature is exact in bf16: k/32, hp/max_hp, 0, 0.5, 1)
                 *reinterpret_cast<uint4*>(lobs + (e * N + a) * ldo + j * 4) =
                     make_uint4(cvt_pk_bf16(lo.x, lo.y), cvt_pk_bf16(lo.z, lo.w), cvt_pk_bf16(hi.x, hi.y),
@@ -906,16 +906,16 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
         const int k = k0 + hl;
         if (k < N * A) {
             const int pt = sd ? ((k / A) << 8) | (k % A) : avtab[k];
-            bt.avail[st_row * N * A + k] = (int)((lavm[e * N + (pt >> 8)] >> (pt & 255)) & 1ull);
+            gst(bt.avail + st_row * N * A + k, (int)((lavm[e * N + (pt >> 8)] >> (pt & 255)) & 1ull));
         }
     }
     sp.mark(11);
     if (hl < U) {
         const int r = mask_role(M, hl);
         float* dst = bt.state + st_row * S + hl * 6;
-        *reinterpret_cast<float2*>(dst) = make_float2((float)(L.hp > 0), (float)L.x * inv_p);
-        *reinterpret_cast<float2*>(dst + 2) = make_float2((float)L.y * inv_p, (float)L.hp * inv_maxhp(r));
-        *reinterpret_cast<float2*>(dst + 4) = make_float2((float)((M.team1 >> hl) & 1), (float)r * 0.5f);
+        gst(reinterpret_cast<float2*>(dst), make_float2((float)(L.hp > 0), (float)L.x * inv_p));
+        gst(reinterpret_cast<float2*>(dst + 2), make_float2((float)L.y * inv_p, (float)L.hp * inv_maxhp(r)));
+        gst(reinterpret_cast<float2*>(dst + 4), make_float2((float)((M.team1 >> hl) & 1), (float)r * 0.5f));
     }
     sp.mark(12);
 }
@@ -1543,8 +1543,8 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
             }
             R.pact[e * N + n] = act;
             const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
-            bt.actions[bt_off] = act;
-            if (!bt.full_write) bt.actions_onehot[bt_off * A + act] = 1.0f;
+            gst(bt.actions + bt_off, (int64_t)act);
+            if (!bt.full_write) gst(bt.actions_onehot + bt_off * A + act, 1.0f);
         }
     }
 }
@@ -1636,8 +1636,8 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
             R.pact[e * N + n] = act;
 #ifndef MLG_ABL_FC2_NOSTORE  // timing ablation only
             const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
-            bt.actions[bt_off] = act;
-            if (!bt.full_write) bt.actions_onehot[bt_off * A + act] = 1.0f;
+            gst(bt.actions + bt_off, (int64_t)act);
+            if (!bt.full_write) gst(bt.actions_onehot + bt_off * A + act, 1.0f);
 #endif
         }
     }
@@ -1736,7 +1736,7 @@ __device__ inline void env_lane_reset(const EnvCtx& C, const MlgEnvState& st, En
         }
         if (hl == 0) {
             st.episode[E.b] = E.ep + 1;
-            C.bt.filled[(int64_t)E.slot * C.bt.T1] = 1;
+            gst(C.bt.filled + (int64_t)E.slot * C.bt.T1, (int64_t)1);
         }
     }
     if (hl == 0) {
@@ -1762,8 +1762,8 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
     if (hl < N && !((C.amask[E.e] >> hl) & 1u)) {  // dead agent: no cell was run; its action is the no-op
         pact[hl] = 0;
         const int64_t off = ((int64_t)E.slot * T1 + t) * N + hl;
-        C.bt.actions[off] = 0;
-        if (!C.bt.full_write) C.bt.actions_onehot[off * A] = 1.0f;
+        gst(C.bt.actions + off, (int64_t)0);
+        if (!C.bt.full_write) gst(C.bt.actions_onehot + off * A, 1.0f);
     }
     if (hl < N) C.R.prev[E.e * N + hl] = pact[hl];
 #ifdef MLG_DUP_ONEHOT
@@ -1776,7 +1776,7 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
 #pragma unroll 1
         for (int k = hl; k < N * A; k += 32) {
             const int pt = C.sd ? ((k / A) << 8) | (k % A) : C.avtab[k];
-            C.bt.actions_onehot[oh + k] = (pt & 255) == pact[pt >> 8] ? 1.0f : 0.0f;
+            gst(C.bt.actions_onehot + oh + k, (pt & 255) == pact[pt >> 8] ? 1.0f : 0.0f);
         }
     }
     if (E.st == 1) {  // final action recorded; env done (parallel_stepper.py:153)
@@ -1784,8 +1784,8 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
         E.zcur = tail_start(E.zcur, t + 1);
         if (hl == 0) C.amask[E.e] = 0u;
         if (C.bt.full_write && hl == 0) {
-            C.bt.reward[(int64_t)E.slot * T1 + t] = 0.f;
-            C.bt.terminated[(int64_t)E.slot * T1 + t] = 0;
+            gst(C.bt.reward + (int64_t)E.slot * T1 + t, 0.f);
+            gst(C.bt.terminated + (int64_t)E.slot * T1 + t, (uint8_t)0);
         }
         if (hl == 0) C.R.status[E.e] = E.st;
         return;
@@ -1844,13 +1844,13 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
     E.ret += r;
     if (hl == 0) {
         const int64_t sl = (int64_t)E.slot * T1 + t;
-        C.bt.reward[sl] = r;
-        C.bt.terminated[sl] = (uint8_t)done;
-        C.bt.filled[sl + 1] = 1;
+        gst(C.bt.reward + sl, r);
+        gst(C.bt.terminated + sl, (uint8_t)done);
+        gst(C.bt.filled + sl + 1, (int64_t)1);
         if (done) {
-            C.info.won[2 * E.b] = wpt;
-            C.info.won[2 * E.b + 1] = wop;
-            C.info.draw[E.b] = !won0 && !won1;
+            gst(C.info.won + 2 * E.b, (int32_t)wpt);
+            gst(C.info.won + 2 * E.b + 1, (int32_t)wop);
+            gst(C.info.draw + E.b, (int32_t)(!won0 && !won1));
         }
     }
     if (done) {
