@@ -363,8 +363,11 @@ __device__ inline void attn_fwd_half(const float* qb, int ldq, const float* kb, 
 // dQ rows < nq (rows >= nq get 0 when writing), dK / dV all 16 rows.
 //   dP = dO V^T, dS = P (dP - sum_k P dP) / 4, dQ = dS K, dK = dS^T Q, dV = P^T dO
 // (masked keys and fully masked rows have P = 0 -> dS = 0, matching the masked_fill backward)
+// force-inlined: a call takes generic pointers, so every access became FLAT (LDS operands included: their waits
+// then also wait for the vector memory path); inlined, the LDS operands are ds_ reads and P a global load
 template <bool ACC>
-__device__ inline void attn_bwd(const float* qkv, const float* P, int nq, const float* dO, int ldo, float* DS, float* dqkv,
+__device__ __forceinline__ void attn_bwd(const float* qkv, const float* P, int nq, const float* dO, int ldo, float* DS,
+                                         float* dqkv,
                                 int lane) {
     const int h = lane >> 4, q = lane & 15;
     {
