@@ -1648,13 +1648,14 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
 // next step's GRU after two more barriers; the fp32 h' it reads was written before barrier B).
 template <int H>
 __device__ inline void hpl_split_tile(const RolloutLds2& lay, float* fm, const int* rmap, const float* hb, int ti, int N,
-                                      int lane, int kc0 = 0, int nkc = H / 16) {
+                                      int lane) {
+    constexpr int HC = H / 16;
     const int col = lane & 15, g = lane >> 4, cr = ti * 16 + col, rm = rmap[cr];
     if (!(rm & 1)) return;
     const float* hr = hb + rmap_er(rm, N) * lay.ldh + 4 * g;
     unsigned int* hq = reinterpret_cast<unsigned int*>(fm + lay.hpl + cr * XPL_STRIDE) + 2 * g;
 #pragma unroll
-    for (int kc = kc0; kc < kc0 + nkc; ++kc) {  // features 16 kc + 4 g .. + 3
+    for (int kc = 0; kc < HC; ++kc) {  // features 16 kc + 4 g .. + 3
         const floatx4 hv = ld4(hr + kc * 16);
         float v[4] = {hv[0], hv[1], hv[2], hv[3]};
 #pragma unroll
@@ -2060,16 +2061,12 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
             ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
 #endif
         // v7: h' planes (hpl_split_tile) by the waves that have no fc2 tile, beside the fc2 phase (when every wave has
-        // one -- tiles >= 8, generic shapes -- by the fc2 waves after their tiles), in (tile, half of the features)
-        // units: in a sparse step one tile's split is shared by two idle waves (one wave splitting a whole tile was the
-        // last arrival at the barrier after fc2: ~2 k cycles of every one-env step; quarter-tile units pushed the
-        // env phase's register allocation into spills)
+        // one -- tiles >= 8, generic shapes -- by the fc2 waves after their tiles)
         if constexpr (G8) {
-            constexpr int HC = H / 16;
             const bool idle = tiles < NW;
             const int step = idle ? NW - tiles : NW;
-            for (int u = idle ? wave - tiles : wave; u >= 0 && u < tiles * 2; u += step)
-                hpl_split_tile<H>(lay, fm, wmap, hn, u >> 1, N, lane, (u & 1) * (HC / 2), HC / 2);
+            for (int ti = idle ? wave - tiles : wave; ti >= 0 && ti < tiles; ti += step)
+                hpl_split_tile<H>(lay, fm, wmap, hn, ti, N, lane);
         }
         sp.mark(2);
         lds_barrier();
