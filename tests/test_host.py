@@ -188,3 +188,61 @@ def test_stepper_two_runs_before_insert_keep_the_ring_intact(monkeypatch):
     ring.insert_episode_batch(b3)
     # b4 took slots 8, 9, 0, 1 (wrap at 10), b3 the next four
     assert (ring["obs"][8:10] == 4).all() and (ring["obs"][0:2] == 4).all() and (ring["obs"][2:6] == 3).all()
+
+
+class _BoundsStepper:
+    """A stepper whose runs resolve lazily: t_env advances by `lens[i]` per run, known exactly only after a resolve
+    (ParallelStepper's run-ahead); bounds = (resolved, resolved + limit per run in flight)."""
+
+    def __init__(self, lens, limit=100, B=4):
+        self.lens, self.limit, self.batch_size = list(lens), limit, B
+        self._t = 0
+        self._pending = []
+        self.resolves = 0
+
+    def run(self):
+        self._pending.append(self.lens.pop(0))
+
+    def t_env_bounds(self):
+        return self._t, self._t + len(self._pending) * self.batch_size * self.limit
+
+    @property
+    def t_env(self):
+        if self._pending:
+            self.resolves += 1
+        self._t += sum(self._pending) * self.batch_size
+        self._pending = []
+        return self._t
+
+
+def test_loop_interval_checks_resolve_only_at_thresholds():
+    """MultiAgentExperiment's t_max / test / save / log checks answer exactly as with the exact t_env, and
+    resolve the runs in flight only when the bounds of t_env straddle a threshold."""
+    from types import SimpleNamespace
+    from maleague.runs.ma_experiment import MultiAgentExperiment
+
+    def run_loop(lens, exact):
+        st = _BoundsStepper(lens)
+        exp = MultiAgentExperiment.__new__(MultiAgentExperiment)
+        exp.args = SimpleNamespace(test_interval=2000, log_interval=3000, save_model=True, save_model_interval=5000,
+                                   test_nepisode=4, batch_size_run=4, t_max=10 ** 9)
+        exp.stepper, exp.last_test_T, exp.last_log_T, exp.model_save_time = st, -2001, 0, 0
+        events = []
+        exp._train_episode = lambda episode_num: st.run()
+        exp._test = lambda n: (events.append(("test", st.t_env)), setattr(exp, "last_test_T", st.t_env))
+        exp.save_models = lambda: (events.append(("save", st.t_env)), setattr(exp, "model_save_time", st.t_env))
+        exp.logger = SimpleNamespace(log_stat=lambda k, v, t: events.append(("log", t)))
+        if exact:  # reference semantics: the exact t_env at every check
+            exp._t_env_reached = lambda thr: st.t_env >= thr
+        ep = 0
+        for _ in range(len(lens)):
+            ep = exp._iteration(ep)
+            if exact:
+                _ = st.t_env
+        return events, st.resolves
+
+    lens = [int(x) for x in np.random.RandomState(0).randint(20, 100, size=60)]
+    ev_exact, _ = run_loop(lens, exact=True)
+    ev_lazy, resolves = run_loop(lens, exact=False)
+    assert ev_lazy == ev_exact and len(ev_exact) > 10
+    assert resolves < len(lens) // 2  # most iterations never waited for their run
