@@ -92,13 +92,15 @@ if int(os.environ.get("TIMELINE", "0")):
     # -DMLG_STAMPS_TIMELINE build: slot k = cycles from the start of the WG's first one-env step to mark k
     order = [(0, "fc1"), (5, "barrier_A"), (1, "gru"), (13, "barrier_B"), (2, "fc2"), (3, "barrier_C"),
              (4, "E1E2"), (6, "E3"), (7, "pair"), (9, "obs"), (11, "avail"), (12, "state"), (8, "tail"), (10, "end")]
-    envw, oth = [], []
+    envw, oth, w0 = [], [], []
     for g in range(grid):
         for w in range(8):
             if a[g, w, 31] != 1 or a[g, w, 10] == 0:
                 continue
             (envw if a[g, w, 7] > 0 else oth).append(a[g, w, :15])
-    for nm, rows in (("env wave", envw), ("other waves", oth)):
+            if w == 0 and a[g, w, 7] == 0:  # wave 0 holds the one tile's fc2 in a one-env step (wave < tiles)
+                w0.append(a[g, w, :15])
+    for nm, rows in (("env wave", envw), ("other waves", oth), ("wave 0 (fc2 tile, no env)", w0)):
         if not rows:
             continue
         r = np.array(rows)
