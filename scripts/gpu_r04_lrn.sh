@@ -1,28 +1,29 @@
 #!/bin/bash
-# Learner A/B: the learner GPU tests, then the train() microbenchmark (scripts/bench_learner.py) for QMIX and REFIL
-# with the default build vs an env switch (AB_ENV, e.g. MLG_REFIL_REC16=1), alternating, and a rocprofv3 stats run.
+# REFIL learner change check: its GPU tests, then train() A/B (this tree vs the PRE variant library, 2 repetitions,
+# scripts/bench_learner.py MODE=refil) and a rocprofv3 kernel split of this tree's train() calls.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-export TMPDIR=/tmp
-mkdir -p gpurun_out/lrn
+O=gpurun_out/lrn2
+mkdir -p $O
 T="python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 500 $T ${TESTS:-tests/test_gpu_learner.py tests/test_gpu_refil_learner.py} > gpurun_out/lrn/tests.log 2>&1 \
-    || { tail -40 gpurun_out/lrn/tests.log; exit 1; }
-tail -1 gpurun_out/lrn/tests.log
+timeout -k 10 400 $T ${TESTS:-tests/test_gpu_refil_learner.py} > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+PRE=${PRE:-prelrn}
 for rep in 1 2; do
-  for mode in ${LMODES:-qmix refil}; do
-    MODE=$mode timeout -k 10 200 python scripts/bench_learner.py > gpurun_out/lrn/${mode}_def_$rep.json 2> gpurun_out/lrn/err.txt \
-        || { tail -20 gpurun_out/lrn/err.txt; exit 1; }
-    echo "$mode default $(cat gpurun_out/lrn/${mode}_def_$rep.json)"
-    if [ -n "$AB_ENV" ]; then
-      env $AB_ENV MODE=$mode timeout -k 10 200 python scripts/bench_learner.py > gpurun_out/lrn/${mode}_ab_$rep.json 2> gpurun_out/lrn/err.txt \
-          || { tail -20 gpurun_out/lrn/err.txt; exit 1; }
-      echo "$mode $AB_ENV $(cat gpurun_out/lrn/${mode}_ab_$rep.json)"
-    fi
+  for v in def $PRE; do
+    lib=ma-league_amd/maleague/_lib/libmaleague.so
+    [ $v = def ] || lib=ma-league_amd/maleague/_lib/variants/$v.so
+    MODE=${MODE:-refil} MLG_LIB=$lib timeout -k 10 300 python scripts/bench_learner.py > $O/${v}_$rep.json 2> $O/${v}_$rep.err \
+        || { echo "bench $v failed"; tail -20 $O/${v}_$rep.err; exit 1; }
+    echo "$v $rep $(cat $O/${v}_$rep.json)"
   done
 done
-for mode in ${LMODES:-qmix refil}; do
-  MODE=$mode REPS=20 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/lrn/prof_$mode" -o run \
-      -- python3 scripts/bench_learner.py > gpurun_out/lrn/prof_$mode.json 2> gpurun_out/lrn/err.txt || { tail -20 gpurun_out/lrn/err.txt; exit 1; }
-  python3 scripts/prof_top.py gpurun_out/lrn/prof_$mode/run_kernel_stats.csv 14
-done
+MODE=${MODE:-refil} REPS=20 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+    python scripts/bench_learner.py > $O/prof.json 2> $O/prof.err || { echo "prof failed"; tail -20 $O/prof.err; exit 1; }
+f=$(find $O/prof -name '*kernel_stats.csv' | head -1)
+python - "$f" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:14]:
+    print(f'{float(r["AverageNs"])/1e3:8.1f} us x{r["Calls"]:>4}  {r["Name"][:70]}')
+PY
