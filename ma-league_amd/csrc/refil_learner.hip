@@ -188,10 +188,10 @@ struct CopyPairs {
     const float* src[kCap];
     float* dst[kCap];
 };
-__global__ void copy_jobs_kernel(CopyJobs J, CopyPairs pp) {
-    const float* __restrict__ src = pp.src[blockIdx.y];
-    float* __restrict__ dst = pp.dst[blockIdx.y];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void copy_jobs_body(const CopyJobs& J, const CopyPairs& pp, int bx, int by) {
+    const float* __restrict__ src = pp.src[by];
+    float* __restrict__ dst = pp.dst[by];
+    const int64_t i = (int64_t)bx * blockDim.x + threadIdx.x;
     if (i >= J.total) return;
     float v = 0.f;
     for (int q = 0; q < J.n; ++q) {
@@ -259,28 +259,28 @@ struct HSplit {
     const float* src[kCap];
     float* dst[kCap];
 };
-__global__ void hyper_split_kernel(HSplit J) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void hyper_split_body(const HSplit& J, int bx, int by) {
+    const int64_t k = (int64_t)bx * blockDim.x + threadIdx.x;
     if (k >= REFIL_HSP) return;
     const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
     const int pc = reg % 3, kk = (reg / 3) % 2, mt = reg / 6;
     const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * (lane >> 4) + i0 % 4;
-    const float* W = J.src[blockIdx.y] + (int64_t)(mt * 16 + (lane & 15)) * EMB;
-    J.dst[blockIdx.y][k] = split_bf16_pair(W[f0], W[f0 + 1], pc);
+    const float* W = J.src[by] + (int64_t)(mt * 16 + (lane & 15)) * EMB;
+    J.dst[by][k] = split_bf16_pair(W[f0], W[f0 + 1], pc);
 }
 
 // in_trans^T [64][192] (the dX1 = W_in^T dQKV operand of the backward kernels) as split-bf16 A operands, from the
 // canonical in_trans [192][64]: element ((reg * 64 + lane) * 4 + q), reg = (tile * 6 + kk) * 3 + piece, tile < 4,
 // kk < 6 (K = 192). blockIdx.y = block (src[y] canonical in_trans, dst[y]).
-__global__ void hyper_splitT_kernel(HSplit J) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void hyper_splitT_body(const HSplit& J, int bx, int by) {
+    const int64_t k = (int64_t)bx * blockDim.x + threadIdx.x;
     if (k >= REFIL_HSP) return;
     const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), reg = (int)(k >> 8);
     const int pc = reg % 3, kk = (reg / 3) % 6, mt = reg / 18;
     const int i0 = 2 * q, f0 = (2 * kk + i0 / 4) * 16 + 4 * (lane >> 4) + i0 % 4;
     const int row = mt * 16 + (lane & 15);
-    const float* W = J.src[blockIdx.y];
-    J.dst[blockIdx.y][k] = split_bf16_pair(W[(int64_t)f0 * EMB + row], W[(int64_t)(f0 + 1) * EMB + row], pc);
+    const float* W = J.src[by];
+    J.dst[by][k] = split_bf16_pair(W[(int64_t)f0 * EMB + row], W[(int64_t)(f0 + 1) * EMB + row], pc);
 }
 
 // acc[mt] += in_trans^T . X over one 16-row tile (X = dQKV rows in LDS, K = 192) as split-bf16 fp32 emulation;
@@ -364,9 +364,9 @@ struct TrJobs {
     TrJob j[kCap];
     int n;
 };
-__global__ void transpose_kernel(TrJobs J) {
-    const TrJob& t = J.j[blockIdx.y];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void transpose_body(const TrJobs& J, int bx, int by) {
+    const TrJob& t = J.j[by];
+    const int64_t i = (int64_t)bx * blockDim.x + threadIdx.x;
     if (i >= (int64_t)t.rows * t.cols) return;
     const int r = (int)(i / t.cols), c = (int)(i % t.cols);
     t.dst[(int64_t)c * t.rows + r] = t.src[i];
@@ -383,8 +383,7 @@ __device__ __forceinline__ float emask_at(const MlgEntityBatch& bt, int b, int t
     return m;
 }
 
-__global__ void mask_sum_kernel(MlgEntityBatch bt, int B, int T, float* __restrict__ msum) {
-    __shared__ float red[1024];
+__device__ void mask_sum_body(const MlgEntityBatch& bt, int B, int T, float* __restrict__ msum, float* red) {
     // msum[1] = max_t_filled (the reference's truncation, ma_experiment.py:235-239): the learner uses transitions
     // t < max_t_filled - 1 only; the sequential kernels stop there and the per-t kernels skip the steps beyond
     int mx = 0;  // a wave per episode: filled steps counted with ballots
@@ -423,8 +422,8 @@ __global__ void mask_sum_kernel(MlgEntityBatch bt, int B, int T, float* __restri
 __device__ __forceinline__ int t_eff(const float* msum) { return (int)msum[1]; }
 
 // entity inputs ein[i][j][c] (K1 columns, zero padded)
-__global__ void ein_kernel(RCfg c, MlgEntityBatch bt, float* __restrict__ ein) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void ein_body(const RCfg& c, const MlgEntityBatch& bt, float* __restrict__ ein, int bx) {
+    const int64_t idx = (int64_t)bx * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)c.I * NE * c.K1) return;
     const int col = (int)(idx % c.K1);
     const int j = (int)((idx / c.K1) % NE);
@@ -439,27 +438,72 @@ __global__ void ein_kernel(RCfg c, MlgEntityBatch bt, float* __restrict__ ein) {
     ein[idx] = v;
 }
 
+// The whole prologue in one launch of 256-thread blocks (was seven launches, each a few microseconds of mostly
+// launch / drain latency): block ranges in this order -- the mask sum (one block, the longest single-block task,
+// dispatched first), the agent packs (online + target), the hypernet packs (4 x 2), the in_trans splits (10), the
+// in_trans^T splits (5), the weight transposes, the entity inputs. The tasks are independent: each reads only the
+// parameters / the batch and writes its own workspace region.
+struct Prologue {
+    CopyJobs aj, hj;
+    CopyPairs ap, hp;
+    HSplit hs, hsT;
+    TrJobs tj;
+    RCfg c;
+    MlgEntityBatch bt;
+    float *ein, *msum;
+    int nb_a, nb_h, nb_s, nb_t, nb_e;  // blocks per agent pack, hypernet pack, split block, transpose job; ein blocks
+};
+static_assert(sizeof(Prologue) <= 4096, "prologue kernel arguments over 4 KB");
+inline int prologue_blocks(const Prologue& P) {
+    return 1 + 2 * P.nb_a + 8 * P.nb_h + 15 * P.nb_s + P.tj.n * P.nb_t + P.nb_e;
+}
+__global__ void __launch_bounds__(256) prologue_kernel(Prologue P) {
+    __shared__ float red[256];
+    int blk = blockIdx.x;
+    if (blk == 0) {
+        mask_sum_body(P.bt, P.c.B, P.c.T, P.msum, red);
+        return;
+    }
+    blk -= 1;
+    if (blk < 2 * P.nb_a) return copy_jobs_body(P.aj, P.ap, blk % P.nb_a, blk / P.nb_a);
+    blk -= 2 * P.nb_a;
+    if (blk < 8 * P.nb_h) return copy_jobs_body(P.hj, P.hp, blk % P.nb_h, blk / P.nb_h);
+    blk -= 8 * P.nb_h;
+    if (blk < 10 * P.nb_s) return hyper_split_body(P.hs, blk % P.nb_s, blk / P.nb_s);
+    blk -= 10 * P.nb_s;
+    if (blk < 5 * P.nb_s) return hyper_splitT_body(P.hsT, blk % P.nb_s, blk / P.nb_s);
+    blk -= 5 * P.nb_s;
+    if (blk < P.tj.n * P.nb_t) return transpose_body(P.tj, blk % P.nb_t, blk / P.nb_t);
+    blk -= P.tj.n * P.nb_t;
+    ein_body(P.c, P.bt, P.ein, blk);
+}
+
 // ---- masks -----------------------------------------------------------------------------------------------
+// a mask row of n <= NE bytes as bits (bit j = byte j != 0), bits >= n set: the NE loads are unrolled and issued
+// back to back (a loop over the runtime n waited for each byte in turn; these sit on every per-item kernel's
+// critical path)
+__device__ __forceinline__ uint32_t mask_row_bits(const uint8_t* row, int n) {
+    uint32_t m = ~((1u << n) - 1u) & 0xFFFFu;
+    uint8_t v[NE];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) v[j] = row[j < n ? j : 0];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) m |= (uint32_t)(j < n && v[j] != 0) << j;
+    return m;
+}
 // entity mask bits of (b, t); bits >= NE set (absent)
 __device__ __forceinline__ uint32_t em_bits(const RCfg& c, const MlgEntityBatch& bt, int b, int t) {
-    const uint8_t* em = bt.entity_mask + (eslot(bt, b) * bt.T1 + t) * c.NE;
-    uint32_t m = ~((1u << c.NE) - 1u) & 0xFFFFu;
-    for (int j = 0; j < c.NE; ++j) m |= (uint32_t)(em[j] != 0) << j;
-    return m;
+    return mask_row_bits(bt.entity_mask + (eslot(bt, b) * bt.T1 + t) * c.NE, c.NE);
 }
 __device__ __forceinline__ uint32_t om_row(const RCfg& c, const MlgEntityBatch& bt, int b, int t, int q) {
     if (q >= c.NE) return 0xFFFFu;
-    const uint8_t* om = bt.obs_mask + ((eslot(bt, b) * bt.T1 + t) * c.NE + q) * c.NE;
-    uint32_t m = ~((1u << c.NE) - 1u) & 0xFFFFu;
-    for (int j = 0; j < c.NE; ++j) m |= (uint32_t)(om[j] != 0) << j;
-    return m;
+    return mask_row_bits(bt.obs_mask + ((eslot(bt, b) * bt.T1 + t) * c.NE + q) * c.NE, c.NE);
 }
 // imagine group bits of episode b: gA = groupA | em0, gB = !groupA | em0 (entity_rnn_agent.py:97-101)
 __device__ __forceinline__ void group_bits(const RCfg& c, const MlgEntityBatch& bt, const uint8_t* groupA, int b,
                                            uint32_t& gA, uint32_t& gB, uint32_t& em0) {
     em0 = em_bits(c, bt, b, 0);
-    uint32_t ga = 0;
-    for (int j = 0; j < c.NE; ++j) ga |= (uint32_t)(groupA[(int64_t)b * c.NE + j] != 0) << j;
+    const uint32_t ga = mask_row_bits(groupA + (int64_t)b * c.NE, c.NE) & ((1u << c.NE) - 1u);
     gA = (ga | em0) & 0xFFFFu;
     gB = ((~ga) | em0) & 0xFFFFu;
 }
@@ -891,87 +935,126 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, M
                 for (int q = lane; q < NAS * EM; q += 64) io.dX[k][((int64_t)v * c.I + i) * NAS * EM + q] = 0.f;
         return;
     }
+    // Every global load of the item is issued before the first one is consumed: one wave per item, so the kernel
+    // time is one item's chain of memory round trips (was ~100 dependent loads: per-agent / per-action loops with a
+    // runtime trip count), not its arithmetic. Two round trips remain: the actions, then the chosen Q they index.
     const int64_t srow = eslot(bt, b) * bt.T1;
-    const uint32_t dead = dead_bits(c, em_bits(c, bt, b, t));
-    // ---- chosen Q of the three copies, target max (double Q) ----
-    float caq[3][NAS], tmax[NAS];
-    int act[NAS];
+    const int hl = lane >> 5;  // half-wave: agent 2p + hl of pass p for the per-action rows (lane e = action)
+    const int an = lane < NA ? (int)bt.actions[(srow + t) * NA + (lane < NA ? lane : 0)] : 0;
+    const bool emv = lane < c.NE && bt.entity_mask[(srow + t) * c.NE + (lane < c.NE ? lane : 0)] != 0;
+    const float r = bt.reward[srow + t];
+    const float term = (float)bt.terminated[srow + t];
+    const float m = emask_at(bt, b, t);
+    int avv[NAS / 2];
+    float tqv[NAS / 2], mqv[NAS / 2];
+#pragma unroll
+    for (int p = 0; p < NAS / 2; ++p) {
+        const int n = 2 * p + hl, nn = n < NA ? n : 0, aa = e < c.A ? e : 0;
+        avv[p] = bt.avail[((srow + t + 1) * NA + nn) * c.A + aa];
+        tqv[p] = io.tmac[((int64_t)(t + 1) * c.Rtg + (int64_t)b * NA + nn) * c.A + aa];
+        mqv[p] = c.double_q ? io.mac[((int64_t)(t + 1) * c.Ron + (int64_t)b * NA + nn) * c.A + aa] : 0.f;
+    }
+    // column e of every hypernet output row (rows n >= NA are allocated; their values are never used)
+    const int64_t xo = (int64_t)i * NAS * EM + e, vstride = (int64_t)c.I * NAS * EM;
+    float xt[4][NAS], xP[NAS], xW[NAS], xI[NAS], xwf[NAS], xb1[NAS], xV[NAS];
+#pragma unroll
     for (int n = 0; n < NAS; ++n) {
-        act[n] = 0;
-        tmax[n] = 0.f;
-        for (int cc = 0; cc < 3; ++cc) caq[cc][n] = 0.f;
-        if (n >= NA) continue;
-        const int a = (int)bt.actions[(srow + t) * NA + n];
-        act[n] = a;
-        for (int cc = 0; cc < 3; ++cc)
-            caq[cc][n] = io.mac[((int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * NA + n) * c.A + a];
-        const int32_t* av = bt.avail + ((srow + t + 1) * NA + n) * c.A;
-        const float* tq = io.tmac + ((int64_t)(t + 1) * c.Rtg + (int64_t)b * NA + n) * c.A;
-        if (c.double_q) {
-            const float* mq = io.mac + ((int64_t)(t + 1) * c.Ron + (int64_t)b * NA + n) * c.A;
-            float bv = 0.f;
-            int bi = -1;
-            for (int a2 = 0; a2 < c.A; ++a2) {
-                const float v = av[a2] == 0 ? -9999999.f : mq[a2];
-                if (bi < 0 || amax_better(v, a2, bv, bi)) { bv = v; bi = a2; }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xt[k][n] = io.Xtg[k][xo + n * EM];
+        xP[n] = io.X[0][xo + n * EM];
+        xW[n] = io.X[0][vstride + xo + n * EM];
+        xI[n] = io.X[0][2 * vstride + xo + n * EM];
+        xwf[n] = io.X[1][xo + n * EM];
+        xb1[n] = io.X[2][xo + n * EM];
+        xV[n] = io.X[3][xo + n * EM];
+    }
+    float caqv[3];  // lane n < NA: chosen Q of agent n in each copy
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc)
+        caqv[cc] = lane < NA ? io.mac[((int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * NA + (lane < NA ? lane : 0)) * c.A + an]
+                             : 0.f;
+    const uint32_t dead = dead_bits(c, (~((1u << c.NE) - 1u) & 0xFFFFu) | ((uint32_t)__ballot(emv) & 0xFFFFu));
+    // ---- target max (double Q: the online argmax over the available actions picks the target Q) ----
+    float tmax[NAS];
+#pragma unroll
+    for (int p = 0; p < NAS / 2; ++p) {
+        const int n = 2 * p + hl;
+        const bool ok = n < NA && e < c.A;
+        const float tqm = avv[p] == 0 ? -9999999.f : tqv[p];
+        float res;
+        if (c.double_q) {  // argmax with the sequential scan's order (NaN first, ties -> lowest index): a total order
+            float bv = ok ? (avv[p] == 0 ? -9999999.f : mqv[p]) : -INFINITY;
+            int bi = ok ? e : 64 + e;
+#pragma unroll
+            for (int s2 = 1; s2 < 32; s2 <<= 1) {
+                const float ov = __shfl_xor(bv, s2);
+                const int oi = __shfl_xor(bi, s2);
+                const bool take = amax_better(ov, oi, bv, bi);
+                bv = take ? ov : bv;
+                bi = take ? oi : bi;
             }
-            tmax[n] = av[bi] == 0 ? -9999999.f : tq[bi];
-        } else {
-            float bv = 0.f;
-            for (int a2 = 0; a2 < c.A; ++a2) {
-                const float v = av[a2] == 0 ? -9999999.f : tq[a2];
-                bv = a2 == 0 ? v : fmaxf(bv, v);
-            }
-            tmax[n] = bv;
+            res = __shfl(tqm, hl * 32 + (bi & 31));
+        } else {  // fmaxf ignores NaN operands like the sequential fmaxf scan; NaN pads are neutral
+            res = ok ? tqm : __builtin_nanf("");
+#pragma unroll
+            for (int s2 = 1; s2 < 32; s2 <<= 1) res = fmaxf(res, __shfl_xor(res, s2));
         }
+        tmax[2 * p] = __shfl(res, 0);
+        tmax[2 * p + 1] = __shfl(res, 32);
+    }
+    float caq[3][NAS];
+    int act[NAS];
+#pragma unroll
+    for (int n = 0; n < NAS; ++n) {
+        act[n] = __shfl(an, n);
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) caq[cc][n] = __shfl(caqv[cc], n);
     }
     const float invN = 1.f / (float)NA, invNE = 1.f / ((float)NA * (float)EM);
-    // column e of each hypernet output over the agent rows
-    auto col_sum = [&](const float* X) {
+    auto col_sum = [&](const float(&x)[NAS]) {  // column e over the agent rows, in row order
         float s = 0.f;
-        for (int n = 0; n < NA; ++n) s += X[n * EM + e];
+#pragma unroll
+        for (int n = 0; n < NAS; ++n)
+            if (n < NA) s += x[n];
         return s;
     };
     // ---- target mixer (flex_qmix on the t + 1 entities, target weights) ----
     float y_tg;
     {
-        const float* Xw1 = io.Xtg[0] + (int64_t)i * NAS * EM;
-        float pre = col_sum(io.Xtg[2] + (int64_t)i * NAS * EM) * invN;  // b1
-        for (int n = 0; n < NA; ++n) pre += tmax[n] * mw(Xw1[n * EM + e], c.softmax);
+        float pre = col_sum(xt[2]) * invN;  // b1
+#pragma unroll
+        for (int n = 0; n < NAS; ++n)
+            if (n < NA) pre += tmax[n] * mw(xt[0][n], c.softmax);
         const float hid = elu_f(pre);
-        const float wf = mw(col_sum(io.Xtg[1] + (int64_t)i * NAS * EM) * invN, c.softmax);
-        const float vsum = sum32(col_sum(io.Xtg[3] + (int64_t)i * NAS * EM));
+        const float wf = mw(col_sum(xt[1]) * invN, c.softmax);
+        const float vsum = sum32(col_sum(xt[3]));
         y_tg = sum32(hid * wf) + vsum * invNE;
     }
     // ---- online mixer: plain and imagined ----
-    const float* XP = io.X[0] + ((int64_t)0 * c.I + i) * NAS * EM;
-    const float* XW = io.X[0] + ((int64_t)1 * c.I + i) * NAS * EM;
-    const float* XI = io.X[0] + ((int64_t)2 * c.I + i) * NAS * EM;
-    const float* Xwf = io.X[1] + (int64_t)i * NAS * EM;
-    const float* Xb1 = io.X[2] + (int64_t)i * NAS * EM;
-    const float* XV = io.X[3] + (int64_t)i * NAS * EM;
-    const float b1 = col_sum(Xb1) * invN;
-    const float wfpre = col_sum(Xwf) * invN;
+    const float b1 = col_sum(xb1) * invN;
+    const float wfpre = col_sum(xwf) * invN;
     const float wf = mw(wfpre, c.softmax);
-    const float vv = sum32(col_sum(XV)) * invNE;
+    const float vv = sum32(col_sum(xV)) * invNE;
     float w1P[NAS], w1W[NAS], w1I[NAS];
     float preP = b1, preI = b1;
+#pragma unroll
     for (int n = 0; n < NAS; ++n) {
         w1P[n] = w1W[n] = w1I[n] = 0.f;
         if (n >= NA) continue;
-        w1P[n] = mw(XP[n * EM + e], c.softmax);
-        w1W[n] = mw(XW[n * EM + e], c.softmax);
-        w1I[n] = mw(XI[n * EM + e], c.softmax);
+        w1P[n] = mw(xP[n], c.softmax);
+        w1W[n] = mw(xW[n], c.softmax);
+        w1I[n] = mw(xI[n], c.softmax);
         preP += caq[0][n] * w1P[n];
     }
-    for (int n = 0; n < NA; ++n) preI += caq[1][n] * w1W[n];
-    for (int n = 0; n < NA; ++n) preI += caq[2][n] * w1I[n];
+#pragma unroll
+    for (int n = 0; n < NAS; ++n)
+        if (n < NA) preI += caq[1][n] * w1W[n];
+#pragma unroll
+    for (int n = 0; n < NAS; ++n)
+        if (n < NA) preI += caq[2][n] * w1I[n];
     const float hidP = elu_f(preP), hidI = elu_f(preI);
     const float yP = sum32(hidP * wf) + vv;
     const float yI = sum32(hidI * wf) + vv;
-    const float r = bt.reward[srow + t];
-    const float term = (float)bt.terminated[srow + t];
-    const float m = emask_at(bt, b, t);
     const float target = r + c.gamma * (1.f - term) * y_tg;
     const float tdP = (yP - target) * m, tdI = (yI - target) * m;
     if (lane == 0) {
@@ -1001,13 +1084,14 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, M
     float* dXb1 = io.dX[2] + (int64_t)i * NAS * EM;
     float* dXV = io.dX[3] + (int64_t)i * NAS * EM;
     float dqP[NAS], dqW[NAS], dqI[NAS];
+#pragma unroll
     for (int n = 0; n < NAS; ++n) {
         const bool live = n < NA && !((dead >> n) & 1u);
         float vP = 0.f, vW = 0.f, vI = 0.f, vwf = 0.f, vb1 = 0.f, vV = 0.f;
         if (n < NA) {
-            vP = mw_bwd(caq[0][n] * dpP, w1P[n], XP[n * EM + e], c.softmax);
-            vW = mw_bwd(caq[1][n] * dpI, w1W[n], XW[n * EM + e], c.softmax);
-            vI = mw_bwd(caq[2][n] * dpI, w1I[n], XI[n * EM + e], c.softmax);
+            vP = mw_bwd(caq[0][n] * dpP, w1P[n], xP[n], c.softmax);
+            vW = mw_bwd(caq[1][n] * dpI, w1W[n], xW[n], c.softmax);
+            vI = mw_bwd(caq[2][n] * dpI, w1I[n], xI[n], c.softmax);
             vwf = dwfpre * invN;
             vb1 = db1 * invN;
             vV = dv * invNE;
@@ -1024,15 +1108,24 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, M
             dXV[n * EM + e] = live ? vV : 0.f;
         }
     }
-    if (lane < NA) {  // dQ of the chosen actions (masked agents: q was masked_fill'ed -> 0)
-        const int n = lane;
-        const bool live = !((dead >> n) & 1u);
-        const float dd[3] = {dqP[n], dqW[n], dqI[n]};
+    // dQ of the chosen actions (masked agents: q was masked_fill'ed -> 0) and whole d2 rows (no memset pass):
+    // half-wave hl writes agent 2p + hl, lane e action e
+#pragma unroll
+    for (int p = 0; p < NAS / 2; ++p) {
+        const int n = 2 * p + hl;
+        if (2 * p >= NA) break;
+        const bool live = n < NA && !((dead >> n) & 1u);
+        const int actn = hl ? act[2 * p + 1] : act[2 * p];
+        const float dd[3] = {hl ? dqP[2 * p + 1] : dqP[2 * p], hl ? dqW[2 * p + 1] : dqW[2 * p],
+                             hl ? dqI[2 * p + 1] : dqI[2 * p]};
+#pragma unroll
         for (int cc = 0; cc < 3; ++cc) {
             const int64_t row = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * NA + n;
             const float v = live ? dd[cc] : 0.f;
-            io.dq[row] = v;
-            for (int a2 = 0; a2 < c.A; ++a2) io.d2[row * c.A + a2] = a2 == act[n] ? v : 0.f;  // whole row: no memset
+            if (n < NA) {
+                if (e < c.A) io.d2[row * c.A + e] = e == actn ? v : 0.f;
+                if (e == 0) io.dq[row] = v;
+            }
         }
     }
 }
@@ -1441,19 +1534,19 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     const float* params = bufs->params;
     const float* tparams = bufs->target_params;
     const WsR& w = p.w;
-    // ---- pack: three launches (agent blocks, hypernet blocks, all transposes) ----
-    const CopyJobs aj = agent_jobs(p.La), hj = hyper_jobs(p.Lh);
-    MLG_REQUIRE(!aj.overflow && !hj.overflow, "refil learner: pack job table over capacity (%d)", CopyJobs::kCap);
+    // ---- prologue, one launch: mask sum, parameter packs, in_trans splits, transposes, entity inputs ----
+    Prologue P{};
+    P.aj = agent_jobs(p.La);
+    P.hj = hyper_jobs(p.Lh);
+    MLG_REQUIRE(!P.aj.overflow && !P.hj.overflow, "refil learner: pack job table over capacity (%d)", CopyJobs::kCap);
     static_assert(2 * 4 <= CopyPairs::kCap && 2 * 4 + 2 <= HSplit::kCap, "prologue tables: one slot per block");
-    CopyPairs ap{}, hpp{};
-    ap.src[0] = params;
-    ap.dst[0] = ws + w.pa_on;
-    ap.src[1] = tparams;
-    ap.dst[1] = ws + w.pa_tg;
-    hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((aj.total + 255) / 256), 2), dim3(256), 0, s, aj, ap);
+    P.ap.src[0] = params;
+    P.ap.dst[0] = ws + w.pa_on;
+    P.ap.src[1] = tparams;
+    P.ap.dst[1] = ws + w.pa_tg;
     const RAgent& La = p.La;
-    TrJobs tj{};
-    bool tr_bad = false;  // the transpose grid covers jobs of <= 3 * EMB * EMB elements, TrJobs::kCap jobs
+    TrJobs& tj = P.tj;
+    bool tr_bad = false;  // the transpose blocks cover jobs of <= 3 * EMB * EMB elements, TrJobs::kCap jobs
     auto tr = [&](const float* src, float* dst, int rows, int cols) {
         if (tj.n < TrJobs::kCap && (int64_t)rows * cols <= 3 * EMB * EMB) tj.j[tj.n++] = TrJob{src, dst, rows, cols};
         else tr_bad = true;
@@ -1464,17 +1557,16 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     tr(params + La.c_wih, ws + w.a_wihT, 3 * EMB, EMB);
     for (int k = 0; k < 4; ++k) {
         const int64_t G0 = p.n_agent + (int64_t)k * p.Lh.c_total;
-        hpp.src[2 * k] = params + G0;
-        hpp.dst[2 * k] = ws + w.ph_on[k];
-        hpp.src[2 * k + 1] = tparams + G0;
-        hpp.dst[2 * k + 1] = ws + w.ph_tg[k];
+        P.hp.src[2 * k] = params + G0;
+        P.hp.dst[2 * k] = ws + w.ph_on[k];
+        P.hp.src[2 * k + 1] = tparams + G0;
+        P.hp.dst[2 * k + 1] = ws + w.ph_tg[k];
         tr(params + G0 + p.Lh.c_win, ws + w.h_winT[k], 3 * EMB, EMB);
         tr(params + G0 + p.Lh.c_wout, ws + w.h_woutT[k], EMB, EMB);
         tr(params + G0 + p.Lh.c_w2, ws + w.h_w2T[k], EM, EMB);
     }
     MLG_REQUIRE(!tr_bad, "refil learner: transpose job table over capacity or job larger than the grid");
-    hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)((hj.total + 255) / 256), 8), dim3(256), 0, s, hj, hpp);
-    HSplit hs{};
+    HSplit& hs = P.hs;
     for (int k = 0; k < 4; ++k) {
         const int64_t G0 = p.n_agent + (int64_t)k * p.Lh.c_total;
         hs.src[k] = params + G0 + p.Lh.c_win;
@@ -1486,20 +1578,22 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     hs.src[9] = tparams + La.c_win;
     hs.dst[8] = ws + w.h_wsp[8];
     hs.dst[9] = ws + w.h_wsp[9];
-    hipLaunchKernelGGL(hyper_split_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 10), dim3(256), 0, s, hs);
-    HSplit hsT{};
     for (int k = 0; k < 4; ++k) {
-        hsT.src[k] = hs.src[k];
-        hsT.dst[k] = ws + w.h_wspT[k];
+        P.hsT.src[k] = hs.src[k];
+        P.hsT.dst[k] = ws + w.h_wspT[k];
     }
-    hsT.src[4] = params + La.c_win;
-    hsT.dst[4] = ws + w.h_wspT[4];
-    hipLaunchKernelGGL(hyper_splitT_kernel, dim3((unsigned)((REFIL_HSP + 255) / 256), 5), dim3(256), 0, s, hsT);
-    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((3 * EMB * EMB + 255) / 256), (unsigned)tj.n), dim3(256), 0, s,
-                       tj);
-    hipLaunchKernelGGL(mask_sum_kernel, dim3(1), dim3(1024), 0, s, bt, c.B, c.T, ws + w.msum);
-    const int64_t n_ein = (int64_t)c.I * NE * c.K1;
-    hipLaunchKernelGGL(ein_kernel, dim3((unsigned)((n_ein + 255) / 256)), dim3(256), 0, s, c, bt, ws + w.ein);
+    P.hsT.src[4] = params + La.c_win;
+    P.hsT.dst[4] = ws + w.h_wspT[4];
+    P.c = c;
+    P.bt = bt;
+    P.ein = ws + w.ein;
+    P.msum = ws + w.msum;
+    P.nb_a = (int)((P.aj.total + 255) / 256);
+    P.nb_h = (int)((P.hj.total + 255) / 256);
+    P.nb_s = (int)((REFIL_HSP + 255) / 256);
+    P.nb_t = (3 * EMB * EMB + 255) / 256;
+    P.nb_e = (int)(((int64_t)c.I * NE * c.K1 + 255) / 256);
+    hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)prologue_blocks(P)), dim3(256), 0, s, P);
     // ---- agent forward ----
     AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on,
                  ws + w.h_wsp[8]};
