@@ -40,7 +40,9 @@ import torch  # noqa: E402
 
 FP32_MFMA_PEAK = 157.3e12  # MI355X dense fp32 (MFMA == VALU rate), MI355X_MICROARCH.md chip table
 HBM_PEAK = 8.0e12
-TIMING_EVERY = 1  # HIP-event pair around every k-th rollout launch of the timed region (--timing-every)
+# HIP-event pair around every k-th rollout launch of the timed region (--timing-every): an event pair on every
+# launch costs ~8 us of queue time per iteration (its system-scope release fence; profiles/r04/s11_timing_ab/)
+TIMING_EVERY = 4
 METRIC = "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X"
 COUNTERS_JSON = os.path.join(ROOT, "profiles", "counters.json")
 
@@ -102,7 +104,8 @@ def timed_loop(ctx: Ctx, iteration, stepper, steps: int, warmup: int) -> dict:
     ctx.barrier()
     timing_ok = ctx.dev.type == "cuda"
     stepper.timing = [] if timing_ok else None
-    stepper.timing_every = TIMING_EVERY
+    stepper.timing_every = TIMING_EVERY if steps >= 2 * TIMING_EVERY else 1  # short runs: every launch
+    stepper._launches = 0  # sampled launches counted from the start of the timed region
     t0_env = stepper.t_env
     rows0 = int(stepper.agent_rows.item())
     ctx.sync()
@@ -336,8 +339,9 @@ def main():
     ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--timing-every", type=int, default=1,
-                    help="HIP events around every k-th rollout launch of the timed region (0: none, A/B only)")
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="HIP events around every k-th rollout launch of the timed region (0: none, A/B only; "
+                         "every launch when --steps < 2k)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / process-group plumbing only: init the group, report the world, run no leg")
     argv = sys.argv[1:]
