@@ -20,7 +20,7 @@ def _bench(*args, timeout=240):
                           timeout=timeout, env=env, cwd=ROOT)
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])  # 8: the driver's full-node run
 def test_bench_gpus_n_self_launches_n_ranks(n):
     p = _bench("--gpus", str(n), "--backend", "gloo", "--dry-run")
     assert p.returncode == 0, p.stderr[-2000:]
