@@ -40,9 +40,11 @@ import torch  # noqa: E402
 
 FP32_MFMA_PEAK = 157.3e12  # MI355X dense fp32 (MFMA == VALU rate), MI355X_MICROARCH.md chip table
 HBM_PEAK = 8.0e12
-# HIP-event pair around every k-th rollout launch of the timed region (--timing-every): an event pair on every
-# launch costs ~8 us of queue time per iteration (its system-scope release fence; profiles/r04/s11_timing_ab/)
-TIMING_EVERY = 4
+# HIP-event pair around every k-th rollout launch of the timed region (--timing-every). Every launch (default): the
+# pair costs ~8-10 us of queue time per iteration (0.7 % of ms_per_step at config 2, a device-scope-release event
+# pair the same), but a sample of every 4th launch biases the kernel average (launch times vary 0.68-1.03 ms with
+# the iteration's longest episode): profiles/r04/s11_timing_ab/
+TIMING_EVERY = 1
 METRIC = "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X"
 COUNTERS_JSON = os.path.join(ROOT, "profiles", "counters.json")
 
@@ -339,7 +341,7 @@ def main():
     ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--timing-every", type=int, default=4,
+    ap.add_argument("--timing-every", type=int, default=1,
                     help="HIP events around every k-th rollout launch of the timed region (0: none, A/B only; "
                          "every launch when --steps < 2k)")
     ap.add_argument("--dry-run", action="store_true",
