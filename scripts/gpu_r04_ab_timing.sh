@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/ab
 for rep in 1 2 3; do
-  for te in 1 4 0; do
+  for te in ${TES:-1 4 0}; do
     for m in ${MODES:-ai}; do
       timeout -k 10 200 python bench.py --mode $m --steps 30 --warmup 5 --no-cpu-baseline --timing-every $te \
           > gpurun_out/ab/${m}_te${te}_$rep.json 2> gpurun_out/ab/${m}_te${te}_$rep.err || { tail -20 gpurun_out/ab/${m}_te${te}_$rep.err; exit 1; }
