@@ -1025,17 +1025,22 @@ extern "C" int mlg_refil_rollout(const MlgEntityEnvSpec* spec, MlgEnvState* st, 
     const bool v1 = (var && strcmp(var, "v1") == 0) || L.K1 != 32;
     if (!v1) {
         const size_t lds4 = sizeof(R4Shared);
-        static bool attr4 = false;
-        if (!attr4) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(refil_rollout4_kernel<2>),
+        // the refil_8 shape (16 units: the checks above fix the rest of the dims) as the static instantiation
+        // (MLG_REFIL_GENERIC=1: the generic one, A/B)
+        const bool generic = getenv("MLG_REFIL_GENERIC") != nullptr;
+        const bool st16 = sp.U == 16 && !generic;
+        auto kern4 = st16 ? refil_rollout4_kernel<2, 16> : refil_rollout4_kernel<2, 0>;
+        static bool attr4[2] = {false, false};
+        if (!attr4[st16]) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern4),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4);
             if (e != hipSuccess) return mlg::fail("refil_rollout: LDS %zu B: %s", lds4, hipGetErrorString(e));
-            attr4 = true;
+            attr4[st16] = true;
         }
         const int per_block4 = R4_ENVS * R4_WAVES;
-        hipLaunchKernelGGL(refil_rollout4_kernel<2>, dim3((unsigned)((bt.B + per_block4 - 1) / per_block4)),
-                           dim3(64 * R4_WAVES), lds4, (hipStream_t)stream, *spec, *st, L, packed, bt, *info, a,
-                           test_mode ? 0.f : epsilon, test_mode);
+        hipLaunchKernelGGL(kern4, dim3((unsigned)((bt.B + per_block4 - 1) / per_block4)), dim3(64 * R4_WAVES), lds4,
+                           (hipStream_t)stream, *spec, *st, L, packed, bt, *info, a, test_mode ? 0.f : epsilon,
+                           test_mode);
         return mlg::check_launch("refil_rollout4");
     }
     auto kern = L.K1 <= 16 ? refil_rollout_kernel<1> : (L.K1 <= 32 ? refil_rollout_kernel<2> : refil_rollout_kernel<3>);

@@ -85,11 +85,28 @@ def _rollout(device, B=12, T=40, seed=5, eps=0.0, test_mode=True, ring=None, age
     return spec, ag, a, np_batch(batch), summary, st
 
 
-@pytest.fixture(params=["v4", "v1"])
+@pytest.fixture(params=["v4", "v4g", "v1"])
 def rollout_variant(request, monkeypatch):
-    """v4: four envs per wave (refil_ro4.inc, the default); v1: the two-env kernel (MLG_REFIL_ROLLOUT=v1)."""
-    monkeypatch.setenv("MLG_REFIL_ROLLOUT", request.param)
+    """v4: four envs per wave (refil_ro4.inc, the default; the refil_8 plan runs its static-shape instantiation);
+    v4g: the same kernel's generic instantiation (MLG_REFIL_GENERIC=1); v1: the two-env kernel (MLG_REFIL_ROLLOUT=v1)."""
+    monkeypatch.setenv("MLG_REFIL_ROLLOUT", "v1" if request.param == "v1" else "v4")
+    if request.param == "v4g":
+        monkeypatch.setenv("MLG_REFIL_GENERIC", "1")
     return request.param
+
+
+def test_rollout_static_shape_equals_generic(device, monkeypatch):
+    """The refil_8 static-shape instantiation of the four-env kernel (layout offsets and dims as immediates) writes
+    the same bytes as its generic instantiation: 256 envs (16 workgroups), train mode, episode limit 100."""
+    from maleague.envs.teams_env import VecEnvState
+    B, T, seed, eps = 256, 100, 3, 0.1
+    spec, ag, a, nb0, s0, _ = _rollout(device, B, T, seed, eps, test_mode=False)
+    monkeypatch.setenv("MLG_REFIL_GENERIC", "1")
+    *_, nb1, s1, _ = _rollout(device, B, T, seed, eps, test_mode=False, st=VecEnvState(spec, B, device))
+    for k in nb0:
+        np.testing.assert_array_equal(nb0[k], nb1[k], err_msg=k)
+    for k in s0:
+        np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
 
 
 @pytest.mark.parametrize("eps,test_mode,B,T,seed", [(0.0, True, 12, 40, 5), (0.3, False, 12, 40, 5),
