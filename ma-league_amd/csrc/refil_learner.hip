@@ -169,6 +169,31 @@ Plan make_plan(const MlgRefilLearnerCfg* cfg, int T1) {
     return p;
 }
 
+// The refil_8 shape (8 agent slots, 16 entities, entity width 8 + the 21-action last-action one-hot, 21 actions) as
+// a static instantiation of the per-item kernels (S8 = 1): their dims and the packed-block offsets become
+// immediates (loops over agents / entities unrolled, no kernel-argument SGPRs held across them). Other shapes run
+// S8 = 0 with the same code.
+struct S8Dims {
+    static constexpr int NA = 8, NE = 16, ED = 8, A = 21, D0 = 29, K1 = 32, Ap = 32;
+};
+template <int S8>
+__device__ __forceinline__ RCfg static_cfg(RCfg c) {
+    if constexpr (S8 != 0) {
+        c.NA = S8Dims::NA;
+        c.NE = S8Dims::NE;
+        c.ED = S8Dims::ED;
+        c.A = S8Dims::A;
+        c.D0 = S8Dims::D0;
+        c.K1 = S8Dims::K1;
+        c.Ap = S8Dims::Ap;
+    }
+    return c;
+}
+inline bool is_s8(const RCfg& c) {
+    return c.NA == S8Dims::NA && c.NE == S8Dims::NE && c.ED == S8Dims::ED && c.A == S8Dims::A && c.D0 == S8Dims::D0 &&
+           getenv("MLG_REFIL_GENERIC") == nullptr;
+}
+
 // ---- small kernels ---------------------------------------------------------------------------------------
 struct CopyJob {
     int64_t src, src2, dst;
@@ -526,9 +551,12 @@ struct AgentPtrs {
     const float* wsp;  // split-bf16 in_trans (hyper_split_kernel layout)
 };
 
-__global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
-                                                     RAgent L, const float* __restrict__ ein, AgentPtrs on,
+template <int S8>
+__global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c_arg, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
+                                                     RAgent L_arg, const float* __restrict__ ein, AgentPtrs on,
                                                      AgentPtrs tg, const float* __restrict__ msum) {
+    const RCfg c = static_cfg<S8>(c_arg);
+    const RAgent L = S8 ? make_ragent(S8Dims::D0, S8Dims::A) : L_arg;
     __shared__ float s_ein[NE * LDI];
     __shared__ float s_x1[NE * LDX];
     __shared__ float s_qkv[NE * LDQ];
@@ -735,10 +763,13 @@ __device__ __forceinline__ void row_bn(const RCfg& c, int r, int& b, int& n) {
 }
 
 // fc3 for every (t, row): grid (ntiles_max, T, 2), Ap/16 waves (wave = action tile); masked agents -> 0
-__global__ void __launch_bounds__(128) q_kernel(RCfg c, MlgEntityBatch bt, RAgent L, const float* __restrict__ Pon,
+template <int S8>
+__global__ void __launch_bounds__(128) q_kernel(RCfg c_arg, MlgEntityBatch bt, RAgent L_arg, const float* __restrict__ Pon,
                                                 const float* __restrict__ Ptg, const float* __restrict__ hs_on,
                                                 const float* __restrict__ hs_tg, float* __restrict__ mac,
                                                 float* __restrict__ tmac, const float* __restrict__ msum) {
+    const RCfg c = static_cfg<S8>(c_arg);
+    const RAgent L = S8 ? make_ragent(S8Dims::D0, S8Dims::A) : L_arg;
     const bool online = blockIdx.z == 0;
     const int R = online ? c.Ron : c.Rtg;
     const int tile = blockIdx.x, t = blockIdx.y;
@@ -779,9 +810,12 @@ struct HypPtrs {
     float* Xtg[4];
 };
 
-__global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
-                                                       RHyper L, const float* __restrict__ ein, HypPtrs hp,
+template <int S8>
+__global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c_arg, MlgEntityBatch bt, const uint8_t* __restrict__ groupA,
+                                                       RHyper L_arg, const float* __restrict__ ein, HypPtrs hp,
                                                        const float* __restrict__ msum) {
+    const RCfg c = static_cfg<S8>(c_arg);
+    const RHyper L = S8 ? make_rhyper(S8Dims::D0) : L_arg;
     // s_ein and s_x1 live inside s_o (dead before the attention writes it): 21 KB of LDS per item instead of 29 KB,
     // seven workgroups per CU instead of five
     static_assert(NE * LDI + NE * LDX <= 32 * LDX, "s_ein + s_x1 alias s_o");
@@ -913,7 +947,9 @@ __device__ __forceinline__ float mw_bwd(float dy, float y, float x, int softmax)
     return y * (dy - sum32(y * dy));
 }
 
-__global__ void __launch_bounds__(64) mix_td_kernel(RCfg c, MlgEntityBatch bt, MixIO io) {
+template <int S8>
+__global__ void __launch_bounds__(64) mix_td_kernel(RCfg c_arg, MlgEntityBatch bt, MixIO io) {
+    const RCfg c = static_cfg<S8>(c_arg);
     const int Te = (int)io.msum[1];
     const int lane = threadIdx.x;
     const int i = blockIdx.x;
@@ -1146,8 +1182,10 @@ struct HypBwd {
     float* dfc1m[4];
 };
 
-__global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c, MlgEntityBatch bt, HypBwd hb,
+template <int S8>
+__global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c_arg, MlgEntityBatch bt, HypBwd hb,
                                                        const float* __restrict__ msum) {
+    const RCfg c = static_cfg<S8>(c_arg);
     __shared__ float s_qkv[NE * LDQ];
     __shared__ float s_dqkv[NE * LDQ];
     __shared__ float s_do[32 * LDX];
@@ -1346,8 +1384,10 @@ struct EntBwd {
     float *dfc2, *dout, *dqkv, *dfc1;
 };
 
-__global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c, MlgEntityBatch bt, EntBwd eb,
+template <int S8>
+__global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch bt, EntBwd eb,
                                                      const float* __restrict__ msum) {
+    const RCfg c = static_cfg<S8>(c_arg);
     __shared__ float s_do[3][16 * LDX];
     __shared__ float s_qkv[NE * LDQ];
     __shared__ float s_dqkv[NE * LDQ];
@@ -1529,6 +1569,7 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
 
 int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs* bufs, hipStream_t s) {
     const RCfg& c = p.c;
+    const bool s8 = is_s8(c);  // the refil_8 shape: static instantiations of the per-item kernels
     float* ws = bufs->workspace;
     const MlgEntityBatch& bt = bufs->batch;
     const float* params = bufs->params;
@@ -1598,7 +1639,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on,
                  ws + w.h_wsp[8]};
     AgentPtrs tg{ws + w.pa_tg, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ws + w.gi_tg, ws + w.h_wsp[9]};
-    hipLaunchKernelGGL(ent_fwd_kernel, dim3((unsigned)((c.I + 1) / 2), 2), dim3(64), 0, s, c, bt, bufs->groupA, La,
+    hipLaunchKernelGGL(s8 ? ent_fwd_kernel<1> : ent_fwd_kernel<0>, dim3((unsigned)((c.I + 1) / 2), 2), dim3(64), 0, s, c,
+                       bt, bufs->groupA, La,
                        ws + w.ein, on, tg, ws + w.msum);
     const int nt_on = (c.Ron + 15) / 16, nt_tg = (c.Rtg + 15) / 16;
     // the recurrences on 4-row tiles (default) or 16-row tiles (MLG_REFIL_REC16, A/B)
@@ -1611,7 +1653,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hipLaunchKernelGGL(rec4_kernel, dim3((unsigned)((c.Ron + 3) / 4 + (c.Rtg + 3) / 4)), dim3(256), 0, s, c, La,
                            ws + w.pa_on, ws + w.pa_tg, ws + w.gi_on, ws + w.gi_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.gr,
                            ws + w.gz, ws + w.gn, ws + w.ghn, ws + w.msum);
-    hipLaunchKernelGGL(q_kernel, dim3((unsigned)nt_on, (unsigned)c.T, 2), dim3(64 * (c.Ap / 16)), 0, s, c, bt, La,
+    hipLaunchKernelGGL(s8 ? q_kernel<1> : q_kernel<0>, dim3((unsigned)nt_on, (unsigned)c.T, 2), dim3(64 * (c.Ap / 16)), 0,
+                       s, c, bt, La,
                        ws + w.pa_on, ws + w.pa_tg, ws + w.hs_on, ws + w.hs_tg, ws + w.mac, ws + w.tmac, ws + w.msum);
     // ---- mixer ----
     HypPtrs hp;
@@ -1627,7 +1670,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hp.X[k] = ws + w.X[k];
         hp.Xtg[k] = ws + w.Xtg[k];
     }
-    hipLaunchKernelGGL(hyper_fwd_kernel, dim3((unsigned)c.I, 8), dim3(64), 0, s, c, bt, bufs->groupA, p.Lh, ws + w.ein, hp,
+    hipLaunchKernelGGL(s8 ? hyper_fwd_kernel<1> : hyper_fwd_kernel<0>, dim3((unsigned)c.I, 8), dim3(64), 0, s, c, bt,
+                       bufs->groupA, p.Lh, ws + w.ein, hp,
                        ws + w.msum);
     MixIO io;
     for (int k = 0; k < 4; ++k) {
@@ -1641,7 +1685,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     io.dq = ws + w.dq;
     io.d2 = ws + w.d2;
     io.part = ws + w.part;
-    hipLaunchKernelGGL(mix_td_kernel, dim3((unsigned)c.I), dim3(64), 0, s, c, bt, io);
+    hipLaunchKernelGGL(s8 ? mix_td_kernel<1> : mix_td_kernel<0>, dim3((unsigned)c.I), dim3(64), 0, s, c, bt, io);
     HypBwd hb;
     for (int k = 0; k < 4; ++k) {
         hb.Pon[k] = ws + w.ph_on[k];
@@ -1657,7 +1701,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hb.dqkvm[k] = ws + w.dqkvm[k];
         hb.dfc1m[k] = ws + w.dfc1m[k];
     }
-    hipLaunchKernelGGL(hyper_bwd_kernel, dim3((unsigned)c.I, 4), dim3(64), 0, s, c, bt, hb, ws + w.msum);
+    hipLaunchKernelGGL(s8 ? hyper_bwd_kernel<1> : hyper_bwd_kernel<0>, dim3((unsigned)c.I, 4), dim3(64), 0, s, c, bt, hb,
+                       ws + w.msum);
     // ---- agent backward ----
     if (rec16)
         hipLaunchKernelGGL(rec_bwd_kernel, dim3((unsigned)nt_on), dim3(256), 0, s, c, bt, La, ws + w.pa_on, ws + w.hs_on,
@@ -1668,7 +1713,8 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
                            ws + w.msum);
     EntBwd eb{ws + w.a_wihT, ws + w.a_w2T, ws + w.a_woutT, ws + w.a_winT, ws + w.h_wspT[4], ws + w.x1, ws + w.qkv, ws + w.P, ws + w.x3,
               ws + w.dgi, ws + w.dfc2, ws + w.dout, ws + w.dqkv, ws + w.dfc1};
-    hipLaunchKernelGGL(ent_bwd_kernel, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt, eb, ws + w.msum);
+    hipLaunchKernelGGL(s8 ? ent_bwd_kernel<1> : ent_bwd_kernel<0>, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt,
+                       eb, ws + w.msum);
     // ---- weight gradients, clip, RMSprop ----
     int64_t slab_floats, n_red;
     int n_tasks;

@@ -58,7 +58,12 @@ def _pre(d, prefix):
     return {k[len(prefix):]: d[k] for k in d.files if k.startswith(prefix)}
 
 
-def test_refil_learner_two_calls_match_golden(device, golden):
+@pytest.mark.parametrize("inst", ["static", "generic"])
+def test_refil_learner_two_calls_match_golden(device, golden, inst, monkeypatch):
+    """The refil_8 shape runs the static instantiations of the per-item kernels; MLG_REFIL_GENERIC=1 the generic
+    ones: both against the reference's two train calls."""
+    if inst == "generic":
+        monkeypatch.setenv("MLG_REFIL_GENERIC", "1")
     d = golden("refil_learner.npz")
     a = refil_args(device="cuda")
     eb = _batch_from(_pre(d, "b."), device)
