@@ -208,8 +208,11 @@ def kernel_names(mode, N, A, kc1=0):
         "rollout_v2_kernel<64, true, 3, 6>" if (N, A) == (3, 11) else "rollout_v2_kernel<64, true>")
     sp7 = "rollout_sp7_kernel<10, 10>" if (N, A) == (5, 15) else (
         "rollout_sp7_kernel<6, 6>" if (N, A) == (3, 11) else "rollout_sp7_kernel<0, 0>")
+    # the four-env kernel for the entity width of the env variant; its refil_8 shape (8 agents, 21 actions) runs the
+    # static 16-unit instantiation unless MLG_REFIL_GENERIC is set
+    st16 = (N, A) == (8, 21) and not os.environ.get("MLG_REFIL_GENERIC")
     refil = (f"refil_rollout_kernel<{kc1}>" if (os.environ.get("MLG_REFIL_ROLLOUT") == "v1" or kc1 != 2)
-             else "refil_rollout4_kernel<2>")  # the four-env kernel for the entity width of the env variant
+             else f"refil_rollout4_kernel<2, {16 if st16 else 0}>")
     return {"ai": v7, "league": sp7, "refil": refil}[mode]
 
 
