@@ -61,7 +61,7 @@ class DistributedLeague:
         d.record_result(home, away, result, n)
 
     def record_match(self, home: int, away: int):
-        self._delta[home, away, PayoffEntry.MATCHES] += 1
+        self._delta[home, away, PayoffEntry.MATCHES].add_(1)  # one in-place kernel on a view
 
     def record_runs(self, home: int, away: int, won: torch.Tensor, draw: torch.Tensor):
         """Episode results of one batched run, on the device (no host sync): _extract_result +
@@ -145,10 +145,15 @@ class DistributedLeague:
         bad = not 0 <= steps < 2 ** 48
         s = min(max(steps, 0), 2 ** 48 - 1)
         meta_in = [float(s & 0xFFFFFF), float(s >> 24), 1.0 if checkpoint else 0.0, 1.0 if bad else 0.0]
-        msg = torch.cat([flat.detach().reshape(-1).to(torch.float32), torch.tensor(meta_in, device=flat.device)])
-        gathered = self.share_params(msg)
-        allm = torch.stack(gathered)[: self.n]
-        meta = allm[:, n_p:].detach().cpu().numpy().astype(np.int64)
+        if self._dist:
+            msg = torch.cat([flat.detach().reshape(-1).to(torch.float32), torch.tensor(meta_in, device=flat.device)])
+            gathered = self.share_params(msg)
+            allm = torch.stack(gathered)[: self.n]
+            params = allm[:, :n_p]
+            meta = allm[:, n_p:].detach().cpu().numpy().astype(np.int64)
+        else:  # one player, nothing to gather: the message stays on the host, the parameters on the device
+            params = flat.detach().reshape(1, -1)
+            meta = np.asarray([meta_in], dtype=np.float32).astype(np.int64)
         if meta[:, 3].any():
             raise ValueError(f"trained_steps outside the exchange's exact range [0, 2^48) on player(s) "
                              f"{np.nonzero(meta[:, 3])[0].tolist()} (this player: {steps})")
@@ -156,7 +161,7 @@ class DistributedLeague:
             self.current = torch.empty(self.n, n_p, dtype=torch.float32, device=flat.device)
             cap = self.capacity - self.n
             self.historical = torch.empty(max(cap, 0), n_p, dtype=torch.float32, device=flat.device)
-        self.current.copy_(allm[:, :n_p])
+        self.current.copy_(params)
         new = []
         for pid in range(self.n):
             if meta[pid, 2] > 0:

@@ -20,7 +20,7 @@ from typing import List, Optional, Tuple
 
 import numpy as np
 
-from .payoff import PFSPSampling
+from .payoff import PayoffEntry, PFSPSampling
 
 
 def remove_monotonic_suffix(win_rates, players):
@@ -50,6 +50,14 @@ class LeagueView:
     def win_rates(self, pid, opponents) -> np.ndarray:
         if len(opponents) == 0:
             return np.zeros(0)
+        t = self.payoff.tensor
+        if t.device.type == "cpu":  # the league iteration's host copy: the same float32 arithmetic in numpy
+            row = t.detach().numpy()[pid, list(opponents)]
+            games = row[:, PayoffEntry.GAMES]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                wr = (row[:, PayoffEntry.WIN] + np.float32(0.5) * row[:, PayoffEntry.DRAW]) / games
+            wr[games == 0.0] = 0.5
+            return wr
         return self.payoff.win_rates(pid, list(opponents)).detach().cpu().numpy()
 
     def of_type(self, cls) -> list:

@@ -12,28 +12,34 @@ import torch
 
 from ..controllers import REGISTRY as mac_REGISTRY
 from ..learners.q_learner import FlatParams
-from ..utils.flat import flat_view
+from ..utils.flat import module_flat_view
 from ..steppers import SELF_REGISTRY as self_steppers_REGISTRY
 from .ma_experiment import MultiAgentExperiment
 
 
 def agent_vector(mac) -> torch.Tensor:
-    """The MAC's agent parameters as one flat vector (named_parameters order)."""
+    """The MAC's agent parameters as one flat vector (named_parameters order): a view of them when they are back
+    to back in one buffer (a learner's FlatParams -- callers copy what they keep), else a concatenated copy."""
+    flat = module_flat_view(mac.agent)
+    if flat is not None:
+        return flat.detach()
     return torch.nn.utils.parameters_to_vector(mac.agent.parameters()).detach()
 
 
 @torch.no_grad()
 def load_agent_vector(mac, vec: torch.Tensor):
     """In-place copy (keeps a learner's flat-parameter views valid; bumps versions -> weights repacked)."""
+    flat = module_flat_view(mac.agent)
+    if flat is not None:  # parameters back to back in one buffer: one copy
+        if flat.numel() != vec.numel():
+            raise ValueError(f"parameter vector of {vec.numel()} floats for an agent of {flat.numel()}")
+        flat.copy_(vec.reshape(-1))
+        mac.agent.mark_dirty()  # writes through the flat view bump no parameter version: repack explicitly
+        return
     params = list(mac.agent.parameters())
     n = sum(p.numel() for p in params)
     if n != vec.numel():
         raise ValueError(f"parameter vector of {vec.numel()} floats for an agent of {n}")
-    flat = flat_view(params)
-    if flat is not None:  # parameters back to back in one buffer: one copy
-        flat.copy_(vec.reshape(-1))
-        mac.agent.mark_dirty()  # writes through the flat view bump no parameter version: repack explicitly
-        return
     off = 0
     for p in params:
         k = p.numel()

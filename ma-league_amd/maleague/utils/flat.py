@@ -19,3 +19,16 @@ def flat_view(params) -> torch.Tensor | None:
         off += 4 * p.numel()
     n = sum(p.numel() for p in params)
     return p0.detach().new_empty(0).set_(p0.untyped_storage(), p0.storage_offset(), (n,), (1,))
+
+
+def module_flat_view(module) -> torch.Tensor | None:
+    """flat_view of ``module.parameters()``, cached on the module by the parameters' addresses (the cached view
+    keeps its storage alive, so equal addresses mean the same layout in the same buffer)."""
+    params = list(module.parameters())
+    key = tuple(p.data_ptr() for p in params)
+    hit = getattr(module, "_mlg_flat_view", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    flat = flat_view(params)
+    object.__setattr__(module, "_mlg_flat_view", (key, flat))
+    return flat

@@ -44,5 +44,8 @@ for _ in range(int(os.environ.get("SYNCS", "10"))):
     pr.disable()
     ts.append(time.perf_counter() - t0)
 print("sync ms (cProfile):", [round(t * 1e3, 3) for t in ts], flush=True)
-pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
-pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+st = pstats.Stats(pr).stats
+n = len(ts)
+print("us per sync: cumulative, own, calls, function")
+for (f, line, name), (cc, nc, tt, ct, _) in sorted(st.items(), key=lambda kv: -kv[1][3])[:45]:
+    print(f"{ct / n * 1e6:9.1f} {tt / n * 1e6:9.1f} {nc / n:6.1f}  {os.path.basename(f)}:{line}({name})")
