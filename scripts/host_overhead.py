@@ -23,14 +23,21 @@ exp._init_stepper()
 st = exp.stepper
 st.t_env = 10 ** 6
 B = st.batch_size
+ep = [0]
+
+
+def it():  # one iteration of MultiAgentExperiment.start's loop, as bench.py runs it
+    ep[0] = exp._iteration(ep[0])
+
+
 for i in range(5):
-    exp._train_episode(i * B)
+    it()
 torch.cuda.synchronize()
 host = []
 t0 = time.perf_counter()
 for i in range(20):
     h0 = time.perf_counter()
-    exp._train_episode((5 + i) * B)
+    it()
     host.append(time.perf_counter() - h0)
 t_host = time.perf_counter() - t0
 torch.cuda.synchronize()
@@ -45,7 +52,7 @@ if os.environ.get("PROFILE"):
     pr = cProfile.Profile()
     pr.enable()
     for i in range(20):
-        exp._train_episode((25 + i) * B)
+        it()
     pr.disable()
     torch.cuda.synchronize()
     pstats.Stats(pr).sort_stats("tottime").print_stats(18)
