@@ -347,3 +347,50 @@ def test_checkpoint_clock_reset_when_stored():
         inst.sync()
         inst.sync()
         assert calls == expect
+
+
+def test_host_win_rates_equal_torch_form():
+    """Matchmaking on the host payoff copy computes win rates in numpy: bit-equal to PayoffWrapper.win_rates
+    (payoff_entry.py win rate, games == 0 -> 0.5) on random tables with empty entries."""
+    from maleague.league.payoff import PayoffWrapper
+    from maleague.league.roles import LeagueView
+    g = torch.Generator().manual_seed(0)
+    for _ in range(100):
+        t = torch.randint(0, 50, (6, 6, 5), generator=g).float() * torch.rand(6, 6, 5, generator=g).round()
+        pw = PayoffWrapper(t)
+        for pid, opp in ((1, [0, 2, 3, 5]), (4, [4]), (0, list(range(6)))):
+            a = LeagueView(pw, []).win_rates(pid, opp)
+            b = pw.win_rates(pid, opp).numpy()
+            assert a.dtype == b.dtype and np.array_equal(a, b)
+
+
+def test_agent_vector_flat_view_and_reflatten():
+    """agent_vector returns the agent's flat parameter view when the parameters are back to back (a learner's
+    FlatParams), equal to parameters_to_vector; the cached view follows a re-flatten into a new buffer."""
+    import types
+    from maleague.learners.q_learner import FlatParams
+    from maleague.runs.sp_ma_experiment import agent_vector, load_agent_vector
+
+    class Agent(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a, self.b = torch.nn.Linear(3, 4), torch.nn.Linear(4, 2)
+            self.dirty = 0
+
+        def mark_dirty(self):
+            self.dirty += 1
+
+    mac = types.SimpleNamespace(agent=Agent())
+    ref = torch.nn.utils.parameters_to_vector(mac.agent.parameters()).detach().clone()
+    assert torch.equal(agent_vector(mac), ref)  # separate parameters: a concatenated copy
+    fp = FlatParams(mac.agent.parameters(), "cpu")
+    v = agent_vector(mac)
+    assert torch.equal(v, ref) and v.data_ptr() == fp.flat.data_ptr()
+    load_agent_vector(mac, ref + 1)
+    assert torch.equal(fp.flat, ref + 1) and mac.agent.dirty == 1
+    fp2 = FlatParams(mac.agent.parameters(), "cpu")  # parameters moved to a new buffer
+    load_agent_vector(mac, ref + 2)
+    assert torch.equal(fp2.flat, ref + 2) and torch.equal(fp.flat, ref + 1)
+    assert agent_vector(mac).data_ptr() == fp2.flat.data_ptr()
+    with pytest.raises(ValueError):
+        load_agent_vector(mac, torch.zeros(3))
