@@ -17,7 +17,7 @@ class A:
     plan, envs, episode_limit = None, 4096, 100
 
 
-args, _ = bench.make_args("ai", A, 0, 0)
+args, _ = bench.make_args(os.environ.get("MODE", "ai"), A, 0, 0)  # MODE=refil: config 5
 exp = MultiAgentExperiment(args, MainLogger(log_interval=10 ** 12))
 exp._init_stepper()
 st = exp.stepper
