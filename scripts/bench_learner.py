@@ -49,4 +49,5 @@ for r in range(REPS):
 torch.cuda.synchronize()
 ms = [a.elapsed_time(b) for a, b in ev]
 print(json.dumps({"train_ms": sum(ms) / len(ms), "min_ms": min(ms), "loss": lrn.last_stats["loss"],
-                  "grad_norm": lrn.last_stats["grad_norm"], "T": samples[0].max_seq_length}))
+                  "grad_norm": lrn.last_stats["grad_norm"], "T": samples[0].max_seq_length,
+                  "t_filled_mean": float(np.mean([int(s_.max_t_filled()) for s_ in samples[:10]]))}))

@@ -56,3 +56,7 @@ if os.environ.get("PROFILE"):
     pr.disable()
     torch.cuda.synchronize()
     pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+
+buf = exp.home_buffer
+tf = [int(buf.sample(args.batch_size, view=True).max_t_filled()) for _ in range(10)]
+print(f"sampled batches' filled length (max over the batch's episodes): mean {sum(tf) / len(tf):.1f}, {tf}")
