@@ -40,11 +40,13 @@ import torch  # noqa: E402
 
 FP32_MFMA_PEAK = 157.3e12  # MI355X dense fp32 (MFMA == VALU rate), MI355X_MICROARCH.md chip table
 HBM_PEAK = 8.0e12
+CLOCK_HZ = 2.4e9  # MI355X max engine clock (MI355X_MICROARCH.md): the latency floor is a lower bound
 # HIP-event pair around every k-th rollout launch of the timed region (--timing-every). Every launch (default): the
 # pair costs ~8-10 us of queue time per iteration (0.7 % of ms_per_step at config 2, a device-scope-release event
 # pair the same), but a sample of every 4th launch biases the kernel average (launch times vary 0.68-1.03 ms with
 # the iteration's longest episode): profiles/r04/s11_timing_ab/
 TIMING_EVERY = 1
+LEAGUE_CKPT_STEPS = 8000
 METRIC = "env-steps/sec (rollout+learn), 5v5 QMIX, 4096 envs, at 1/2/4/8 MI355X"
 COUNTERS_JSON = os.path.join(ROOT, "profiles", "counters.json")
 
@@ -109,6 +111,8 @@ def timed_loop(ctx: Ctx, iteration, stepper, steps: int, warmup: int) -> dict:
     stepper.timing_every = TIMING_EVERY if steps >= 2 * TIMING_EVERY else 1  # short runs: every launch
     stepper._launches = 0  # sampled launches counted from the start of the timed region
     t0_env = stepper.t_env
+    run0 = stepper._run_id  # runs launched from here on are the timed ones
+    stepper.t_history = []
     rows0 = int(stepper.agent_rows.item())
     ctx.sync()
     t0 = time.perf_counter()
@@ -118,6 +122,8 @@ def timed_loop(ctx: Ctx, iteration, stepper, steps: int, warmup: int) -> dict:
     ctx.barrier()
     elapsed_local = time.perf_counter() - t0
     local_steps = stepper.t_env - t0_env
+    longest = [t for rid, t in stepper.t_history if rid > run0]
+    stepper.t_history = None
     rows = (int(stepper.agent_rows.item()) - rows0) / steps
     ev_ms = [st.elapsed_time(en) for st, en in stepper.timing] if timing_ok else []
     stepper.timing = None
@@ -126,7 +132,8 @@ def timed_loop(ctx: Ctx, iteration, stepper, steps: int, warmup: int) -> dict:
     total = int(ctx.reduce(float(local_steps), "sum"))
     return {"elapsed": elapsed, "env_steps": total, "local_env_steps": local_steps, "per_rank": per_rank,
             "value": total / elapsed, "ms_per_step": elapsed / steps * 1e3, "rows_per_launch": rows,
-            "avg_kernel_ms": (sum(ev_ms) / len(ev_ms)) if ev_ms else None}
+            "avg_kernel_ms": (sum(ev_ms) / len(ev_ms)) if ev_ms else None,
+            "longest_episode_mean": (sum(longest) / len(longest)) if longest else None}
 
 
 def league_iteration(inst, match_len: int, exchange_s: list, ctx=None):
@@ -149,7 +156,9 @@ def league_iteration(inst, match_len: int, exchange_s: list, ctx=None):
 
 
 def run_league_leg(ctx: Ctx, inst, steps: int, warmup: int, match_len: int) -> dict:
-    """The league leg of the bench (also driven by tests/test_bench_league.py over gloo on CPU)."""
+    """The league leg of the bench (also driven by tests/test_bench_league.py over gloo on CPU). The warm-up runs at
+    least match_len + 1 iterations, so it holds a league iteration after some training (the first snapshot)."""
+    warmup = max(warmup, match_len + 1)
     ex_warm, ex = [], []
     warm_it = league_iteration(inst, match_len, ex_warm, ctx)
     timed_it = league_iteration(inst, match_len, ex, ctx)
@@ -162,11 +171,14 @@ def run_league_leg(ctx: Ctx, inst, steps: int, warmup: int, match_len: int) -> d
     r = timed_loop(ctx, it, inst.experiment.stepper, steps, warmup)
     ex_ms = [e * 1e3 for e in ex]
     lg = inst.league
-    r.update({"league_iterations": len(ex), "exchange_ms_mean": sum(ex_ms) / max(1, len(ex_ms)),
+    r.update({"league_iterations": len(ex), "league_warmup_iterations": warmup, "exchange_ms_mean": sum(ex_ms) / max(1, len(ex_ms)),
               "exchange_ms_max": max(ex_ms) if ex_ms else None,
               "exchange_frac": sum(ex) / r["elapsed"] if r["elapsed"] > 0 else None,
               "collective_backend": lg.backend, "world_size": ctx.world,
               "opponents_rank0": [h[1] for h in inst.history], "historical_snapshots": len(lg.historical_meta),
+              "snapshots_taken": len(lg.historical_meta) + lg.evictions,
+              "historical_matches_rank0": sum(1 for h in inst.history if h[2]),
+              "historical_matches_timed_rank0": sum(1 for h in inst.history[-len(ex):] if h[2]) if ex else 0,
               "evictions": lg.evictions,
               "payoff_games": float(lg.payoff.tensor[..., 0].sum().item())})
     return r
@@ -180,7 +192,11 @@ def make_args(mode, a, rank, local_rank):
                  f"env_args.match_build_plan={plan}", f"env_args.episode_limit={a.episode_limit}",
                  f"seed={rank}", "learner_log_interval=1000000000", "log_interval=1000000000",
                  "runner_log_interval=1000000000", "test_interval=1000000000000", "t_max=1000000000000",
-                 "show_exp_parameters=False", "league_checkpoint_min_steps=20000", "league_checkpoint_max_steps=40000"]
+                 "show_exp_parameters=False",
+                 # a snapshot after every ~3 train calls (a 32-episode batch trains on <= 3.2 k env steps): the first
+                 # fires in the league leg's warm-up, the timed league iterations then gather snapshots and play
+                 # historical opponents (the reference's 2e9 / 4e9 would never fire in a bench)
+                 f"league_checkpoint_min_steps={LEAGUE_CKPT_STEPS}", f"league_checkpoint_max_steps={LEAGUE_CKPT_STEPS}"]
     if mode == "refil":
         cfg = build_config("refil", "ma_entity", overrides=overrides, device_index=local_rank)
     else:
@@ -191,6 +207,17 @@ def make_args(mode, a, rank, local_rank):
     return to_args(cfg), plan
 
 
+def league_setup(world: int, args):
+    """(mode, roles) of the league leg at ``world`` ranks. Every N runs AlphaStar roles, so every player takes
+    historical snapshots (main_player.py:120-132) and plays them (PFSP over historical, :33-35): N = 1 one main
+    player against its own snapshots, N = 2 (config 3) two main players (self-play + PFSP over the pool), N >= 4
+    (config 4) main players + main exploiters (league_roles_for)."""
+    from maleague.league import league_roles_for
+    if world >= 4:
+        return "rolebased", league_roles_for(world, args)
+    return "rolebased", ["main"] * world
+
+
 def league_workload(world, plan, a, roles=None):
     if world >= 4:
         n_main = roles.count("main")
@@ -198,7 +225,8 @@ def league_workload(world, plan, a, roles=None):
                 "BASELINE config 4 (PFSP league: main players + main exploiters, historical snapshots, RCCL)")
     if world > 1:
         return (f"selfplay_pfsp_{world}learners_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
-                f"BASELINE config 3 (self-play QMIX, {world} PFSP learners, opponent swap via RCCL)")
+                f"BASELINE config 3 (self-play QMIX, {world} learners as main players: self-play + PFSP over "
+                f"historical snapshots, opponent swap via RCCL)")
     return (f"league_player_vs_own_snapshots_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
             "1-GPU league player (self-play vs its own snapshots): the per-GPU league cost, scaling denominator")
 
@@ -252,6 +280,16 @@ def roofline(mode, stepper, r, steps, B):
            "hbm_frac": traffic / avg_s / HBM_PEAK if traffic else None,
            "mfma_busy": cnt.get("mfma_busy"), "wave_parked": cnt.get("wait_any_frac"),
            "counters_commit": cnt.get("commit")}
+    # the bound the rollout actually has: a launch lasts at least as long as its longest episode,
+    # whose steps are serial (agent step of t feeds the env step of t feeds the agent step of t + 1); each costs at
+    # least the measured cycles of a step with that one env running (phase stamps, diagnostic build). The floor:
+    # mean over the timed launches of (longest episode + 1 final agent step) x those cycles / the max clock.
+    step_cyc = cnt.get("one_env_step_cycles")
+    if step_cyc and r.get("longest_episode_mean"):
+        floor_ms = (r["longest_episode_mean"] + 1) * step_cyc / CLOCK_HZ * 1e3
+        out.update({"latency_floor_ms": floor_ms, "latency_floor_frac": floor_ms / r["avg_kernel_ms"],
+                    "one_env_step_cycles": step_cyc, "one_env_step_source": cnt.get("one_env_step_source"),
+                    "longest_episode_mean": r["longest_episode_mean"], "latency_floor_clock_ghz": CLOCK_HZ / 1e9})
     if mode == "ai":
         issued = fl / N * r["rows_per_launch"] / avg_s
         out.update({"issued_tflops": issued / 1e12, "issued_frac": issued / FP32_MFMA_PEAK,
@@ -281,6 +319,7 @@ def cpu_entry(c, leg_names):
     main_leg = legs[0]
     return {"value": main_leg["value"], "unit": "env-steps/s", "cores": main_leg["cores"], "kind": "port",
             "sample": main_leg["sample"], "cpu_model": c.get("cpu_model"), "host_cpus": c.get("host_cpus"),
+            "per_gpu_core_share": c.get("per_gpu_core_share"), "usable_cpus": c.get("usable_cpus"),
             "legs": legs}
 
 
@@ -303,7 +342,17 @@ def launch_ranks(a, argv, out_fd) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL peer buffers)
     env.setdefault("OMP_NUM_THREADS", "1")
-    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    # a rank hung in RCCL init or a collective must not hang the bench: bound the child by the run's own size
+    limit = 600 + 3 * (a.steps + a.warmup) + 8 * 3 * a.cpu_seconds
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, start_new_session=True)
+    try:
+        stdout, _ = proc.communicate(timeout=limit)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, 9)  # the launcher's own process group: it and its ranks
+        proc.communicate()
+        sys.stderr.write(f"bench: {a.gpus}-rank launch exceeded {limit:.0f} s, killed\n")
+        return 124
+    p = subprocess.CompletedProcess(cmd, proc.returncode, stdout)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     if p.returncode != 0 or len(lines) != 1:
         sys.stderr.write(f"bench: {a.gpus}-rank launch failed (exit {p.returncode}, {len(lines)} result lines)\n"
@@ -321,10 +370,11 @@ def leg_summary(L, a):
            "rollout_kernel": L["roofline"]["kernel"], "avg_kernel_ms": L["avg_kernel_ms"],
            "roofline_frac": L["roofline"]["frac"], "roofline": L["roofline"]}
     if "league_iterations" in L:
-        out.update({"match_len": a.match_len,
+        out.update({"match_len": a.match_len, "league_warmup_iterations": L.get("league_warmup_iterations"),
                     **{k: L[k] for k in ("league_iterations", "exchange_ms_mean", "exchange_ms_max", "exchange_frac",
                                          "collective_backend", "world_size", "opponents_rank0",
-                                         "historical_snapshots", "evictions", "payoff_games")},
+                                         "historical_snapshots", "snapshots_taken", "historical_matches_rank0",
+                                         "historical_matches_timed_rank0", "evictions", "payoff_games")},
                     "note": "league scaling = league.value at N / league.value at N = 1 (same leg, same per-GPU "
                             "workload: weak scaling)"})
     return out
@@ -332,7 +382,8 @@ def leg_summary(L, a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default 1, or WORLD_SIZE under an outer torch.distributed.run")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="auto", choices=["auto", "ai", "league", "refil"])
@@ -360,6 +411,8 @@ def main():
     os.dup2(2, 1)
 
     launched = "WORLD_SIZE" in os.environ  # torch.distributed.run (any nproc) -> a process group, RCCL
+    if a.gpus is None:  # a plain `torchrun --nproc-per-node N bench.py` takes N from the launcher
+        a.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus > 1 and not launched:
         sys.exit(launch_ranks(a, argv, out_fd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -427,13 +480,10 @@ def main():
                 cfg_name = "BASELINE config 2 (QMIX 5v5, 4096 envs per GPU, one learner per GPU vs scripted AI)"
             parallelism = f"replicas{world}"
         else:
-            from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
+            from maleague.league import DistributedLeague, LeagueInstance
             lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=4 * world)
-            roles = league_roles_for(world, args) if world >= 4 else None
-            if roles:
-                inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="rolebased", role=roles, seed=0)
-            else:
-                inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="matchmaking", seed=0)
+            lmode, roles = league_setup(world, args)
+            inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode=lmode, role=roles, seed=0)
             workload, cfg_name = league_workload(world, plan, a, roles)
             exp = inst.experiment
             parallelism = f"league{world}_{lg.backend}"
@@ -482,7 +532,9 @@ def main():
         if head == "league":
             out["league"] = {k: h[k] for k in ("league_iterations", "exchange_ms_mean", "exchange_ms_max",
                                                "exchange_frac", "collective_backend", "world_size",
-                                               "opponents_rank0", "historical_snapshots", "evictions")}
+                                               "opponents_rank0", "historical_snapshots", "snapshots_taken",
+                                               "historical_matches_rank0", "historical_matches_timed_rank0",
+                                               "evictions")}
         if "league" in results and head != "league":
             out["league"] = leg_summary(results["league"], a)
         if "refil" in results and head != "refil":

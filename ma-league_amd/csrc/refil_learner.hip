@@ -1765,7 +1765,8 @@ __global__ void refil_groups_kernel(int B, int NE, uint64_t seed, uint32_t draw,
 
 extern "C" int mlg_refil_draw_groups(int32_t B, int32_t NE, uint64_t seed, uint32_t draw, uint8_t* groupA,
                                      void* stream) {
-    MLG_REQUIRE(groupA && B >= 1 && NE >= 1 && NE <= 4096, "refil_draw_groups: B=%d NE=%d", B, NE);
+    // the counter keeps 16 bits of b and 12 of j + 1 (mlg_ctr): B <= 65536 and NE < 4096 keep every draw distinct
+    MLG_REQUIRE(groupA && B >= 1 && B <= 65536 && NE >= 1 && NE < 4096, "refil_draw_groups: B=%d NE=%d", B, NE);
     hipLaunchKernelGGL(refil_groups_kernel, dim3((unsigned)((B * NE + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        B, NE, seed, draw, groupA);
     return mlg::check_launch("refil_draw_groups");

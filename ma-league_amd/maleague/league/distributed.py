@@ -34,8 +34,14 @@ log = logging.getLogger(__name__)
 
 class DistributedLeague:
     def __init__(self, n_players: int, device, reference_compat: bool = False, seed: int = 0,
-                 max_historical: int = 0):
+                 max_historical: int = 0, player_id: int = None):
+        """``player_id`` (no process group only): this process plays that pid of an ``n_players`` league whose other
+        players' parameters are fixed replicas installed with set_player_params (e.g. a main exploiter trained on one
+        GPU against a main player loaded from its checkpoint)."""
         self._dist = dist.is_available() and dist.is_initialized()
+        if player_id is not None and (self._dist or not 0 <= player_id < n_players):
+            raise ValueError(f"player_id={player_id}: only without a process group, and < n_players={n_players}")
+        self._pid = player_id
         self.rank = dist.get_rank() if self._dist else 0
         self.world = dist.get_world_size() if self._dist else 1
         self.n = n_players
@@ -52,7 +58,20 @@ class DistributedLeague:
         self.payoff_host = None  # host copy of the payoff taken by host_snapshot() (what matchmaking reads)
 
     def player(self) -> int:
-        return self.rank % self.n
+        return self.rank % self.n if self._pid is None else self._pid
+
+    def set_player_params(self, pid: int, flat: torch.Tensor):
+        """Install player ``pid``'s current parameters (a fixed replica; league without a process group)."""
+        if self._dist:
+            raise RuntimeError("set_player_params: the process group's all_gather owns the pool")
+        flat = flat.detach().reshape(-1).to(torch.float32)
+        self._alloc_pool(flat.numel(), flat.device)
+        self.current[pid].copy_(flat)
+
+    def _alloc_pool(self, n_p: int, device):
+        if self.current is None:
+            self.current = torch.zeros(self.n, n_p, dtype=torch.float32, device=device)
+            self.historical = torch.empty(max(self.capacity - self.n, 0), n_p, dtype=torch.float32, device=device)
 
     # ---- payoff ------------------------------------------------------------------------------------------
     def record(self, home: int, away: int, result: PayoffEntry, n: int = 1):
@@ -70,6 +89,12 @@ class DistributedLeague:
         mlg_league_record_runs launch; host tensors (CPU rehearsals / tests): the same reduction in torch."""
         if self._delta.is_cuda:
             from .. import _native
+            B = int(won.shape[0])
+            # the kernel reads int32 rows: [B, 2] won (policy team first) and [B] draw
+            if won.dtype != torch.int32 or draw.dtype != torch.int32 or tuple(won.shape) != (B, 2) or \
+                    tuple(draw.shape) != (B,) or not won.is_cuda or not draw.is_cuda:
+                raise ValueError(f"record_runs: won must be int32 [B, 2] and draw int32 [B] on the device, got "
+                                 f"{won.dtype} {tuple(won.shape)} / {draw.dtype} {tuple(draw.shape)}")
             entry = self._delta[home, away]
             _native.call("mlg_league_record_runs", _native.ptr(won.contiguous()), _native.ptr(draw.contiguous()),
                          int(won.shape[0]), entry.data_ptr(), int(not self.payoff.reference_compat),
@@ -101,6 +126,7 @@ class DistributedLeague:
                 dist.all_reduce(self._delta, op=dist.ReduceOp.SUM)
         self.payoff.tensor.add_(self._delta)
         self._delta.zero_()
+        self.payoff_host = None  # stale now: host_snapshot() is the only thing that installs a host copy
         return self.payoff.tensor
 
     def host_snapshot(self, counter: torch.Tensor = None):
@@ -151,17 +177,19 @@ class DistributedLeague:
             allm = torch.stack(gathered)[: self.n]
             params = allm[:, :n_p]
             meta = allm[:, n_p:].detach().cpu().numpy().astype(np.int64)
-        else:  # one player, nothing to gather: the message stays on the host, the parameters on the device
-            params = flat.detach().reshape(1, -1)
-            meta = np.asarray([meta_in], dtype=np.float32).astype(np.int64)
+        else:  # nothing to gather: the message stays on the host, the parameters on the device; the other players
+            # (player_id leagues) keep their installed replicas and never ask for checkpoints
+            meta = np.zeros((self.n, 4), dtype=np.int64)
+            meta[self.player()] = np.asarray(meta_in, dtype=np.float32).astype(np.int64)
+            params = None
         if meta[:, 3].any():
             raise ValueError(f"trained_steps outside the exchange's exact range [0, 2^48) on player(s) "
                              f"{np.nonzero(meta[:, 3])[0].tolist()} (this player: {steps})")
-        if self.current is None:
-            self.current = torch.empty(self.n, n_p, dtype=torch.float32, device=flat.device)
-            cap = self.capacity - self.n
-            self.historical = torch.empty(max(cap, 0), n_p, dtype=torch.float32, device=flat.device)
-        self.current.copy_(params)
+        self._alloc_pool(n_p, flat.device)
+        if params is not None:
+            self.current.copy_(params)
+        else:
+            self.current[self.player()].copy_(flat.detach().reshape(-1))
         new = []
         for pid in range(self.n):
             if meta[pid, 2] > 0:

@@ -116,6 +116,7 @@ class ParallelStepper(EnvStepper):
         self.away_mac = None  # self-play only (SelfPlayParallelStepper)
         self.timing = None  # list -> (start, end) HIP events around rollout launches (bench.py)
         self.timing_every = 1  # time every k-th launch only (an event pair costs a few us of GPU queue time)
+        self.t_history = None  # list -> (run_id, longest episode) of every resolved run (bench.py latency floor)
         self._launches = 0
         self._ring = None   # ReplayBuffer written in place (zero-copy insert), see attach_replay()
 
@@ -240,6 +241,8 @@ class ParallelStepper(EnvStepper):
         host = buf.numpy().copy()
         ep_len = host[0:B]
         self._t = int(ep_len.max())
+        if self.t_history is not None:
+            self.t_history.append((run_id, self._t))
         if not test_mode:
             self.env_steps_this_run = int(ep_len.sum())
             self._t_env += self.env_steps_this_run

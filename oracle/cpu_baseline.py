@@ -242,7 +242,7 @@ def run_process_model(seconds=15.0, B=None, episode_limit=100, eps=0.05, threads
     """ParallelStepper.run in the reference's process model: B worker processes (one env each); per step the
     parent sends ("step", actions) to every running env, then receives every result (parallel_stepper.py:143-191),
     with the stepper bookkeeping of stepper_ref.run and one QLearner.train per run."""
-    B = B or min(16, os.cpu_count() or 1)
+    B = B or core_share()[0]
     threads = threads or B
     p = PLAN_MEDIUM_1H_4T
     U, N = 10, 5
@@ -350,6 +350,26 @@ def _cpu_model():
     return platform.processor() or None
 
 
+def _cgroup_cpus():
+    """CPUs this process may use: the cgroup v2 quota (cpu.max) and the affinity mask, whichever is smaller."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def core_share():
+    """Threads / env-worker processes of the CPU legs: this GPU's share of the host (host CPUs / 8 GPUs per node;
+    VERDICT r4), capped by what the process may actually use (cgroup quota, affinity)."""
+    share = max(1, (os.cpu_count() or 8) // 8)
+    return min(share, _cgroup_cpus()), share
+
+
 def main(argv=None):
     import argparse
     ap = argparse.ArgumentParser()
@@ -358,14 +378,14 @@ def main(argv=None):
     ap.add_argument("--episode-limit", type=int, default=100)
     ap.add_argument("--legs", default="vector,process")
     a = ap.parse_args(argv)
-    threads = min(16, os.cpu_count() or 1)
+    threads, share = core_share()
     legs = []
     for leg in a.legs.split(","):
         if leg == "vector":
             r = run(seconds=a.seconds, B=64, episode_limit=a.episode_limit, threads=threads)
             what = "vectorised port: one process, oracle stepper + C env + PyTorch-CPU DRQN/QMIX learner"
         elif leg == "process":
-            r = run_process_model(seconds=a.seconds, episode_limit=a.episode_limit)
+            r = run_process_model(seconds=a.seconds, B=threads, episode_limit=a.episode_limit)
             what = (f"reference process model: {r['workers']} env-worker processes (one env each, pipe round trip "
                     f"per env per step) + PyTorch-CPU DRQN/QMIX learner in the parent")
         elif leg == "refil":
@@ -376,7 +396,8 @@ def main(argv=None):
         legs.append({"leg": leg, "value": r["value"], "cores": r["cores"], "B": r["B"],
                      "sample": f"{r['runs']} runs x {r['B']} envs (+1 train each), {r['env_steps']} env steps in "
                                f"{r['seconds']:.1f}s; {what}"})
-    out = {"legs": legs, "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
+    out = {"legs": legs, "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(), "per_gpu_core_share": share,
+           "usable_cpus": _cgroup_cpus()}
     print(json.dumps(out) if a.json else out)
 
 

@@ -33,6 +33,8 @@ class _Stepper:
         self.t_env = 0
         self.agent_rows = torch.zeros(1, dtype=torch.int64)
         self.timing = None
+        self.t_history = None
+        self._run_id = 0
 
 
 class _Experiment:
@@ -68,14 +70,14 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     from types import SimpleNamespace
-    from maleague.league import DistributedLeague, LeagueInstance, league_roles_for
+    from maleague.league import DistributedLeague, LeagueInstance
     args = SimpleNamespace(matchmaking="pfsp", league_checkpoint_min_steps=300, league_checkpoint_max_steps=600,
                            env_args={})
     lg = DistributedLeague(n_players=world, device="cpu", seed=0, max_historical=2)
-    roles = league_roles_for(world, args) if world >= 4 else None
-    inst = LeagueInstance(args, None, lg, mode="rolebased" if roles else "matchmaking", role=roles, seed=0,
-                          experiment=_Experiment(rank))
+    mode, roles = bench.league_setup(world, args)
+    inst = LeagueInstance(args, None, lg, mode=mode, role=roles, seed=0, experiment=_Experiment(rank))
     ctx = bench.Ctx(dist, torch.device("cpu"))
+    assert mode == "rolebased" and len(roles) == world
     r = bench.run_league_leg(ctx, inst, steps=12, warmup=3, match_len=2)
     out.put((rank, r, lg.payoff.tensor.numpy().tolist(), list(lg.historical_meta)))
     dist.destroy_process_group()
@@ -111,6 +113,9 @@ def _check(res, world):
         assert meta == res[0][3]
     # every played episode is in the replicated payoff once the last exchange has run
     assert r0["payoff_games"] > 0
+    # snapshots are taken and historical opponents played inside the timed league iterations
+    assert r0["snapshots_taken"] > 0 and r0["historical_snapshots"] > 0
+    assert any(r["historical_matches_timed_rank0"] > 0 for _, r, _, _ in res)
 
 
 def test_bench_league_leg_gloo_world2():

@@ -15,6 +15,9 @@ from helpers import assert_near_tie_divergence, np_batch, qmix_args, ref_envs_fo
 pytestmark = pytest.mark.gpu
 
 Q_TOL = 1e-4
+# the measured number of v7 episodes (of 100) that diverge from v2 at a near-tie argmax flip,
+# per plan (static and runtime shapes), pinned with a small margin (was a blanket B // 10)
+V7_MAX_DIVERGING = {"medium_1h_4t": 2, "medium": 2, "small": 2}  # measured 0 / 0 / 0 (both shapes, r05)
 
 
 def _mk_env(device, plan, B, episode_limit=60, seed=3, stochastic=True):
@@ -459,4 +462,5 @@ def test_rollout_v7_split_bf16_gru_matches_fp32(device, plan, generic, monkeypat
     assert worst <= 1e-5, worst
     # episodes that differ from v2's must diverge at a near-tie flip of an argmax, not anywhere
     n_diff = assert_near_tie_divergence([out["v2"][0]], [nb], [q], B)
-    assert n_diff <= B // 10, n_diff
+    print(f"v7 vs v2 [{plan}, generic={generic}]: {n_diff} of {B} episodes diverge (near-tie flips)")
+    assert n_diff <= V7_MAX_DIVERGING[plan], (plan, generic, n_diff)

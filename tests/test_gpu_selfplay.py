@@ -19,6 +19,9 @@ from helpers import assert_near_tie_divergence, np_batch, qmix_args, ref_envs_fo
 pytestmark = pytest.mark.gpu
 
 Q_TOL = 1e-4
+# the measured number of sp7 episodes (of 100) that diverge from sp2 at a near-tie argmax flip,
+# per plan, pinned with a small margin (was a blanket B // 10)
+SP7_MAX_DIVERGING = {"medium_1h_4t": 2, "small": 2, "medium": 2}  # measured 0 / 0 / 0 (r05)
 
 
 def _sp_args(B, episode_limit, seed, plan="medium_1h_4t", **kw):
@@ -48,37 +51,45 @@ def _build(device, plan="medium_1h_4t", B=48, episode_limit=40, seed=5):
     return stepper, home, away, args
 
 
-def _check_sides(stepper, macs, args, batches, infos, episode, test_mode, eps):
+def _check_sides(stepper, macs, args, batches, infos, episode, test_mode, eps, envs=None):
+    """Teacher-forced env replay of both sides + oracle agent check. ``envs``: the env indices to check (all by
+    default; a spread subset at the 4096-env config-3 shape). Returns the counts (greedy picks checked, near ties,
+    epsilon draws)."""
     spec = stepper.spec
     B, N, A, T1 = stepper.batch_size, spec.n_agents // 2, spec.n_actions, stepper.episode_limit + 1
+    sub = np.arange(B) if envs is None else np.asarray(envs, dtype=np.int64)
     nbs = [np_batch(b) for b in batches]
     ep_len = stepper.last_run["ep_len"].numpy()
     assert (ep_len >= 1).all() and (ep_len <= stepper.episode_limit).all()
     # --- env side + bookkeeping, teacher forced through the oracle self-play stepper ---
-    refs = ref_envs_for(spec, B, seed=args.seed)
+    all_refs = ref_envs_for(spec, B, seed=args.seed)
+    refs = [all_refs[int(b)] for b in sub]
     for r in refs:
         r.episode = episode
-    pol = [lambda t, run, b, s=s: nbs[s]["actions"][run, t, :, 0] for s in range(2)]
-    out = stepper_ref.run_self_play(stepper_ref.RefVecEnv(refs), pol[0], pol[1], B, T1, N, A, 8 * spec.U,
+    pol = [lambda t, run, b, s=s: nbs[s]["actions"][sub[run], t, :, 0] for s in range(2)]
+    out = stepper_ref.run_self_play(stepper_ref.RefVecEnv(refs), pol[0], pol[1], len(sub), T1, N, A, 8 * spec.U,
                                     6 * spec.U, test_mode=test_mode)
     for s, key in enumerate(("home", "away")):
         for k, v in out[key].items():
-            np.testing.assert_array_equal(nbs[s][k], v, err_msg=f"{key}[{k}]")
-    assert stepper.t == out["t"]
-    np.testing.assert_array_equal(stepper.last_run["returns"].numpy(), np.float32(out["returns"][0]))
-    np.testing.assert_array_equal(stepper.last_run["away_returns"].numpy(), np.float32(out["returns"][1]))
-    assert [infos[i] for i in range(B)] == out["env_infos"]
-    if not test_mode:
-        assert int(ep_len.sum()) == out["env_steps"]
+            np.testing.assert_array_equal(nbs[s][k][sub], v, err_msg=f"{key}[{k}]")
+    np.testing.assert_array_equal(stepper.last_run["returns"].numpy()[sub], np.float32(out["returns"][0]))
+    np.testing.assert_array_equal(stepper.last_run["away_returns"].numpy()[sub], np.float32(out["returns"][1]))
+    if envs is None:
+        assert stepper.t == out["t"]
+        assert [infos[i] for i in range(B)] == out["env_infos"]
+        if not test_mode:
+            assert int(ep_len.sum()) == out["env_steps"]
+    else:
+        assert stepper.t == ep_len.max() and len(infos) == B
     # --- agent side per side: oracle Q on the recorded batch; greedy / epsilon picks bit-exact ---
-    n_random = 0
+    n_random = n_greedy = n_tie = 0
     for s, (mac, nb) in enumerate(zip(macs, nbs)):
         params = {k: v.detach().cpu() for k, v in mac.agent.state_dict().items()}
-        tb = {k: torch.from_numpy(v) for k, v in nb.items()}
+        tb = {k: torch.from_numpy(v[sub]) for k, v in nb.items()}
         with torch.no_grad():
-            q, _ = LR.mac_unroll(params, tb, N, T=int(ep_len.max()) + 1)
-        q = q.numpy()
-        for b in range(B):
+            q, _ = LR.mac_unroll(params, tb, N, T=int(ep_len[sub].max()) + 1)
+        q = dict(zip(sub.tolist(), q.numpy()))
+        for b in sub.tolist():
             for t in range(int(ep_len[b]) + 1):
                 for n in range(N):
                     a = int(nb["actions"][b, t, n, 0])
@@ -91,14 +102,17 @@ def _check_sides(stepper, macs, args, batches, infos, episode, test_mode, eps):
                             assert a == envref.random_available(av.tolist(), r2)
                             n_random += 1
                             continue
-                    m = np.where(av == 0, -np.inf, q[b, t, n])
+                    m = np.where(av == 0, -np.inf, q[b][t, n])
                     srt = np.sort(m)
+                    n_greedy += 1
                     if srt[-1] - srt[-2] > Q_TOL:
                         assert a == int(np.argmax(m)), (s, b, t, n)
                     else:
                         assert m[a] >= srt[-1] - Q_TOL
+                        n_tie += 1
     if not test_mode and max(eps) > 0.2:
         assert n_random > 0
+    return {"greedy": n_greedy, "near_ties": n_tie, "epsilon_draws": n_random}
 
 
 @pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium_1h_2t_2a_melee"])
@@ -194,6 +208,23 @@ def test_selfplay_headline_shape_properties(device):
             o = r.obs()
             np.testing.assert_array_equal(nbs[0]["obs"][b, t + 1], o[:N])
             np.testing.assert_array_equal(nbs[1]["obs"][b, t + 1], o[N:])
+
+
+def test_selfplay_headline_shape_agent_parity(device):
+    """config 3 at its full shape (5v5 self-play, 4096 envs, episode_limit 100, train mode at the
+    steady-state epsilon 0.05 on both sides, the sp7 kernel): 64 envs spread over the launch, BOTH sides, replayed
+    through the oracle self-play stepper + C env (both batches and returns bit-exact) and the fp32 oracle MAC of each
+    side -- every epsilon draw bit-exact vs the counter RNG, every greedy pick the oracle's argmax (near ties within
+    Q_TOL). self_play_stepper.py:44-147, basic_controller.py:29-36."""
+    stepper, home, away, args = _build(device, B=4096, episode_limit=100, seed=0)
+    stepper.t_env = 10 ** 6
+    hb, ab, infos = stepper.run(test_mode=False)
+    eps = tuple(float(e) for e in stepper.epsilons)
+    assert eps == (pytest.approx(0.05), pytest.approx(0.05))
+    sub = np.linspace(0, 4095, 64).astype(int)
+    n = _check_sides(stepper, (home, away), args, (hb, ab), infos, episode=0, test_mode=False, eps=eps, envs=sub)
+    print(f"config-3 full-shape agent parity: {n}")
+    assert n["greedy"] > 10000 and n["epsilon_draws"] > 0
 
 
 def test_selfplay_episode_stepper(device):
@@ -328,7 +359,8 @@ def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, monkeypatch):
                 worst = max(worst, float((qm.max(axis=-1) - chosen).max()))
     assert worst <= 1e-5, worst
     n_diff = assert_near_tie_divergence(out["sp2"][0], nbs, qs, B)  # only near-tie flips diverge
-    assert n_diff <= B // 10, n_diff
+    print(f"sp7 vs sp2 [{plan}]: {n_diff} of {B} episodes diverge (near-tie flips)")
+    assert n_diff <= SP7_MAX_DIVERGING[plan], (plan, n_diff)
 
 
 @pytest.mark.parametrize("compat", [False, True])
@@ -347,3 +379,72 @@ def test_league_record_runs_device_kernel(device, compat):
         lg_h.record_runs(home, away, torch.from_numpy(won), torch.from_numpy(draw))
     np.testing.assert_array_equal(lg_d._delta.cpu().numpy(), lg_h._delta.numpy())
     assert lg_h._delta[0, 2, 1:4].sum() == 2 * B
+
+
+def _league_args(B, episode_limit, **over):
+    from maleague.utils.config import build_config, to_args
+    cfg = build_config("qmix", "ma", overrides=[f"batch_size_run={B}", "runner=parallel", "buffer_cpu_only=False",
+                                                "buffer_size=8192", f"env_args.episode_limit={episode_limit}",
+                                                "t_max=1000000000", "test_interval=100000000",
+                                                "league_checkpoint_min_steps=1", "league_checkpoint_max_steps=1"]
+                       + [f"{k}={v}" for k, v in over.items()])
+    return to_args(cfg)
+
+
+def test_league_main_player_faces_historical_4096(device):
+    """a role-based main player at the config-3 per-learner shape (4096 envs, episode_limit 100) takes
+    snapshots and, within a bounded number of league iterations, draws a historical opponent
+    (main_player.py:18-43: PFSP over historical players): the away MAC then holds that snapshot's parameters (not the
+    current ones) and the games land in the payoff row of the snapshot."""
+    from maleague.custom_logging import MainLogger
+    from maleague.league import DistributedLeague, LeagueInstance, PayoffEntry
+    from maleague.runs.sp_ma_experiment import agent_vector
+    lg = DistributedLeague(n_players=1, device=device, max_historical=3)
+    inst = LeagueInstance(_league_args(4096, 100), MainLogger(), lg, mode="rolebased", role=["main"])
+    hist_it = None
+    for it in range(10):
+        assert inst.sync() is not None
+        if inst.history[-1][2]:
+            hist_it = it
+            break
+        inst.play(1)
+    assert hist_it is not None, inst.history
+    opp = inst.opponent
+    assert opp >= 1 and any(h[0] == opp for h in lg.historical_meta)
+    away = agent_vector(inst.experiment.away_mac).clone()
+    assert torch.equal(away, lg.params_of(opp))
+    games0 = float(lg.payoff.tensor[0, opp, PayoffEntry.GAMES])
+    inst.play(1)
+    assert torch.equal(agent_vector(inst.experiment.away_mac), away)  # the snapshot stays frozen
+    assert not torch.equal(away, agent_vector(inst.experiment.home_mac))  # the main player trained past it
+    lg.sync_payoff()
+    torch.cuda.synchronize()
+    assert float(lg.payoff.tensor[0, opp, PayoffEntry.GAMES]) == games0 + 4096
+    assert float(lg.payoff.tensor[0, opp, PayoffEntry.WIN:PayoffEntry.DRAW + 1].sum()) == games0 + 4096
+
+
+def test_league_main_exploiter_vs_replicated_main(device):
+    """a MainExploiter (exploiters.py:8-65) trained on one GPU against a main player whose parameters
+    are a fixed replica (DistributedLeague(player_id=1), set_player_params): it plays the main player, the away MAC
+    holds the replica, its results land in payoff[1, 0], and it checkpoints itself (parent 1)."""
+    from maleague.custom_logging import MainLogger
+    from maleague.league import DistributedLeague, LeagueInstance, MainExploiter, PayoffEntry
+    from maleague.runs.sp_ma_experiment import agent_vector
+    lg = DistributedLeague(n_players=2, device=device, max_historical=3, player_id=1)
+    inst = LeagueInstance(_league_args(4096, 100), MainLogger(), lg, mode="rolebased",
+                          role=["main", "main_exploiter"], seed=1)
+    assert isinstance(inst.me, MainExploiter) and inst.pid == 1
+    ex = inst.experiment
+    g = torch.Generator(device="cpu").manual_seed(123)
+    home0 = agent_vector(ex.home_mac)
+    main_vec = (0.1 * torch.randn(home0.numel(), generator=g)).to(device)  # the main player's replica
+    lg.set_player_params(0, main_vec)
+    for it in range(3):
+        assert inst.sync() == (0, False)  # the exploiter's only main player (no win rate > 0.1 test can fail yet)
+        assert torch.equal(agent_vector(ex.away_mac), main_vec)
+        assert torch.equal(lg.params_of(0), main_vec)
+        inst.play(1)
+    lg.sync_payoff()
+    torch.cuda.synchronize()
+    assert float(lg.payoff.tensor[1, 0, PayoffEntry.GAMES]) == 3 * 4096
+    assert [p for _, p, _ in lg.historical_meta] == [1, 1]  # checkpoints at the 2nd and 3rd sync (trained > 1 step)
