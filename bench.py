@@ -234,8 +234,13 @@ def league_workload(world, plan, a, roles=None):
 def kernel_names(mode, N, A, kc1=0):
     v7 = "rollout_v2_kernel<64, true, 5, 10>" if (N, A) == (5, 15) else (
         "rollout_v2_kernel<64, true, 3, 6>" if (N, A) == (3, 11) else "rollout_v2_kernel<64, true>")
-    sp7 = "rollout_sp7_kernel<10, 10>" if (N, A) == (5, 15) else (
-        "rollout_sp7_kernel<6, 6>" if (N, A) == (3, 11) else "rollout_sp7_kernel<0, 0>")
+    # self-play: the one-round sp8 kernel for the static 5v5 / 3v3 shapes, sp7 otherwise (MLG_ROLLOUT_KERNEL=sp7: sp7)
+    sp8_on = os.environ.get("MLG_ROLLOUT_KERNEL") not in ("sp7", "sp2", "v1") and not os.environ.get("MLG_ROLLOUT_GENERIC")
+    if sp8_on and (N, A) in ((5, 15), (3, 11)):
+        sp7 = "rollout_sp8_kernel<10, 10>" if (N, A) == (5, 15) else "rollout_sp8_kernel<6, 6>"
+    else:
+        sp7 = "rollout_sp7_kernel<10, 10>" if (N, A) == (5, 15) else (
+            "rollout_sp7_kernel<6, 6>" if (N, A) == (3, 11) else "rollout_sp7_kernel<0, 0>")
     # the four-env kernel for the entity width of the env variant; its refil_8 shape (8 agents, 21 actions) runs the
     # static 16-unit instantiation unless MLG_REFIL_GENERIC is set
     st16 = (N, A) == (8, 21) and not os.environ.get("MLG_REFIL_GENERIC")

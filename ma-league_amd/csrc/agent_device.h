@@ -19,12 +19,14 @@
 //                 {W_in;W_hn} rows, pieces 0..2; a u32 = two bf16), so a weight swap is 18 straight loads
 //   w1s [H/16 chunks][KK][3 pieces][64 lanes][4]  (H = 64 only) fc1 obs columns as split-bf16 A operands
 //                 (K steps of 32, zero padded past d_obs)
+//   w2s [Ap/16][2 K steps][3 pieces][64 lanes][4]  (H = 64 only) fc2 as split-bf16 A operands (rows >= A zero; the
+//                 one-round self-play kernel sp8 runs fc2 on the bf16 planes of h')
 #pragma once
 #include "mlg_device.h"
 
 struct AgentLayout {
     int H, A, Ap, N, d_obs, Dob, d_in, Dip, last_action, agent_id;
-    int32_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, gsp, w1s, total;  // 32-bit: fewer SGPRs
+    int32_t w1d, w1o, w1a, w1n, b1, wih, bih, whh, bhh, brz, w2, b2, gsp, w1s, w2s, total;  // 32-bit: fewer SGPRs
 };
 
 __host__ __device__ constexpr int64_t mlg_align4(int64_t v) { return (v + 3) & ~int64_t(3); }
@@ -57,6 +59,7 @@ __host__ __device__ constexpr AgentLayout make_agent_layout(const MlgAgentDims& 
     o = mlg_align4(o);
     L.gsp = o; o += L.H == 64 ? 8 * 18 * 64 * 4 : 0;
     L.w1s = o; o += L.H == 64 ? (int64_t)(L.H / 16) * ((L.Dob + 31) / 32) * 3 * 64 * 4 : 0;
+    L.w2s = o; o += L.H == 64 ? (int64_t)(L.Ap / 16) * 2 * 3 * 64 * 4 : 0;
     L.total = mlg_align4(o);
     return L;
 }
@@ -107,7 +110,7 @@ __device__ __forceinline__ float pack_agent_elem(const AgentLayout& L, const Mlg
                                                 : (hi ? p.w_hh : p.w_ih) + (int64_t)(2 * H + f) * H);
         const int kb = 32 * kk + 8 * g + 2 * q;
         v = split_bf16_pair(src[kb], src[kb + 1], piece);
-    } else {  // split fc1 obs columns: k = (((j * KK + kk) * 3 + piece) * 64 + lane) * 4 + q
+    } else if (i < L.w2s) {  // split fc1 obs columns: k = (((j * KK + kk) * 3 + piece) * 64 + lane) * 4 + q
         const int64_t k = i - L.w1s;
         const int KK = (L.Dob + 31) / 32;
         const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), r = (int)(k >> 8);
@@ -116,6 +119,14 @@ __device__ __forceinline__ float pack_agent_elem(const AgentLayout& L, const Mlg
         const int kb = 32 * kk + 8 * (lane >> 4) + 2 * q;
         const float a = kb < L.d_obs ? p.fc1_w[row * L.d_in + kb] : 0.f;
         const float b = kb + 1 < L.d_obs ? p.fc1_w[row * L.d_in + kb + 1] : 0.f;
+        v = split_bf16_pair(a, b, piece);
+    } else if (i < L.total) {  // split fc2: k = ((((at * 2 + kk) * 3 + piece) * 64 + lane) * 4 + q
+        const int64_t k = i - L.w2s;
+        const int q = (int)(k & 3), lane = (int)((k >> 2) & 63), r = (int)(k >> 8);
+        const int piece = r % 3, kk = (r / 3) % 2, at = r / 6;
+        const int row = 16 * at + (lane & 15), kb = 32 * kk + 8 * (lane >> 4) + 2 * q;
+        const float a = row < L.A ? p.fc2_w[(int64_t)row * H + kb] : 0.f;
+        const float b = row < L.A ? p.fc2_w[(int64_t)row * H + kb + 1] : 0.f;
         v = split_bf16_pair(a, b, piece);
     }
     return v;

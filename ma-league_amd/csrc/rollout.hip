@@ -2272,6 +2272,7 @@ __global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel
 // Standalone env kernels (one thread per env) -- the EnvWorker command set for host-side TeamsEnv use
 // and for kernel-level parity tests.
 #include "rollout_sp.inc"
+#include "rollout_sp8.inc"
 
 __global__ void env_reset_kernel(MlgEnvSpec spec, MlgEnvState st) {
     __shared__ SpecShared SS;
@@ -2681,10 +2682,33 @@ extern "C" int mlg_rollout_selfplay(const MlgEnvSpec* spec, MlgEnvState* st, con
     sd.eps[1] = test_mode ? 0.f : eps_away;
     sd.ns = 2;
     sd.nh = nh;
-    // self-play kernels (two policies): sp7 (v7 agent phases) for H = 64, else sp2 (v2 structure) when the shape
-    // allows it, else the generic v1 kernel. MLG_ROLLOUT_KERNEL=v1 | sp2 forces one.
+    // self-play kernels (two policies): sp8 (one round of 16-env workgroups) for the static 5v5 / 3v3 self-play shapes
+    // at H = 64, else sp7 (v7 agent phases, 8 envs per workgroup) for H = 64, else sp2 (v2 structure) when the shape
+    // allows it, else the generic v1 kernel. MLG_ROLLOUT_KERNEL=v1 | sp2 | sp7 forces one.
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
     const bool force_v1 = k && k[0] == 'v' && k[1] == '1', force_sp2 = k && !strcmp(k, "sp2");
+    const bool force_sp7 = k && !strcmp(k, "sp7");
+    if (!force_v1 && !force_sp2 && !force_sp7 && L.H == 64 && !getenv("MLG_ROLLOUT_GENERIC")) {
+        void (*kern8)(MlgEnvSpec, MlgEnvState, const float*, const float*, MlgBatch, MlgBatch, MlgRunInfo, float, float,
+                      int) = nullptr;
+        size_t bytes = 0;
+        if (static_shape_matches_sp8<10, 10>(L, spec->n_agents)) {
+            kern8 = rollout_sp8_kernel<10, 10>;
+            bytes = (size_t)StaticShapeSP8<10, 10>::lay.total * 4;
+        } else if (static_shape_matches_sp8<6, 6>(L, spec->n_agents)) {
+            kern8 = rollout_sp8_kernel<6, 6>;
+            bytes = (size_t)StaticShapeSP8<6, 6>::lay.total * 4;
+        }
+        if (kern8) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern8),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+            if (e != hipSuccess)
+                return mlg::fail("rollout_selfplay: LDS attribute (%zu B): %s", bytes, hipGetErrorString(e));
+            hipLaunchKernelGGL(kern8, dim3((st->B + RS8 - 1) / RS8), dim3(512), bytes, (hipStream_t)stream, *spec, *st,
+                               home_packed, away_packed, *home, *away, *info, sd.eps[0], sd.eps[1], test_mode);
+            return mlg::check_launch("rollout_sp8_kernel");
+        }
+    }
     const RolloutLdsSP l7 = make_rollout_lds_sp(L, spec->U, spec->n_agents, true);
     if (!force_v1 && !force_sp2 && L.H == 64 && L.Dob <= 32 * SP7_MAXKK && l7.total * 4 <= LDS_LIMIT_BYTES) {
         const size_t bytes = (size_t)l7.total * 4;

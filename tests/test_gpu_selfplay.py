@@ -321,25 +321,28 @@ def test_selfplay_kernel_equals_v1(device, plan, monkeypatch):
         assert torch.equal(out["v1"][i], out["sp"][i])
 
 
+@pytest.mark.parametrize("kernel", ["sp8", "sp7"])
 @pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium"])
-def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, monkeypatch):
-    """sp7 (default for H = 64): the v7 agent phases with two policies -- GRU products as split-bf16 fp32 emulation,
-    each wave swapping between the home and away weights. Along sp7's own trajectory (test mode) the fp32 oracle
-    MAC of each side must rate every recorded action as an available argmax up to a 1e-5 tie, and sp7 must
+def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, kernel, monkeypatch):
+    """sp8 (default for the static 5v5 / 3v3 self-play shapes at H = 64: one round of 16-env workgroups, x / h' as bf16
+    planes in two step-parity LDS regions, fc2 split-bf16 on the h' planes) and sp7 (8 envs per workgroup; the default
+    for other H = 64 shapes): the v7 agent phases with two policies -- GRU products as split-bf16 fp32 emulation, each
+    wave swapping between the home and away weights. Along the kernel's own trajectory (test mode) the fp32 oracle
+    MAC of each side must rate every recorded action as an available argmax up to a 1e-5 tie, and the kernel must
     reproduce sp2's episodes bit for bit except where a near-tie flips an argmax (the env code is sp2's)."""
     from maleague.envs.teams_env import VecEnvState
     B, TL = 100, 60
     stepper, home, away, args = _build(device, plan=plan, B=B, episode_limit=TL, seed=3)
     out = {}
-    for k in ("sp2", "sp7"):
-        if k == "sp2":
-            monkeypatch.setenv("MLG_ROLLOUT_KERNEL", "sp2")
-        else:
+    for k in ("sp2", kernel):
+        if k == "sp8":
             monkeypatch.delenv("MLG_ROLLOUT_KERNEL", raising=False)
+        else:
+            monkeypatch.setenv("MLG_ROLLOUT_KERNEL", k)
         stepper.envs = VecEnvState(stepper.spec, B, device)
         hb, ab, _ = stepper.run(test_mode=True)
         out[k] = ([np_batch(hb), np_batch(ab)], stepper.last_run["ep_len"].numpy().copy())
-    nbs, L = out["sp7"]
+    nbs, L = out[kernel]
     N = args.n_agents
     worst = 0.0
     qs = []
@@ -359,8 +362,8 @@ def test_selfplay_sp7_split_bf16_matches_fp32(device, plan, monkeypatch):
                 worst = max(worst, float((qm.max(axis=-1) - chosen).max()))
     assert worst <= 1e-5, worst
     n_diff = assert_near_tie_divergence(out["sp2"][0], nbs, qs, B)  # only near-tie flips diverge
-    print(f"sp7 vs sp2 [{plan}]: {n_diff} of {B} episodes diverge (near-tie flips)")
-    assert n_diff <= SP7_MAX_DIVERGING[plan], (plan, n_diff)
+    print(f"{kernel} vs sp2 [{plan}]: {n_diff} of {B} episodes diverge (near-tie flips)")
+    assert n_diff <= SP7_MAX_DIVERGING[plan], (kernel, plan, n_diff)
 
 
 @pytest.mark.parametrize("compat", [False, True])
