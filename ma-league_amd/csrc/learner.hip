@@ -305,11 +305,7 @@ struct LStamps {
     __device__ void flush(int) {}
 };
 #endif
-#ifdef MLG_TE_CAP  // timing variant builds only (wrong results): cap the recurrences' step count
-__device__ __forceinline__ int t_eff(const float* msum) { return min((int)msum[1], MLG_TE_CAP); }
-#else
 __device__ __forceinline__ int t_eff(const float* msum) { return (int)msum[1]; }
-#endif
 
 
 // ================================================================================================

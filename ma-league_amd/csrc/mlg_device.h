@@ -73,15 +73,6 @@ struct Split3 {
 __device__ __forceinline__ Split3 split3(floatx4 a, floatx4 b) {
     float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     Split3 s;
-#ifdef MLG_G8_NOSPLIT  // timing ablation only: one conversion, copied to all pieces
-    {
-        u32x4 w;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
-        s.p[0] = s.p[1] = s.p[2] = __builtin_bit_cast(bf16x8, w);
-        return s;
-    }
-#endif
 #pragma unroll
     for (int lvl = 0; lvl < 3; ++lvl) {
         u32x4 w;
@@ -102,9 +93,6 @@ __device__ __forceinline__ Split3 split3(floatx4 a, floatx4 b) {
 
 // acc += A . B over one 32-wide K step with the six partial products (small terms first).
 __device__ __forceinline__ floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 c) {
-#ifdef MLG_G8_P1  // timing ablation only: the leading product alone
-    return mfma_bf16(a.p[0], b.p[0], c);
-#endif
     c = mfma_bf16(a.p[2], b.p[0], c);
     c = mfma_bf16(a.p[1], b.p[1], c);
     c = mfma_bf16(a.p[0], b.p[2], c);

@@ -936,7 +936,7 @@ __device__ __forceinline__ void v2_observe(const UnitMasks& M, const MlgEnvSpec&
 // Barriers per step: A|B, B|C, C|env, env|A.
 struct RolloutLds2 {
     int32_t w1o, w1a, w1n, b1, w2, b2, gb, obs, avail, xb, hb, hsz, pairtab, avtab, pk, act, am, rmap, hpl, total;
-    int ldo, ldh, nhb;  // nhb: hidden-state buffers (2: double buffered by step parity; 1: v6 / v7, see below)
+    int ldo, ldh, nhb;  // nhb: hidden-state buffers (2: double buffered by step parity, v2; 1: v7, see below)
     int xpl;            // v7: x held as three bf16 planes per row, row stride XPL_STRIDE words (0: fp32 rows)
     int rms;            // v7: words per wave row map
     RoEnvLds env;
@@ -965,11 +965,9 @@ __host__ __device__ constexpr RolloutLds2 make_rollout_lds2(const AgentLayout& L
     r.gb = ro_take(o, 4 * L.H);
     const int rows = rew * N, rows16 = (rows + 15) / 16 * 16;
     // v7: one fp32 hidden-state buffer (updated in place: each lane reads and writes only its own two features of a
-    // row, the GRU's h operand comes from the h planes below), so nhb is 1 without v6's aliasing.
+    // row, the GRU's h operand comes from the h planes below), so nhb is 1.
     if (xpl) nhb = 1;
-    // nhb == 1 (v6): the obs rows double as the compact h' rows between the GRU and fc2 phases
-    const int64_t nobs = (int64_t)rows * r.ldo, nhx = (nhb == 1 && !xpl) ? (int64_t)rows16 * r.ldh : 0;
-    r.obs = ro_take(o, nobs > nhx ? nobs : nhx);
+    r.obs = ro_take(o, (int64_t)rows * r.ldo);
     r.avail = ro_take(o, (int64_t)rows * 2);  // uint64 avail mask per agent row
     r.xb = ro_take(o, (int64_t)rows16 * (xpl ? XPL_STRIDE : r.ldh));
     // v7: h' of step t as three bf16 planes per compact row of step t (split once, by the fc2 phase), the GRU's h
@@ -998,7 +996,7 @@ __device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
     return __builtin_ctz(m);
 }
 
-// Workgroup-wide prologue of the v2/v4 kernels: spec tables, small weights -> LDS (padded rows), activation
+// Workgroup-wide prologue of the v2 / v7 kernels: spec tables, small weights -> LDS (padded rows), activation
 // buffers zeroed (the obs pad columns stay zero), index tables.
 __device__ void v2_prologue(const MlgEnvSpec& spec, const AgentLayout& L, const float* __restrict__ P,
                             const RolloutLds2& lay, int* smem, int rows) {
@@ -1044,7 +1042,7 @@ __device__ void v2_prologue(const MlgEnvSpec& spec, const AgentLayout& L, const 
     __syncthreads();
 }
 
-// ---- agent phase pieces (shared by v2 and v4) -----------------------------------------------------
+// ---- agent phase pieces (v2) ---------------------------------------------------------------------
 // The wave's GRU weight rows for feature chunk j (3 gates x 16 features x H, A-operand layout) + biases.
 template <int H>
 struct GruChunk {
@@ -1141,9 +1139,8 @@ __device__ inline void ph_fc1(const AgentLayout& L, const RolloutLds2& lay, floa
     }
 }
 
-// B: GRU cell for (tile, chunk j) -> h' (rows of running envs, hidden state indexed by env row). CX: h' goes to
-// a compact-row buffer instead (row cr of the tile list; v6), copied back to the env rows by phase C.
-template <int H, bool CX = false>
+// B: GRU cell for (tile, chunk j) -> h' (rows of running envs, hidden state indexed by env row).
+template <int H>
 __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, float* fm, const float* hc, float* hn,
                               const StepRows& SR, int N_, int j, int ti0, int dt, int lane) {
     constexpr int HC = H / 16;
@@ -1176,10 +1173,7 @@ __device__ inline void ph_gru(const GruChunk<H>& W, const RolloutLds2& lay, floa
             const float ng = tanhf(ain[r] + rg * ahn[r]);
             hv[r] = ng + zg * (ho[r] - ng);
         }
-        if (CX)
-            *reinterpret_cast<floatx4*>(hn + (int64_t)cr * ldh + j * 16 + 4 * g) = hv;
-        else if (valid)
-            *reinterpret_cast<floatx4*>(hn + (int64_t)er * ldh + j * 16 + 4 * g) = hv;
+        if (valid) *reinterpret_cast<floatx4*>(hn + (int64_t)er * ldh + j * 16 + 4 * g) = hv;
     }
 }
 
@@ -1480,18 +1474,15 @@ __device__ inline void ph_gru_g8(const GruG8& W, const RolloutLds2& lay, float* 
     // this lane's two output features after the exchange: lower lanes 8w+4g+{0,1}, upper 8w+4(g-2)+2+{0,1}
     const int fo = 8 * w + 4 * ((lane >> 4) & 1) + (lane >= 32 ? 2 : 0);
     int ti = 0;
-#ifndef MLG_GRU_SERIAL  // A/B: one tile at a time
     for (; ti + 1 < tiles; ti += 2) gru_g8_tiles<2>(W, lay, fm, rmap, hb, ti, N, fo, lane);
-#endif
     for (; ti < tiles; ++ti) gru_g8_tiles<1>(W, lay, fm, rmap, hb, ti, N, fo, lane);
 }
 
 // C: fc2 + masked argmax + epsilon-greedy per tile; records the actions (batch + LDS pending actions).
-// CX: h' is read from the compact-row buffer hn and the tile's valid rows are stored to the env rows of hstore.
-template <int H, bool CX = false>
+template <int H>
 __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, const RolloutLds2& lay, float* fm,
                               const RoEnv& R, const MlgBatch& bt, const float* hn, const StepRows& SR, int ti0, int dt,
-                              int e0, int t, float eps, int test_mode, int lane, float* hstore = nullptr) {
+                              int e0, int t, float eps, int test_mode, int lane) {
     constexpr int HC = H / 16;
     const int col = lane & 15, g = lane >> 4, N = L.N, ldh = lay.ldh, A = spec.n_actions, n_at = L.Ap / 16;
     const uint64_t* lavm = reinterpret_cast<const uint64_t*>(fm + lay.avail);
@@ -1502,12 +1493,7 @@ __device__ inline void ph_fc2(const MlgEnvSpec& spec, const AgentLayout& L, cons
         int e, n;
         const bool valid = SR.at(cr, e, n);
         const int er = e * N + n;
-        const float* hr = hn + (int64_t)(CX ? cr : er) * ldh + 4 * g;
-        if (CX && valid) {
-#pragma unroll
-            for (int kc = 0; kc < HC; ++kc)
-                *reinterpret_cast<floatx4*>(hstore + (int64_t)er * ldh + 4 * g + kc * 16) = ld4(hr + kc * 16);
-        }
+        const float* hr = hn + (int64_t)er * ldh + 4 * g;
         const uint64_t avm = lavm[er];
         ArgmaxState as{-INFINITY, 1 << 30};
         for (int at = 0; at < n_at; ++at) {
@@ -1634,11 +1620,9 @@ __device__ inline void ph_fc2_g8(const MlgEnvSpec& spec, const AgentLayout& L, c
         if (valid && g == 0) {
             if (ract >= 0) act = ract;
             R.pact[e * N + n] = act;
-#ifndef MLG_ABL_FC2_NOSTORE  // timing ablation only
             const int64_t bt_off = ((int64_t)R.slot[e] * bt.T1 + t) * N + n;
             gst(bt.actions + bt_off, (int64_t)act);
             if (!bt.full_write) gst(bt.actions_onehot + bt_off * A + act, 1.0f);
-#endif
         }
     }
 }
@@ -1672,7 +1656,7 @@ __device__ inline void hpl_split_tile(const RolloutLds2& lay, float* fm, const i
     }
 }
 
-// ---- env lanes (half-wave per env; shared by v2 and v4) -------------------------------------------
+// ---- env lanes (half-wave per env; v2 / v7) -----------------------------------------------------
 struct EnvLane {
     UnitLane u;
     int e, b, st, slot, len, h0, act;
@@ -1766,9 +1750,6 @@ __device__ inline void env_lane_step1(const EnvCtx& C, EnvLane& E, int t, int hl
         if (!C.bt.full_write) gst(C.bt.actions_onehot + off * A, 1.0f);
     }
     if (hl < N) C.R.prev[E.e * N + hl] = pact[hl];
-#ifdef MLG_DUP_ONEHOT
-    for (int rep = 0; rep < 2; ++rep)
-#endif
     if (C.bt.full_write) {  // whole one-hot rows of the recorded actions
         const int64_t oh = ((int64_t)E.slot * T1 + t) * N * A;
         // rolled: the unrolled copy's rounded trip count was the v2 kernel's last VGPR spill, and its in-loop
@@ -1866,14 +1847,8 @@ __device__ inline void env_lane_step2(const EnvCtx& C, EnvLane& E, int t, int hl
     sp.mark(6);
     // observation at t + 1 (incl. envs that just terminated)
     v2_pair_pass(C.M, U, hl, E.u, C.pk + E.e * 32);
-#ifdef MLG_DUP_PAIR
-    v2_pair_pass(C.M, U, hl, E.u, C.pk + E.e * 32);
-#endif
     sp.mark(7);
     env_observe(C, spec, E.slot, t + 1, E.e, hbase, hl, E.u, sp);
-#ifdef MLG_DUP_OBS
-    env_observe(C, spec, E.slot, t + 1, E.e, hbase, hl, E.u, sp);
-#endif
 }
 
 // Full-write mode: a finished env's half-wave zeroes a few more steps of its slot's tail.
@@ -1938,11 +1913,9 @@ __device__ inline EnvCtx make_env_ctx(const MlgEnvSpec& spec, const RolloutLds2&
 // from the spill lanes.
 __device__ __forceinline__ EnvCtx env_ctx_step(const EnvCtx& C) {
     EnvCtx c = C;
-#ifndef MLG_ENV_SGPR_CTX  // A/B: the loop-invariant (SGPR) context
     asm volatile("" : "+v"(c.M.team1), "+v"(c.M.healer), "+v"(c.M.tank), "+v"(c.M.melee));
     asm volatile("" : "+v"(c.bt.obs), "+v"(c.bt.state), "+v"(c.bt.avail), "+v"(c.bt.actions));
     asm volatile("" : "+v"(c.bt.actions_onehot), "+v"(c.bt.reward), "+v"(c.bt.terminated), "+v"(c.bt.filled));
-#endif
     return c;
 }
 
@@ -1963,10 +1936,8 @@ struct StaticShape {
 // The batch pointers as eight independent SGPR pairs: loaded as one 16-SGPR tuple (s_load_dwordx16), a spilled
 // tuple is reloaded whole (16 v_readlane) wherever any one pointer is used.
 __device__ __forceinline__ MlgBatch split_batch_sgprs(MlgBatch b) {
-#ifndef MLG_ENV_SGPR_CTX
     asm volatile("" : "+s"(b.obs), "+s"(b.state), "+s"(b.avail), "+s"(b.actions));
     asm volatile("" : "+s"(b.actions_onehot), "+s"(b.reward), "+s"(b.terminated), "+s"(b.filled));
-#endif
     return b;
 }
 
@@ -1993,9 +1964,6 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
     else
         load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
     __syncthreads();
-#ifdef MLG_PRIO  // A/B: static priority for the second-dispatched half of the workgroup (MI355X_MICROARCH.md)
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
     Stamps sp;
     sp.init();
     uint64_t rows_issued = 0;  // agent rows issued to the MFMA cell (incl. tile padding)
@@ -2015,23 +1983,15 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
             // rebuilt every step (skipping unchanged maps measured slower: the extra live registers spill)
             tiles = make_rmap(C.amask[lane & 15], wmap, lane, m_prev, x_prev);
             sp.mark(14);  // v7 stamps: row map (incl. the step's status ballot) in slot 14
-#ifndef MLG_FC1_SERIAL  // A/B: the tile-by-tile fc1
             if constexpr (SN > 0) {
                 const int nu = tiles > gi ? (tiles - gi + G - 1) / G : 0;
                 fc1_g8_static<H, (8 * SU + 31) / 32, (SN + G - 1) / G>(L, lay, fm, wmap, C.R.prev, nu, j, gi, G, t, lane);
             } else
-#endif
                 ph_fc1_g8<H>(L, lay, fm, wmap, C.R.prev, tiles, j, gi, G, t, lane);
-#ifdef MLG_DUP_FC1  // timing ablation only: the phase twice (idempotent)
-            ph_fc1_g8<H>(L, lay, fm, wmap, C.R.prev, tiles, j, gi, G, t, lane);
-#endif
         } else {
             SR = make_rows(C.amask, 0, 16, lane);
             tiles = SR.tiles;
             ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
-#ifdef MLG_DUP_FC1
-            ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
-#endif
         }
         rows_issued += tiles * 16;
         sp.mark(0);
@@ -2044,9 +2004,6 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
             ph_gru_g8<H>(W8, lay, fm, wmap, hn, tiles, N, wave, lane);
         else
             ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
-#ifdef MLG_DUP_GRU  // v2 only (v7 updates h in place: a second pass would not be idempotent)
-        if constexpr (!G8) ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
-#endif
         sp.mark(1);
         lds_barrier();
         if constexpr (G8) sp.mark(13);
@@ -2054,12 +2011,6 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
             ph_fc2_g8<H>(spec, L, lay, fm, wmap, C.R, bt, hn, tiles, wave, NW, e0, t, eps, test_mode, lane, pre);
         else
             ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
-#ifdef MLG_DUP_FC2
-        if constexpr (G8)
-            ph_fc2_g8<H>(spec, L, lay, fm, wmap, C.R, bt, hn, tiles, wave, NW, e0, t, eps, test_mode, lane);
-        else
-            ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, NW, e0, t, eps, test_mode, lane);
-#endif
         // v7: h' planes (hpl_split_tile) by the waves that have no fc2 tile, beside the fc2 phase (when every wave has
         // one -- tiles >= 8, generic shapes -- by the fc2 waves after their tiles)
         if constexpr (G8) {
@@ -2075,9 +2026,6 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         env_lane_step1(Ce, E, t, hl);
         sp.mark(4);
         env_lane_step2(Ce, E, t, hl, sp);
-#ifdef MLG_DUP_TAIL  // timing ablation: the tail zeroing twice over the same steps
-        if (!E.stepped && (t & 1)) { const int z0 = E.zcur; env_lane_tail(Ce, E, 8, hl); E.zcur = z0; }  // packed
-#endif
         if (!E.stepped && (t & 1)) env_lane_tail(Ce, E, 8, hl);
         sp.mark(8);
         lds_barrier();
@@ -2100,177 +2048,6 @@ __global__ void __launch_bounds__(512, 2) rollout_v2_kernel(MlgEnvSpec spec, Mlg
                                G8);  // v7 layouts hold no index tables (arithmetic indices)
 }
 
-// ================================================================================================
-// v6 kernel: v2 at half the size -- 4 waves, 8 envs -- so that two workgroups share a CU (LDS < 80 KB, 256
-// VGPRs per wave at one wave per SIMD per workgroup). The two workgroups' barriers are independent, so one
-// workgroup's env step (VALU / LDS latency) runs while the other's agent phases keep the matrix cores busy,
-// and a workgroup only runs as long as the longest of its 8 episodes. LDS is cut by holding the hidden
-// state once: the GRU writes h' to compact rows aliasing the obs buffer (dead between fc1 and the env
-// step), fc2 reads them there and stores the valid rows back to the env-row hidden state.
-// Barriers per step: A|B, B|C, C|env, env|A. Arithmetic identical to v2 (bit-identical batches).
-template <int H>
-__global__ void __launch_bounds__(256, 2) rollout_v6_kernel(MlgEnvSpec spec, MlgEnvState st, AgentLayout L,
-                                                           const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
-                                                           float eps, int test_mode, RolloutLds2 lay) {
-    constexpr int HC = H / 16, NW = 4, REW = 8, G = NW / HC;
-    extern __shared__ __attribute__((aligned(16))) int smem[];
-    float* fm = reinterpret_cast<float*>(smem);
-    const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
-    const int e0 = blockIdx.x * REW, T1 = bt.T1;
-    v2_prologue(spec, L, P, lay, smem, REW * N);
-    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info, spec.U, spec.n_agents, spec.n_actions, false);
-    EnvLane E;
-    env_lane_reset(C, st, E, wave * 2 + (lane >> 5), e0, hl);
-    const int j = wave % HC, gi = wave / HC;
-    GruChunk<H> W;
-    load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
-    __syncthreads();
-    Stamps sp;
-    sp.init();
-    uint64_t rows_issued = 0;
-    float* h = fm + lay.hb;
-    float* hx = fm + lay.obs;
-    for (int t = 0; t < T1; ++t) {
-        const uint32_t run = (uint32_t)__ballot(lane < REW && C.R.status[lane & (REW - 1)] < 2);
-        if (run == 0) break;
-        const StepRows SR = make_rows(C.amask, 0, REW, lane);
-        rows_issued += SR.tiles * 16;
-        ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, t, lane);
-        __syncthreads();
-        ph_gru<H, true>(W, lay, fm, h, hx, SR, N, j, gi, G, lane);
-        __syncthreads();
-        ph_fc2<H, true>(spec, L, lay, fm, C.R, bt, hx, SR, wave, NW, e0, t, eps, test_mode, lane, h);
-        __syncthreads();
-        env_lane_step1(C, E, t, hl);
-        env_lane_step2(C, E, t, hl, sp);
-        if (!E.stepped && (t & 1)) env_lane_tail(C, E, 8, hl);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && info.agent_rows) atomicAdd(info.agent_rows, (unsigned long long)rows_issued);
-    env_lane_finish(C, st, E, hl);
-}
-
-// ================================================================================================
-// v4 kernel: wave-specialised, two env groups in flight. Waves 0..AW-1 are agent waves (wave w owns GRU chunk
-// w % HC of tiles w / HC, w / HC + AW / HC, ... with its weights in VGPRs), the last 4 waves are env waves (half-wave per env: envs 0-7 form group 0,
-// 8-15 group 1; env wave v steps envs 2v, 2v + 1 of both groups). Phase p runs the agent step of group
-// X = p % 2 while the env waves run the env step of the other group, so the matrix cores work while the
-// envs step. Three barriers per phase (A|B, B|C, end); the env step is split to fit the agent segments:
-//   segment 1: agent A (fc1)        || env bookkeeping, executed actions, resolution
-//   segment 2: agent B (GRU)        || env reduction, reward, pair pass, observation
-//   segment 3: agent C (fc2+select) || tail zeroing (full-write mode)
-// Identical arithmetic to v1/v2 per env (bit-identical batches).
-template <int H, int AW>
-__global__ void __launch_bounds__((AW + 4) * 64, (AW + 4) / 4) rollout_v4_kernel(
-    MlgEnvSpec spec, MlgEnvState st, AgentLayout L, const float* __restrict__ P, MlgBatch bt, MlgRunInfo info,
-    float eps, int test_mode, RolloutLds2 lay) {
-    constexpr int HC = H / 16, REW = 16, G = AW / HC;
-    extern __shared__ __attribute__((aligned(16))) int smem[];
-    float* fm = reinterpret_cast<float*>(smem);
-    const int N = spec.n_agents, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31;
-    const int e0 = blockIdx.x * REW, T1 = bt.T1;
-    v2_prologue(spec, L, P, lay, smem, REW * N);
-    const EnvCtx C = make_env_ctx(spec, lay, smem, bt, info, spec.U, spec.n_agents, spec.n_actions, false);
-    // The two roles run separate copies of the phase loop (same uniform control state, same barrier count),
-    // so the agent waves' weight registers and the env waves' unit registers are allocated over each other.
-    // Phase state: tg[g] = next agent step of group g, pend[g] = env step tg[g] - 1 still to run.
-    struct PhaseState {  // scalar fields (no dynamically indexed local arrays)
-        int tg0, tg1;
-        bool pend0, pend1;
-        __device__ int tg(int x) const { return x ? tg1 : tg0; }
-        __device__ bool pend(int x) const { return x ? pend1 : pend0; }
-    };
-    auto phase_begin = [&](const PhaseState& ps, int p, uint32_t& runX, bool& done) {
-        const int X = p & 1;
-        const int sv = C.R.status[lane & 15];
-        const uint32_t run16 = (uint32_t)__ballot(lane < 16 && sv < 2);
-        runX = (run16 >> (8 * X)) & 0xFFu;
-        done = run16 == 0 && !ps.pend0 && !ps.pend1;
-    };
-    auto phase_end = [&](PhaseState& ps, int p, bool doAgent) {
-        const int X = p & 1;
-        if (X) {
-            ps.pend0 = false;
-            if (doAgent) { ps.pend1 = true; ps.tg1 += 1; }
-        } else {
-            ps.pend1 = false;
-            if (doAgent) { ps.pend0 = true; ps.tg0 += 1; }
-        }
-    };
-    Stamps sp;
-    if (wave < AW) {
-        const int j = wave % HC, gi = wave / HC;
-        GruChunk<H> W;
-        load_gru_chunk<H>(W, P, L, fm, lay, j, lane);
-        __syncthreads();
-        sp.init();
-        PhaseState ps{0, 0, false, false};
-        uint64_t rows_issued = 0;
-        for (int p = 0;; ++p) {
-            uint32_t runX;
-            bool done;
-            phase_begin(ps, p, runX, done);
-            if (done) break;
-            const int X = p & 1, tX = ps.tg(X);
-            const bool doAgent = runX != 0 && tX < T1;
-            const StepRows SR = make_rows(C.amask, 8 * X, 8, lane);
-            rows_issued += doAgent ? SR.tiles * 16 : 0;
-            const float* hc = fm + lay.hb + (tX & 1) * lay.hsz;
-            float* hn = fm + lay.hb + ((tX & 1) ^ 1) * lay.hsz;
-            if (doAgent) ph_fc1<H>(L, lay, fm, C.R.prev, SR, j, gi, G, tX, lane);
-            sp.mark(0);
-            __syncthreads();
-            if (doAgent) ph_gru<H>(W, lay, fm, hc, hn, SR, N, j, gi, G, lane);
-            sp.mark(1);
-            __syncthreads();
-            if (doAgent) ph_fc2<H>(spec, L, lay, fm, C.R, bt, hn, SR, wave, AW, e0, tX, eps, test_mode, lane);
-            sp.mark(2);
-            __syncthreads();
-            sp.mark(10);
-            phase_end(ps, p, doAgent);
-        }
-        sp.flush();
-        if (threadIdx.x == 0 && info.agent_rows) atomicAdd(info.agent_rows, (unsigned long long)rows_issued);
-    } else {
-        EnvLane E0, E1;  // this half-wave's env of group 0 and of group 1
-        const int v = wave - AW, h = lane >> 5;
-        env_lane_reset(C, st, E0, 2 * v + h, e0, hl);
-        env_lane_reset(C, st, E1, 8 + 2 * v + h, e0, hl);
-        __syncthreads();
-        sp.init();
-        PhaseState ps{0, 0, false, false};
-        for (int p = 0;; ++p) {
-            uint32_t runX;
-            bool done;
-            phase_begin(ps, p, runX, done);
-            if (done) break;
-            const int X = p & 1, Y = X ^ 1;
-            const bool doAgent = runX != 0 && ps.tg(X) < T1;
-            const bool pendY = ps.pend(Y);
-            const int tY = ps.tg(Y) - 1;
-            EnvLane& EY = Y ? E1 : E0;
-            if (pendY) env_lane_step1(C, EY, tY, hl);
-            sp.mark(4);
-            __syncthreads();
-            if (pendY) env_lane_step2(C, EY, tY, hl, sp);
-            sp.mark(5);
-            __syncthreads();
-            env_lane_tail(C, EY, 8, hl);
-            sp.mark(8);
-            __syncthreads();
-            sp.mark(10);
-            phase_end(ps, p, doAgent);
-        }
-        sp.flush();
-        env_lane_finish(C, st, E0, hl);
-        env_lane_finish(C, st, E1, hl);
-    }
-}
-
-
-// ------------------------------------------------------------------------------------------------
-// Standalone env kernels (one thread per env) -- the EnvWorker command set for host-side TeamsEnv use
-// and for kernel-level parity tests.
 #include "rollout_sp.inc"
 #include "rollout_sp8.inc"
 
@@ -2423,16 +2200,12 @@ int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& 
                       const float* P, const MlgBatch& bt, const MlgRunInfo& info, float eps, int tm,
                       const RolloutLds2& lay) {
     const size_t bytes = (size_t)lay.total * 4;
-    auto kern = V == 4 ? rollout_v4_kernel<H, 4>
-                       : (V == 5 ? rollout_v4_kernel<H, 8>
-                                 : (V == 6 ? rollout_v6_kernel<H>
-                                           : (V == 7 ? rollout_v2_kernel<64, true> : rollout_v2_kernel<H>)));
+    auto kern = V == 7 ? rollout_v2_kernel<64, true> : rollout_v2_kernel<H>;
     if (V == 7 && !getenv("MLG_ROLLOUT_GENERIC")) {
         if (static_shape_matches<5, 10>(L, lay)) kern = rollout_v2_kernel<64, true, 5, 10>;
         else if (static_shape_matches<3, 6>(L, lay)) kern = rollout_v2_kernel<64, true, 3, 6>;
     }
-    const int threads = V == 4 ? 512 : (V == 5 ? 768 : (V == 6 ? 256 : 512));
-    const int rew = V == 6 ? 8 : 16;
+    const int threads = 512, rew = 16;
     if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)bytes);
@@ -2444,15 +2217,11 @@ int launch_rollout_v2(hipStream_t s, const MlgEnvSpec& spec, const MlgEnvState& 
 }
 
 // v7 for H = 64 and v2 for H = 32 when the shape allows it (U <= 32, LDS fits), else v1. MLG_ROLLOUT_KERNEL=
-// v1|v2|v4|v5|v6|v7 forces a variant (v4 / v5: the wave-specialised kernel with 4 / 8 agent waves).
+// v1|v2|v7 forces a variant (v1: the reference restatement, v2: fp32 compacted; both kept for the bit-identity tests).
 int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay) {
     const char* k = getenv("MLG_ROLLOUT_KERNEL");
     const int want = (k && k[0] == 'v') ? k[1] - '0' : (L.H == 64 ? 7 : 2);
     if (want == 1 || (L.H != 64 && L.H != 32) || spec.U > 32) return 1;
-    if (want == 6) {  // two workgroups per CU need the layout to fit half the LDS
-        *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 8, 1);
-        if (lay->total * 4 <= LDS_LIMIT_BYTES / 2) return 6;
-    }
     *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
     if (lay->total * 4 > LDS_LIMIT_BYTES) return 1;
     if (want == 7 && L.H == 64) {
@@ -2460,7 +2229,7 @@ int pick_rollout(const AgentLayout& L, const MlgEnvSpec& spec, RolloutLds2* lay)
         if (lay->total * 4 <= LDS_LIMIT_BYTES) return 7;
         *lay = make_rollout_lds2(L, spec.U, spec.n_agents, 16);
     }
-    return (want == 4 || want == 5) ? want : 2;
+    return 2;
 }
 
 }  // namespace
@@ -2633,10 +2402,7 @@ extern "C" int mlg_rollout(const MlgEnvSpec* spec, MlgEnvState* st, const MlgAge
         int rc = 0;
 #define MLG_V(VV) rc = h64 ? launch_rollout_v2<64, VV>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2) \
                            : launch_rollout_v2<32, VV>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2)
-        if (variant == 4) MLG_V(4);
-        else if (variant == 5) MLG_V(5);
-        else if (variant == 6) MLG_V(6);
-        else if (variant == 7) rc = launch_rollout_v2<64, 7>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
+        if (variant == 7) rc = launch_rollout_v2<64, 7>(s, *spec, *st, L, packed, *batch, *info, eps, test_mode, lay2);
         else MLG_V(2);
 #undef MLG_V
         if (rc) return rc;

@@ -338,7 +338,7 @@ def test_stepper_summary_ring_runahead_matches_resolved(device):
             assert torch.equal(x[k], y[k]), (i, k)
 
 
-@pytest.mark.parametrize("kernel", ["v7", "v6", "v5", "v4", "v2", "v1"])
+@pytest.mark.parametrize("kernel", ["v7", "v2", "v1"])
 def test_rollout_ring_mode_zero_copy_insert(device, kernel, monkeypatch):
     """Train-mode rollouts written straight into the replay ring (full-write mode, wrap-around, garbage in the
     slots beforehand) equal the ordinary zero-initialised EpisodeBatch bit for bit, and the buffer indices
@@ -380,7 +380,7 @@ def test_rollout_ring_mode_zero_copy_insert(device, kernel, monkeypatch):
         assert torch.equal(ring[k][:n], ref[k][:n]), k
 
 
-@pytest.mark.parametrize("kernel", ["v2", "v4", "v5", "v6"])
+@pytest.mark.parametrize("kernel", ["v2"])
 @pytest.mark.parametrize("plan", ["medium_1h_4t", "small", "medium_1h_2t_2a", "medium"])
 def test_rollout_v2_equals_v1(device, plan, kernel, monkeypatch):
     """The chunk-split, compacted headline kernel (v2) and the generic per-tile kernel (v1) compute in the same
