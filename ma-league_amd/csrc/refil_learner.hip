@@ -156,7 +156,7 @@ Plan make_plan(const MlgRefilLearnerCfg* cfg, int T1) {
     w.dq = take(T * Ron);
     w.d2 = take(T * Ron * c.A);
     w.part = take(I * 8);
-    w.msum = take(4);
+    w.msum = take(4 + c.B);  // [mask sum, max_t_filled, -, -, live mixer items of episode b ...]
     w.dgi = take(T * Ron * 3 * EMB);
     w.dgh = take(T * Ron * 3 * EMB);
     w.dfc2 = take(T * Ron * EMB);
@@ -442,9 +442,29 @@ __device__ void mask_sum_body(const MlgEntityBatch& bt, int B, int T, float* __r
         msum[0] = red[0];
         msum[1] = (float)Te;
     }
+    // msum[4 + b]: the episode's live mixer items = 1 + the last t < Te - 1 with mask(b, t) != 0 (0: none). Every item
+    // t >= it has mask 0 (its loss, its deltas and every gradient through it are exactly zero), so the per-item kernels
+    // skip items t >= mix_len (mixer, agent backward) and t > mix_len (agent forward: Q at mix_len is the last step's
+    // target): at the bench's sampled batches (max_t_filled 101, episodes ~47 steps) about half of all items.
+    for (int b = wave; b < B; b += nw) {
+        const int64_t base = eslot(bt, b) * bt.T1;
+        int last = -1;
+        for (int t0 = 0; t0 < Te - 1; t0 += 64) {
+            const int t = t0 + lane;
+            bool live = false;
+            if (t < Te - 1) {
+                live = bt.filled[base + t] != 0 && (t == 0 || bt.terminated[base + t - 1] == 0);
+            }
+            const uint64_t m = __ballot(live);
+            if (m) last = t0 + 63 - __builtin_clzll(m);
+        }
+        if (lane == 0) msum[4 + b] = (float)(last + 1);
+    }
 }
 
 __device__ __forceinline__ int t_eff(const float* msum) { return (int)msum[1]; }
+// live mixer items of episode b (mask(b, t) == 0 for every t >= it; see mask_sum_body)
+__device__ __forceinline__ int mix_len(const float* msum, int b) { return (int)msum[4 + b]; }
 
 // entity inputs ein[i][j][c] (K1 columns, zero padded)
 __device__ void ein_body(const RCfg& c, const MlgEntityBatch& bt, float* __restrict__ ein, int bx) {
@@ -570,12 +590,26 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c_arg, MlgEntityBatch 
     const int R = online ? c.Ron : c.Rtg;
     const int i0 = blockIdx.x * 2;
     const int Te = t_eff(msum);
-    const bool v0 = i0 < c.I && i0 % c.T < Te, v1 = i0 + 1 < c.I && (i0 + 1) % c.T < Te;
-    if (!v0 && !v1) return;  // both items past max_t_filled
+    // live items: t < max_t_filled and t <= the episode's live mixer items (the Q of step mix_len is the target of
+    // the last live mixer item); the others only zero their GRU inputs (finite, deterministic recurrence there)
+    auto live = [&](int i) { return i < c.I && i % c.T < Te && i % c.T <= mix_len(msum, i / c.T); };
+    const bool v0 = live(i0), v1 = live(i0 + 1);
+    if (!v0 && !v1) {
+        for (int e = 0; e < 2; ++e) {
+            const int i = i0 + e;
+            if (i >= c.I || i % c.T >= Te) continue;
+            const int b = i / c.T, t = i % c.T;
+            for (int cc = 0; cc < ncopy; ++cc) {
+                float* gi = A.gi + ((int64_t)t * R + ((int64_t)cc * c.B + b) * c.NA) * 3 * EMB;
+                for (int q = lane; q < c.NA * 3 * EMB; q += 64) gi[q] = 0.f;
+            }
+        }
+        return;
+    }
     for (int k = lane; k < 3 * 16 * LDX; k += 64) (&s_o[0][0])[k] = 0.f;
     if (lane < 32) {
         const int e = lane >> 4, q = lane & 15, i = i0 + e;
-        if (i < c.I && i % c.T < Te) {
+        if (live(i)) {
             const int b = i / c.T, t = i % c.T;
             const uint32_t om = om_row(c, bt, b, t, q);
             s_m[0][e][q] = om;
@@ -595,7 +629,7 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c_arg, MlgEntityBatch 
     wave_sync();
     for (int e = 0; e < 2; ++e) {
         const int i = i0 + e;
-        if (i >= c.I || i % c.T >= Te) continue;
+        if (!live(i)) continue;
         for (int k = lane; k < NE * c.K1; k += 64) s_ein[(k / c.K1) * LDI + k % c.K1] = ein[(int64_t)i * NE * c.K1 + k];
         wave_sync();
         dense_lds<true>(A.P + L.w1, L.K1, A.P + L.b1, EMB / 16, s_ein, LDI, L.K1 / 16, s_x1, LDX, lane);
@@ -618,8 +652,10 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c_arg, MlgEntityBatch 
     }
     const int col = lane & 15, g = lane >> 4;
     const int e = col >> 3, n = col & 7, i = i0 + e;
-    const bool valid = i < c.I && n < c.NA && i % c.T < Te;
-    const int b = valid ? i / c.T : 0, t = valid ? i % c.T : 0;
+    const bool valid = n < c.NA && live(i);
+    // rows of a skipped item of the pair (t < max_t_filled, past the episode's live items): GRU inputs zeroed
+    const bool zrow = !valid && n < c.NA && i < c.I && i % c.T < Te;
+    const int b = (valid || zrow) ? i / c.T : 0, t = (valid || zrow) ? i % c.T : 0;
     const uint32_t dead = s_dead[0] | (s_dead[1] << 8);
     const bool rdead = (dead >> col) & 1u;
     for (int cc = 0; cc < ncopy; ++cc) {
@@ -650,10 +686,11 @@ __global__ void __launch_bounds__(64) ent_fwd_kernel(RCfg c_arg, MlgEntityBatch 
             floatx4 acc[4];
             bias_init<4>(acc, q < 2 ? A.P + L.brz + q * EMB : A.P + L.bih + 2 * EMB, 0, lane);
             mm_reg<4, 4>(acc, A.P + L.wih + (int64_t)q * EMB * EMB, EMB, 0, x3, lane);
-            if (valid) {
+            if (valid || zrow) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    *reinterpret_cast<floatx4*>(A.gi + ro * 3 * EMB + q * EMB + k * 16 + 4 * g) = acc[k];
+                    *reinterpret_cast<floatx4*>(A.gi + ro * 3 * EMB + q * EMB + k * 16 + 4 * g) =
+                        valid ? acc[k] : floatx4{0.f, 0.f, 0.f, 0.f};
             }
         }
     }
@@ -828,7 +865,7 @@ __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c_arg, MlgEntityBatc
     const int lane = threadIdx.x;
     const int i = blockIdx.x, k = blockIdx.y & 3, net = blockIdx.y >> 2;
     const int b = i / c.T, t = i % c.T;
-    if (t >= t_eff(msum) - 1) {  // no (unmasked) mixer item: zero the wgrad inputs of the online item
+    if (t >= t_eff(msum) - 1 || t >= mix_len(msum, b)) {  // masked mixer item: zero the wgrad inputs of the online item
         if (!net) {
             for (int q = lane; q < NE * EMB; q += 64) hp.x1m[k][(int64_t)i * NE * EMB + q] = 0.f;
             for (int v = 0; v < nvar(k); ++v)
@@ -957,7 +994,7 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c_arg, MlgEntityBatch b
     const int e = lane & 31;
     const int NA = c.NA;
     float* part = io.part + (int64_t)i * 8;
-    if (t >= Te - 1) {  // t = T - 1, or past max_t_filled (mask 0): no loss, zero deltas
+    if (t >= Te - 1 || t >= mix_len(io.msum, b)) {  // t = T - 1, past max_t_filled or the episode (mask 0): zero deltas
         if (lane < 8) part[lane] = 0.f;
         // dQ / d2 rows of the item's (copy, agent) rows: zeros (the item owns them; no memset pass)
         for (int q = lane; q < 3 * c.NA * (c.A + 1); q += 64) {
@@ -1195,7 +1232,7 @@ __global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c_arg, MlgEntityBatc
     const int b = i / c.T, t = i % c.T;
     const int V = nvar(k);
     const int col = lane & 15, g = lane >> 4;
-    if (t >= t_eff(msum) - 1) {
+    if (t >= t_eff(msum) - 1 || t >= mix_len(msum, b)) {
         for (int q = lane; q < V * NAS * EMB; q += 64) {
             const int v = q / (NAS * EMB), rem = q % (NAS * EMB);
             hb.doutm[k][((int64_t)v * c.I + i) * NAS * EMB + rem] = 0.f;
@@ -1402,13 +1439,16 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
     }
     wave_sync();
     const int Te = t_eff(msum);
+    // items with nonzero deltas: t < max_t_filled and t < the episode's live mixer items (every later item's dQ and
+    // recurrent delta are exactly zero); the others write zero deltas, no math
+    auto live = [&](int ii) { return ii < c.I && ii % c.T < Te && ii % c.T < mix_len(msum, ii / c.T); };
     const int e = col >> 3, n = col & 7, i = i0 + e;
     const bool row_ok = i < c.I && n < c.NA;
-    const bool valid = row_ok && i % c.T < Te;  // items past max_t_filled: zero deltas, no math
+    const bool valid = row_ok && live(i);
     const int b = row_ok ? i / c.T : 0, t = row_ok ? i % c.T : 0;
     const uint32_t dead = s_dead[0] | (s_dead[1] << 8);
     const bool rdead = (dead >> col) & 1u;
-    const bool any = (i0 < c.I && i0 % c.T < Te) || (i0 + 1 < c.I && (i0 + 1) % c.T < Te);
+    const bool any = live(i0) || live(i0 + 1);
     for (int cc = 0; cc < 3; ++cc) {
         const int64_t ro = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * c.NA + n;
         if (!any) {
@@ -1454,7 +1494,7 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
     for (int ee = 0; ee < 2; ++ee) {
         const int ii = i0 + ee;
         if (ii >= c.I) continue;
-        if (ii % c.T >= Te) {  // past max_t_filled: zero deltas
+        if (!live(ii)) {  // past max_t_filled or the episode: zero deltas
             for (int q = lane; q < NE * 3 * EMB; q += 64) eb.dqkv[(int64_t)ii * NE * 3 * EMB + q] = 0.f;
             for (int q = lane; q < NE * EMB; q += 64) eb.dfc1[(int64_t)ii * NE * EMB + q] = 0.f;
             continue;
