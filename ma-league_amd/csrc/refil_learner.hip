@@ -1583,23 +1583,33 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     const int I16 = c.I * NE, TR = c.T * c.Ron;
     RJobs J;
     J.n = 0;
-    J.j[J.n++] = mlg::bjob(at(p.w.dfc1), EMB, at(p.w.ein), c.K1, gp(a.c_w1), gp(a.c_b1), EMB, c.D0, I16);
-    J.j[J.n++] = mlg::bjob(at(p.w.dqkv), 3 * EMB, at(p.w.x1), EMB, gp(a.c_win), nullptr, 3 * EMB, EMB, I16);
-    J.j[J.n++] = mlg::bjob(at(p.w.dout), EMB, at(p.w.o), EMB, gp(a.c_wout), gp(a.c_bout), EMB, EMB, TR);
-    J.j[J.n++] = mlg::bjob(at(p.w.dfc2), EMB, at(p.w.x2), EMB, gp(a.c_w2), gp(a.c_b2), EMB, EMB, TR);
-    J.j[J.n++] = mlg::bjob(at(p.w.dgi), 3 * EMB, at(p.w.x3), EMB, gp(a.c_wih), gp(a.c_bih), 3 * EMB, EMB, TR);
-    J.j[J.n++] = mlg::bjob(at(p.w.dgh), 3 * EMB, at(p.w.hs_on), EMB, gp(a.c_whh), gp(a.c_bhh), 3 * EMB, EMB, TR);
-    J.j[J.n++] = mlg::bjob(at(p.w.d2), c.A, ws ? ws + p.w.hs_on + (int64_t)c.Ron * EMB : nullptr, EMB, gp(a.c_w3),
-                          gp(a.c_b3), c.A, EMB, TR);
+    // rows of items / steps past each episode's live mixer items carry exactly zero deltas (the backward kernels'
+    // zero paths): every job skips them (mix_len at msum + 4, mask_sum_body)
+    static const bool noskip = getenv("MLG_WGRAD_NOSKIP") != nullptr;  // A/B
+    const float* ml = ws ? ws + p.w.msum + 4 : nullptr;
+    auto items = [&](mlg::BJob j, int rpi) { return noskip ? j : mlg::bjob_items(j, ml, rpi, c.I, c.T); };
+    // t-major rows: 8-row groups share one episode only when NA is a multiple of 8 (refil_8); otherwise no skipping
+    auto steps = [&](mlg::BJob j) { return c.NA % 8 == 0 && !noskip ? mlg::bjob_steps(j, ml, c.Ron, c.NA, c.B) : j; };
+    J.j[J.n++] = items(mlg::bjob(at(p.w.dfc1), EMB, at(p.w.ein), c.K1, gp(a.c_w1), gp(a.c_b1), EMB, c.D0, I16), NE);
+    J.j[J.n++] = items(mlg::bjob(at(p.w.dqkv), 3 * EMB, at(p.w.x1), EMB, gp(a.c_win), nullptr, 3 * EMB, EMB, I16), NE);
+    J.j[J.n++] = steps(mlg::bjob(at(p.w.dout), EMB, at(p.w.o), EMB, gp(a.c_wout), gp(a.c_bout), EMB, EMB, TR));
+    J.j[J.n++] = steps(mlg::bjob(at(p.w.dfc2), EMB, at(p.w.x2), EMB, gp(a.c_w2), gp(a.c_b2), EMB, EMB, TR));
+    J.j[J.n++] = steps(mlg::bjob(at(p.w.dgi), 3 * EMB, at(p.w.x3), EMB, gp(a.c_wih), gp(a.c_bih), 3 * EMB, EMB, TR));
+    J.j[J.n++] = steps(mlg::bjob(at(p.w.dgh), 3 * EMB, at(p.w.hs_on), EMB, gp(a.c_whh), gp(a.c_bhh), 3 * EMB, EMB, TR));
+    J.j[J.n++] = steps(mlg::bjob(at(p.w.d2), c.A, ws ? ws + p.w.hs_on + (int64_t)c.Ron * EMB : nullptr, EMB,
+                                 gp(a.c_w3), gp(a.c_b3), c.A, EMB, TR));
     for (int k = 0; k < 4; ++k) {
         const RHyper& h = p.Lh;
         const int64_t G0 = p.n_agent + (int64_t)k * h.c_total;
         const int rows = nvar(k) * c.I * NAS;
-        J.j[J.n++] = mlg::bjob(at(p.w.dfc1m[k]), EMB, at(p.w.ein), c.K1, gp(G0 + h.c_w1), gp(G0 + h.c_b1), EMB, c.D0, I16);
-        J.j[J.n++] = mlg::bjob(at(p.w.dqkvm[k]), 3 * EMB, at(p.w.x1m[k]), EMB, gp(G0 + h.c_win), nullptr, 3 * EMB, EMB, I16);
-        J.j[J.n++] = mlg::bjob(at(p.w.doutm[k]), EMB, at(p.w.om[k]), EMB, gp(G0 + h.c_wout), gp(G0 + h.c_bout), EMB, EMB,
-                              rows);
-        J.j[J.n++] = mlg::bjob(at(p.w.dX[k]), EM, at(p.w.x2m[k]), EMB, gp(G0 + h.c_w2), gp(G0 + h.c_b2), EM, EMB, rows);
+        J.j[J.n++] = items(mlg::bjob(at(p.w.dfc1m[k]), EMB, at(p.w.ein), c.K1, gp(G0 + h.c_w1), gp(G0 + h.c_b1), EMB, c.D0,
+                                     I16), NE);
+        J.j[J.n++] = items(mlg::bjob(at(p.w.dqkvm[k]), 3 * EMB, at(p.w.x1m[k]), EMB, gp(G0 + h.c_win), nullptr, 3 * EMB,
+                                     EMB, I16), NE);
+        J.j[J.n++] = items(mlg::bjob(at(p.w.doutm[k]), EMB, at(p.w.om[k]), EMB, gp(G0 + h.c_wout), gp(G0 + h.c_bout), EMB,
+                                     EMB, rows), NAS);
+        J.j[J.n++] = items(mlg::bjob(at(p.w.dX[k]), EM, at(p.w.x2m[k]), EMB, gp(G0 + h.c_w2), gp(G0 + h.c_b2), EM, EMB,
+                                     rows), NAS);
     }
     int64_t slab_part;
     *slab_floats = mlg::layout_bjobs(J, n_tasks, n_red, &slab_part);

@@ -182,6 +182,12 @@ struct BJob {
     int va, vb;  // delta / x rows readable as 16-byte vectors (ld % 4 == 0, 16-byte aligned base)
     int task0;
     int64_t slab0;
+    // rows with an exactly zero delta skipped (REFIL learner: items past each sampled episode's live steps, whose
+    // deltas the backward kernels write as zeros): 0 off; 1 item-major rows, item = (row / rpi) % I, (b, t) = (item / T,
+    // item % T); 2 t-major rows, t = row / R, b = ((row % R) / NA) % B. Row r is live iff t < mlen[b]. Groups of 8
+    // consecutive rows share one (b, t) (rpi, NA and R multiples of 8).
+    int skip, rpi, I, T, R, NA, B;
+    const float* mlen;
 };
 template <int MJ>
 struct BJobsT {
@@ -221,7 +227,43 @@ inline BJob bjob(const float* delta, int64_t ldd, const float* x, int64_t ldx, f
     j.chunks = (rows + j.ch_rows - 1) / j.ch_rows;
     j.task0 = 0;
     j.slab0 = 0;
+    j.skip = 0;
+    j.rpi = j.I = j.T = j.R = j.NA = j.B = 1;
+    j.mlen = nullptr;
     return j;
+}
+
+// skip rows with zero deltas (see BJob::skip); item-major rows of rpi rows per item over I items of T steps
+inline BJob bjob_items(BJob j, const float* mlen, int rpi, int I, int T) {
+    j.skip = 1;
+    j.mlen = mlen;
+    j.rpi = rpi;
+    j.I = I;
+    j.T = T;
+    return j;
+}
+// t-major rows: R rows per step, row r of a step belongs to episode (r / NA) % B
+inline BJob bjob_steps(BJob j, const float* mlen, int R, int NA, int B) {
+    j.skip = 2;
+    j.mlen = mlen;
+    j.R = R;
+    j.NA = NA;
+    j.B = B;
+    return j;
+}
+
+__device__ __forceinline__ bool bjob_row_live(const BJob& jb, int row) {
+    if (!jb.skip) return true;
+    int b, t;
+    if (jb.skip == 1) {
+        const int item = (row / jb.rpi) % jb.I;
+        b = item / jb.T;
+        t = item % jb.T;
+    } else {
+        t = row / jb.R;
+        b = ((row % jb.R) / jb.NA) % jb.B;
+    }
+    return t < (int)jb.mlen[b];
 }
 
 template <int MJ>
@@ -263,11 +305,18 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
     // rr + 8g + t, so tile i's A operand is element i of the 8 delta vectors and tile j's B operand element j of
     // the 8 x vectors. Same D layout (and output permutation) as the f32 form below.
     for (int rr = r0; rr < r1; rr += 32) {
+        // rows with zero deltas add exactly zero: a lane's 8-row group of them loads nothing (zeros), a step with no
+        // live group is skipped
+        bool glive = rr + 8 * g < r1;
+        if (jb.skip) {
+            glive = glive && bjob_row_live(jb, rr + 8 * g);
+            if (__ballot(glive) == 0) continue;
+        }
         float a[8][4], b[8][4];
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int row = rr + 8 * g + t;
-            const bool rv = row < r1;
+            const bool rv = glive && row < r1;
             const float* dr = jb.delta + (int64_t)row * jb.ldd + m0;
             const float* xr = jb.x + (int64_t)row * jb.ldx + k0;
             if (rv && va) {
