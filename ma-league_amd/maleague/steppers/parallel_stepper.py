@@ -36,18 +36,33 @@ def _same_device(a, b) -> bool:
 
 class EnvInfos(Sequence):
     """The per-run list of env_info dicts (``{"battle_won": [home, away], "draw": bool}``) in order of
-    termination, materialised on access (a plain list of 4096 dicts per run costs milliseconds of host time)."""
+    termination (parallel_stepper.py:124,183-184: by episode length, then env index), materialised on access: a plain
+    list of 4096 dicts per run costs milliseconds of host time, and the ordering itself is computed on first access."""
 
-    def __init__(self, won, draw):
-        self.won, self.draw = won, draw
+    def __init__(self, won, draw, ep_len):
+        self._won, self._draw, self._len, self._order = won, draw, ep_len, None
+
+    def _o(self):
+        if self._order is None:
+            self._order = np.lexsort((np.arange(len(self._len)), self._len))
+        return self._order
+
+    @property
+    def won(self):
+        return self._won[self._o()]
+
+    @property
+    def draw(self):
+        return self._draw[self._o()]
 
     def __len__(self):
-        return len(self.draw)
+        return len(self._draw)
 
     def __getitem__(self, i):
         if isinstance(i, slice):
             return [self[k] for k in range(*i.indices(len(self)))]
-        return {"battle_won": [bool(self.won[i, 0]), bool(self.won[i, 1])], "draw": bool(self.draw[i])}
+        k = self._o()[i]
+        return {"battle_won": [bool(self._won[k, 0]), bool(self._won[k, 1])], "draw": bool(self._draw[k])}
 
 
 class LazyEnvInfos(Sequence):
@@ -253,26 +268,27 @@ class ParallelStepper(EnvStepper):
         mode_now = self.logger.test_mode
         for run_id, host, t_max, t_env, test_mode in self._post:
             self.logger.test_mode = test_mode  # the run's mode (its summary may resolve after a later run())
-            ep_len = host[0:B]
-            won = host[B:3 * B].reshape(B, 2).astype(bool)
-            draw = host[3 * B:4 * B].astype(bool)
+            ep_len = host[0:B]  # host is this run's own copy of the summary ring slot (_resolve_one)
+            won = host[B:3 * B].reshape(B, 2) != 0
+            draw = host[3 * B:4 * B] != 0
             ret = host[4 * B:5 * B].view(np.float32)
             ret_away = host[5 * B:6 * B].view(np.float32)
-            # env_infos in order of termination (parallel_stepper.py:124,183-184): by episode length, then index
-            order = np.lexsort((np.arange(B), ep_len))
-            infos = EnvInfos(won[order], draw[order])
-            last = {"ep_len": torch.from_numpy(ep_len.copy()), "returns": torch.from_numpy(ret.copy()), "order": order}
+            # env_infos in order of termination (EnvInfos: ordered on first access)
+            infos = EnvInfos(won, draw, ep_len)
+            last = {"ep_len": torch.from_numpy(ep_len), "returns": torch.from_numpy(ret)}
             if self.away_mac is not None:
-                last["away_returns"] = torch.from_numpy(ret_away.copy())
+                last["away_returns"] = torch.from_numpy(ret_away)
             self._runs[run_id] = (last, infos)
             self._runs.pop(run_id - 2, None)
-            self.logger.collect(Collectibles.RETURN, ret.astype(np.float64), origin=Originator.HOME, parallel=True)
+            # the per-run arrays go to the logger as arrays (listed at log time); float32 returns list as the same
+            # Python floats as their float64 copies. The won / draw ratios are order-free integer sums, so they are
+            # collected in env order rather than termination order.
+            self.logger.collect(Collectibles.RETURN, ret, origin=Originator.HOME, parallel=True)
             if self.away_mac is not None:
-                self.logger.collect(Collectibles.RETURN, ret_away.astype(np.float64), origin=Originator.AWAY,
-                                    parallel=True)
-            self.logger.collect(Collectibles.WON, won[order, 0], origin=Originator.HOME, parallel=True)
-            self.logger.collect(Collectibles.WON, won[order, 1], origin=Originator.AWAY, parallel=True)
-            self.logger.collect(Collectibles.DRAW, draw[order], parallel=True)
+                self.logger.collect(Collectibles.RETURN, ret_away, origin=Originator.AWAY, parallel=True)
+            self.logger.collect(Collectibles.WON, won[:, 0], origin=Originator.HOME, parallel=True)
+            self.logger.collect(Collectibles.WON, won[:, 1], origin=Originator.AWAY, parallel=True)
+            self.logger.collect(Collectibles.DRAW, draw, parallel=True)
             self.logger.collect(Collectibles.STEPS, t_max, parallel=True)
             self.logger.log(t_env)
         self.logger.test_mode = mode_now

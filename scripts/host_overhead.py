@@ -30,9 +30,22 @@ def it():  # one iteration of MultiAgentExperiment.start's loop, as bench.py run
     ep[0] = exp._iteration(ep[0])
 
 
+# time the host spends blocked on the summary ring (Event.synchronize: the GPU is behind) is not host work
+_wait = [0.0]
+_sync = torch.cuda.Event.synchronize
+
+
+def _timed_sync(self):
+    w0 = time.perf_counter()
+    _sync(self)
+    _wait[0] += time.perf_counter() - w0
+
+
+torch.cuda.Event.synchronize = _timed_sync
 for i in range(5):
     it()
 torch.cuda.synchronize()
+_wait[0] = 0.0
 host = []
 t0 = time.perf_counter()
 for i in range(20):
@@ -45,6 +58,8 @@ t_all = time.perf_counter() - t0
 host.sort()
 print(f"host per iteration: median {host[10] * 1e3:.3f} ms, max {host[-1] * 1e3:.3f} ms; host loop {t_host / 20 * 1e3:.3f} "
       f"ms/it; wall incl. GPU {t_all / 20 * 1e3:.3f} ms/it")
+print(f"host WORK per iteration (host loop minus the waits on the summary ring): "
+      f"{(t_host - _wait[0]) / 20 * 1e3:.3f} ms/it (waits {_wait[0] / 20 * 1e3:.3f} ms/it)")
 
 if os.environ.get("PROFILE"):
     import cProfile
