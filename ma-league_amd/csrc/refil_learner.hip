@@ -865,17 +865,9 @@ __global__ void __launch_bounds__(64) hyper_fwd_kernel(RCfg c_arg, MlgEntityBatc
     const int lane = threadIdx.x;
     const int i = blockIdx.x, k = blockIdx.y & 3, net = blockIdx.y >> 2;
     const int b = i / c.T, t = i % c.T;
-    if (t >= t_eff(msum) - 1 || t >= mix_len(msum, b)) {  // masked mixer item: zero the wgrad inputs of the online item
-        if (!net) {
-            for (int q = lane; q < NE * EMB; q += 64) hp.x1m[k][(int64_t)i * NE * EMB + q] = 0.f;
-            for (int v = 0; v < nvar(k); ++v)
-                for (int q = lane; q < NAS * EMB; q += 64) {
-                    hp.om[k][((int64_t)v * c.I + i) * NAS * EMB + q] = 0.f;
-                    hp.x2m[k][((int64_t)v * c.I + i) * NAS * EMB + q] = 0.f;
-                }
-        }
-        return;
-    }
+    // masked mixer item: nothing to compute, and nothing to write -- the wgrad jobs skip its rows (wgrad_device.h
+    // bjob_items) and no other kernel reads its activations
+    if (t >= t_eff(msum) - 1 || t >= mix_len(msum, b)) return;
     const int ts = net ? t + 1 : t;
     const int ie = b * c.T + ts;
     const float* P = net ? hp.Ptg[k] : hp.Pon[k];
@@ -997,15 +989,15 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c_arg, MlgEntityBatch b
     if (t >= Te - 1 || t >= mix_len(io.msum, b)) {  // t = T - 1, past max_t_filled or the episode (mask 0): zero deltas
         if (lane < 8) part[lane] = 0.f;
         // dQ / d2 rows of the item's (copy, agent) rows: zeros (the item owns them; no memset pass)
+        // dQ rows feed the reverse recurrence at every step; the d2 rows only the fc3 wgrad job, which skips them when
+        // NA is a multiple of 8 (bjob_steps); dX rows only hyper_bwd and wgrad, which both skip the item
+        const bool d2z = c.NA % 8 != 0;
         for (int q = lane; q < 3 * c.NA * (c.A + 1); q += 64) {
             const int cc = q / (c.NA * (c.A + 1)), rem = q % (c.NA * (c.A + 1)), n = rem / (c.A + 1), a2 = rem % (c.A + 1);
             const int64_t row = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * c.NA + n;
             if (a2 == c.A) io.dq[row] = 0.f;
-            else io.d2[row * c.A + a2] = 0.f;
+            else if (d2z) io.d2[row * c.A + a2] = 0.f;
         }
-        for (int k = 0; k < 4; ++k)
-            for (int v = 0; v < nvar(k); ++v)
-                for (int q = lane; q < NAS * EM; q += 64) io.dX[k][((int64_t)v * c.I + i) * NAS * EM + q] = 0.f;
         return;
     }
     // Every global load of the item is issued before the first one is consumed: one wave per item, so the kernel
@@ -1232,15 +1224,8 @@ __global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c_arg, MlgEntityBatc
     const int b = i / c.T, t = i % c.T;
     const int V = nvar(k);
     const int col = lane & 15, g = lane >> 4;
-    if (t >= t_eff(msum) - 1 || t >= mix_len(msum, b)) {
-        for (int q = lane; q < V * NAS * EMB; q += 64) {
-            const int v = q / (NAS * EMB), rem = q % (NAS * EMB);
-            hb.doutm[k][((int64_t)v * c.I + i) * NAS * EMB + rem] = 0.f;
-        }
-        for (int q = lane; q < NE * 3 * EMB; q += 64) hb.dqkvm[k][(int64_t)i * NE * 3 * EMB + q] = 0.f;
-        for (int q = lane; q < NE * EMB; q += 64) hb.dfc1m[k][(int64_t)i * NE * EMB + q] = 0.f;
-        return;
-    }
+    // masked mixer item: its deltas are zero and only the wgrad jobs read them, which skip its rows
+    if (t >= t_eff(msum) - 1 || t >= mix_len(msum, b)) return;
     const uint32_t dead = dead_bits(c, em_bits(c, bt, b, t));
     for (int q = lane; q < NE * 3 * EMB; q += 64)
         s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = hb.qkvm[k][(int64_t)i * NE * 3 * EMB + q];
@@ -1452,7 +1437,7 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
     for (int cc = 0; cc < 3; ++cc) {
         const int64_t ro = (int64_t)t * c.Ron + ((int64_t)cc * c.B + b) * c.NA + n;
         if (!any) {
-            if (row_ok) {
+            if (row_ok && c.NA % 8 != 0) {  // t-major rows the wgrad jobs cannot skip (bjob_steps needs NA % 8 == 0)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     *reinterpret_cast<floatx4*>(eb.dfc2 + ro * EMB + q * 16 + 4 * g) = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1494,11 +1479,7 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
     for (int ee = 0; ee < 2; ++ee) {
         const int ii = i0 + ee;
         if (ii >= c.I) continue;
-        if (!live(ii)) {  // past max_t_filled or the episode: zero deltas
-            for (int q = lane; q < NE * 3 * EMB; q += 64) eb.dqkv[(int64_t)ii * NE * 3 * EMB + q] = 0.f;
-            for (int q = lane; q < NE * EMB; q += 64) eb.dfc1[(int64_t)ii * NE * EMB + q] = 0.f;
-            continue;
-        }
+        if (!live(ii)) continue;  // past max_t_filled or the episode: zero deltas, skipped by the wgrad jobs
         for (int q = lane; q < NE * 3 * EMB; q += 64)
             s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = eb.qkv[(int64_t)ii * NE * 3 * EMB + q];
         wave_sync();
@@ -1585,11 +1566,11 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     J.n = 0;
     // rows of items / steps past each episode's live mixer items carry exactly zero deltas (the backward kernels'
     // zero paths): every job skips them (mix_len at msum + 4, mask_sum_body)
-    static const bool noskip = getenv("MLG_WGRAD_NOSKIP") != nullptr;  // A/B
     const float* ml = ws ? ws + p.w.msum + 4 : nullptr;
-    auto items = [&](mlg::BJob j, int rpi) { return noskip ? j : mlg::bjob_items(j, ml, rpi, c.I, c.T); };
+    // (not optional: the kernels above no longer write the skipped rows)
+    auto items = [&](mlg::BJob j, int rpi) { return mlg::bjob_items(j, ml, rpi, c.I, c.T); };
     // t-major rows: 8-row groups share one episode only when NA is a multiple of 8 (refil_8); otherwise no skipping
-    auto steps = [&](mlg::BJob j) { return c.NA % 8 == 0 && !noskip ? mlg::bjob_steps(j, ml, c.Ron, c.NA, c.B) : j; };
+    auto steps = [&](mlg::BJob j) { return c.NA % 8 == 0 ? mlg::bjob_steps(j, ml, c.Ron, c.NA, c.B) : j; };
     J.j[J.n++] = items(mlg::bjob(at(p.w.dfc1), EMB, at(p.w.ein), c.K1, gp(a.c_w1), gp(a.c_b1), EMB, c.D0, I16), NE);
     J.j[J.n++] = items(mlg::bjob(at(p.w.dqkv), 3 * EMB, at(p.w.x1), EMB, gp(a.c_win), nullptr, 3 * EMB, EMB, I16), NE);
     J.j[J.n++] = steps(mlg::bjob(at(p.w.dout), EMB, at(p.w.o), EMB, gp(a.c_wout), gp(a.c_bout), EMB, EMB, TR));
