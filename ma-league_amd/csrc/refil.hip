@@ -29,13 +29,13 @@ using namespace refil;
 #endif
 
 #ifdef MLG_STAMPS
-// Diagnostic build only: per-wave cycle counts of the REFIL rollout phases, g_refil_stamps[block][16]
-// (slots 0..13 phases, 14 total, 15 = 1).
+// Diagnostic build only: per-wave cycle counts of the REFIL rollout phases, g_refil_stamps[wave][32]
+// (slots 0..29 phases, 30 total, 31 = 1).
 __device__ unsigned long long* g_refil_stamps = nullptr;
 struct RStamps {
-    unsigned long long acc[14], last, begin;
+    unsigned long long acc[30], last, begin;
     __device__ void init() {
-        for (int k = 0; k < 14; ++k) acc[k] = 0;
+        for (int k = 0; k < 30; ++k) acc[k] = 0;
         last = begin = __builtin_amdgcn_s_memtime();
     }
     __device__ void mark(int k) {
@@ -43,18 +43,27 @@ struct RStamps {
         acc[k] += now - last;
         last = now;
     }
+    // steps by kind: k = 0 both pairs running, 1 one pair; cycles in slot 9 + k, step counts in slot 11 + k
+    unsigned long long s0;
+    __device__ void step_begin() { s0 = __builtin_amdgcn_s_memtime(); }
+    __device__ void step_end(int k) {
+        acc[9 + k] += __builtin_amdgcn_s_memtime() - s0;
+        acc[11 + k] += 1;
+    }
     __device__ void flush() {
         if ((threadIdx.x & 63) || !g_refil_stamps) return;
-        unsigned long long* o = g_refil_stamps + ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
-        for (int k = 0; k < 14; ++k) o[k] = acc[k];
-        o[14] = __builtin_amdgcn_s_memtime() - begin;
-        o[15] = 1;
+        unsigned long long* o = g_refil_stamps + ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32;
+        for (int k = 0; k < 30; ++k) o[k] = acc[k];
+        o[30] = __builtin_amdgcn_s_memtime() - begin;
+        o[31] = 1;
     }
 };
 #else
 struct RStamps {
     __device__ void init() {}
     __device__ void mark(int) {}
+    __device__ void step_begin() {}
+    __device__ void step_end(int) {}
     __device__ void flush() {}
 };
 #endif
