@@ -8,6 +8,11 @@ mkdir -p gpurun_out
 T="python -u -m pytest -x -q ${PYTEST_ARGS:-} --timeout 200 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 700 $T ${TESTS:-tests -m gpu} > gpurun_out/tests.log 2>&1 || { tail -40 gpurun_out/tests.log; exit 1; }
 tail -2 gpurun_out/tests.log
+if [ -n "$SMOKE" ]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+      || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
+  tail -3 gpurun_out/smoke.log
+fi
 if [ -z "$NO_BENCH" ]; then
   timeout -k 10 400 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err \
       || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
@@ -22,7 +27,7 @@ if [ -n "$TRACE" ]; then
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/trace_$m" -o run \
         -- python3 bench.py --mode $m --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/trace_$m.json 2> gpurun_out/trace_$m.err \
         || { echo "trace $m failed"; tail -20 gpurun_out/trace_$m.err; exit 1; }
-    key=$( [ $m = ai ] && echo rollout_v2_kernel || ( [ $m = league ] && echo rollout_sp7 || echo refil_rollout ) )
+    key=$( [ $m = ai ] && echo rollout_v2_kernel || ( [ $m = league ] && echo rollout_sp || echo refil_rollout ) )
     python3 scripts/trace_iter.py gpurun_out/trace_$m/run_kernel_trace.csv $key 6 > gpurun_out/trace_$m.txt || exit 1
     head -${TRACE_LINES:-24} gpurun_out/trace_$m.txt
   done
