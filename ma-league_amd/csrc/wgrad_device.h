@@ -274,7 +274,7 @@ __device__ __forceinline__ int find_bjob(const BJobsT<MJ>& J, int task) {
 }
 
 template <int MJ>
-__global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* __restrict__ slab) {
+__global__ void __launch_bounds__(256, 2) wgrad_block_kernel(BJobsT<MJ> J, float* __restrict__ slab) {
     const int lane = threadIdx.x & 63;
     const int task = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const BJob& last = J.j[J.n - 1];
@@ -304,10 +304,17 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
     // mlg_device.h mfma_x6): lane (col, g) loads rows rr + 8g .. rr + 8g + 7; K slot t of its operands = row
     // rr + 8g + t, so tile i's A operand is element i of the 8 delta vectors and tile j's B operand element j of
     // the 8 x vectors. Same D layout (and output permutation) as the f32 form below.
-    for (int rr = r0; rr < r1; rr += 32) {
+    // jobs that skip dead rows deal their 32-row steps to the chunks round-robin (chunk ch takes steps ch, ch +
+    // chunks, ...): the live rows (a prefix of every episode) then spread evenly over the job's waves instead of
+    // leaving whole chunks with all the work; other jobs keep contiguous chunks
+    const bool strided = jb.skip != 0;
+    const int s0 = strided ? ch : r0 >> 5, s1 = strided ? (jb.rows + 31) >> 5 : (r1 + 31) >> 5;
+    const int ds = strided ? jb.chunks : 1, rend = strided ? jb.rows : r1;
+    for (int s = s0; s < s1; s += ds) {
+        const int rr = s << 5;
         // rows with zero deltas add exactly zero: a lane's 8-row group of them loads nothing (zeros), a step with no
         // live group is skipped
-        bool glive = rr + 8 * g < r1;
+        bool glive = rr + 8 * g < rend;
         if (jb.skip) {
             glive = glive && bjob_row_live(jb, rr + 8 * g);
             if (__ballot(glive) == 0) continue;
@@ -316,7 +323,7 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int row = rr + 8 * g + t;
-            const bool rv = glive && row < r1;
+            const bool rv = glive && row < rend;
             const float* dr = jb.delta + (int64_t)row * jb.ldd + m0;
             const float* xr = jb.x + (int64_t)row * jb.ldx + k0;
             if (rv && va) {
@@ -336,18 +343,21 @@ __global__ void __launch_bounds__(256) wgrad_block_kernel(BJobsT<MJ> J, float* _
                 for (int i = 0; i < 4; ++i) b[t][i] = (rv && k0 + i < jb.K) ? xr[i] : 0.f;
             }
         }
-        Split3 as[4], bs[4];
+        Split3 as[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             as[i] = split3(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]});
-            bs[i] = split3(floatx4{b[0][i], b[1][i], b[2][i], b[3][i]}, floatx4{b[4][i], b[5][i], b[6][i], b[7][i]});
 #pragma unroll
             for (int t = 0; t < 8; ++t) bsum[i] += a[t][i];
         }
+        // x tiles split one at a time (12 VGPRs live instead of 48: 256 registers, two waves per SIMD); every
+        // accumulator sees the same product sequence as with all four split up front
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            const Split3 bs = split3(floatx4{b[0][j], b[1][j], b[2][j], b[3][j]}, floatx4{b[4][j], b[5][j], b[6][j], b[7][j]});
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_x6(as[i], bs[j], acc[i][j]);
+            for (int i = 0; i < 4; ++i) acc[i][j] = mfma_x6(as[i], bs, acc[i][j]);
+        }
     }
 #else
     // two 4-row steps per iteration: both steps' loads are issued before the first step's MFMAs (same
