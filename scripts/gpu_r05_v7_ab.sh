@@ -3,7 +3,7 @@
 # replay ring), one process per library, two passes.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/v7_ab
-for pass in 1 2; do
+for pass in $(seq 1 ${PASSES:-2}); do
   for v in ${VARIANTS:-default}; do
     if [ "$v" = default ]; then lib=""; else lib=ma-league_amd/maleague/_lib/variants/$v.so; fi
     MLG_LIB=$lib RING=1 MLG_BENCH_KERNELS=v7 timeout -k 10 200 python scripts/bench_rollout.py > gpurun_out/v7_ab/${v}_$pass.json 2> gpurun_out/v7_ab/${v}_$pass.err \
