@@ -20,6 +20,8 @@
 //   finish      clip_grad_norm_ (10), RMSprop, stats (:211-231)
 // Agent rows: r = (c * B + b) * NA + n for copy c (0 plain, 1 within, 2 interact); target rows r = b * NA + n.
 // Items i = b * T + t. Mixer items use t < T - 1 (the other kernels write zeros for t = T - 1).
+#include <mutex>
+
 #include "mlg_host.h"
 #include "gru4_device.h"
 #include "refil_device.h"
@@ -1598,6 +1600,28 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     return J;
 }
 
+// The mixer's hypernetwork kernels run on a second stream beside the agent path: hyper_fwd needs only the
+// prologue's outputs (beside ent_fwd -> rec4 -> q), hyper_bwd only mix_td's dX (beside rec_bwd4 -> ent_bwd); the
+// sequential recurrences leave most CUs idle. One side stream and four events per device, created on first use.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+SideStream* side_stream() {
+    static SideStream side[64];
+    static std::mutex mu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    SideStream& ss = side[dev];
+    if (!ss.s) {
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        for (auto& e : ss.ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    }
+    return &ss;
+}
+
 int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs* bufs, hipStream_t s) {
     const RCfg& c = p.c;
     const bool s8 = is_s8(c);  // the refil_8 shape: static instantiations of the per-item kernels
@@ -1666,6 +1690,13 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     P.nb_t = (3 * EMB * EMB + 255) / 256;
     P.nb_e = (int)(((int64_t)c.I * NE * c.K1 + 255) / 256);
     hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)prologue_blocks(P)), dim3(256), 0, s, P);
+    static const bool one_stream = getenv("MLG_REFIL_ONE_STREAM") != nullptr;
+    SideStream* side = one_stream ? nullptr : side_stream();
+    const hipStream_t sh = side ? side->s : s;  // the hypernet kernels' stream
+    if (side) {
+        MLG_REQUIRE(hipEventRecord(side->ev[0], s) == hipSuccess && hipStreamWaitEvent(sh, side->ev[0], 0) == hipSuccess,
+                    "refil learner: side stream fork");
+    }
     // ---- agent forward ----
     AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on,
                  ws + w.h_wsp[8]};
@@ -1701,9 +1732,13 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hp.X[k] = ws + w.X[k];
         hp.Xtg[k] = ws + w.Xtg[k];
     }
-    hipLaunchKernelGGL(s8 ? hyper_fwd_kernel<1> : hyper_fwd_kernel<0>, dim3((unsigned)c.I, 8), dim3(64), 0, s, c, bt,
+    hipLaunchKernelGGL(s8 ? hyper_fwd_kernel<1> : hyper_fwd_kernel<0>, dim3((unsigned)c.I, 8), dim3(64), 0, sh, c, bt,
                        bufs->groupA, p.Lh, ws + w.ein, hp,
                        ws + w.msum);
+    if (side) {
+        MLG_REQUIRE(hipEventRecord(side->ev[1], sh) == hipSuccess && hipStreamWaitEvent(s, side->ev[1], 0) == hipSuccess,
+                    "refil learner: side stream join");
+    }
     MixIO io;
     for (int k = 0; k < 4; ++k) {
         io.X[k] = ws + w.X[k];
@@ -1717,6 +1752,10 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     io.d2 = ws + w.d2;
     io.part = ws + w.part;
     hipLaunchKernelGGL(s8 ? mix_td_kernel<1> : mix_td_kernel<0>, dim3((unsigned)c.I), dim3(64), 0, s, c, bt, io);
+    if (side) {
+        MLG_REQUIRE(hipEventRecord(side->ev[2], s) == hipSuccess && hipStreamWaitEvent(sh, side->ev[2], 0) == hipSuccess,
+                    "refil learner: side stream fork");
+    }
     HypBwd hb;
     for (int k = 0; k < 4; ++k) {
         hb.Pon[k] = ws + w.ph_on[k];
@@ -1732,8 +1771,9 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
         hb.dqkvm[k] = ws + w.dqkvm[k];
         hb.dfc1m[k] = ws + w.dfc1m[k];
     }
-    hipLaunchKernelGGL(s8 ? hyper_bwd_kernel<1> : hyper_bwd_kernel<0>, dim3((unsigned)c.I, 4), dim3(64), 0, s, c, bt, hb,
+    hipLaunchKernelGGL(s8 ? hyper_bwd_kernel<1> : hyper_bwd_kernel<0>, dim3((unsigned)c.I, 4), dim3(64), 0, sh, c, bt, hb,
                        ws + w.msum);
+    if (side) MLG_REQUIRE(hipEventRecord(side->ev[3], sh) == hipSuccess, "refil learner: side stream record");
     // ---- agent backward ----
     if (rec16)
         hipLaunchKernelGGL(rec_bwd_kernel, dim3((unsigned)nt_on), dim3(256), 0, s, c, bt, La, ws + w.pa_on, ws + w.hs_on,
@@ -1746,6 +1786,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
               ws + w.dgi, ws + w.dfc2, ws + w.dout, ws + w.dqkv, ws + w.dfc1};
     hipLaunchKernelGGL(s8 ? ent_bwd_kernel<1> : ent_bwd_kernel<0>, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt,
                        eb, ws + w.msum);
+    if (side) MLG_REQUIRE(hipStreamWaitEvent(s, side->ev[3], 0) == hipSuccess, "refil learner: side stream join");
     // ---- weight gradients, clip, RMSprop ----
     int64_t slab_floats, n_red;
     int n_tasks;
