@@ -1887,6 +1887,25 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     else
         hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, Mtg, p.mp,
                            ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
+    // weight gradients as two job views: fc2 and the mixer's (their deltas are final after the mixer kernel) on a side
+    // stream beside the reverse recurrence, then fc1 / W_ih / W_hh after agent_dx (same dW / db as one table)
+    int64_t slab_floats, n_red;
+    int n_tasks;
+    WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
+    static const bool one_stream = getenv("MLG_LEARNER_ONE_STREAM") != nullptr;
+    mlg::SideStream* side = one_stream ? nullptr : mlg::side_stream();
+    const hipStream_t se = side ? side->s : s;
+    int ta, tb;
+    int64_t ra, rb;
+    const WJobs JA = mlg::bjob_view(J, 3, J.n, &ta, &ra), JB = mlg::bjob_view(J, 0, 3, &tb, &rb);
+    const int nra = (int)((ra + 255) / 256), nrb = (int)((rb + 255) / 256);
+    if (side) {
+        MLG_REQUIRE(mlg::fork_join(side, 0, s, se), "qlearner: side stream fork");
+    }
+    hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((ta + 3) / 4)), dim3(256), 0, se, JA, ws + p.w.slab);
+    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)nra), dim3(256), 0, se, JA, ws + p.w.slab,
+                       ws + p.w.nrm);
+    if (side) MLG_REQUIRE(hipEventRecord(side->ev[1], se) == hipSuccess, "qlearner: side stream record");
     if (rec16)
         hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                            ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi,
@@ -1897,14 +1916,11 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
                            ws + p.w.dgh, ws + p.w.msum);
     hipLaunchKernelGGL((agent_dx_kernel<H>), dim3(ntiles, c.T), dim3(threads), 0, s, c, ws + p.w.wihT, ws + p.w.x,
                        ws + p.w.dgi, ws + p.w.da, ws + p.w.msum);
-    int64_t slab_floats, n_red;
-    int n_tasks;
-    WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
-    hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((n_tasks + 3) / 4)), dim3(256), 0, s, J,
-                       ws + p.w.slab);
-    const int n_red_blocks = (int)((n_red + 255) / 256);
-    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J,
-                       ws + p.w.slab, ws + p.w.nrm);
+    hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((tb + 3) / 4)), dim3(256), 0, s, JB, ws + p.w.slab);
+    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)nrb), dim3(256), 0, s, JB, ws + p.w.slab,
+                       ws + p.w.nrm + nra);
+    if (side) MLG_REQUIRE(hipStreamWaitEvent(s, side->ev[1], 0) == hipSuccess, "qlearner: side stream join");
+    const int n_red_blocks = nra + nrb;
     const int64_t n_par = p.n_agent + p.n_mixer;
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + p.w.part,
                        p.w.n_mix_tiles, ws + p.w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr,

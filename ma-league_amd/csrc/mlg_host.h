@@ -4,6 +4,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <mutex>
 #include <string>
 
 namespace mlg {
@@ -27,6 +28,31 @@ inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail("%s: %s", what, hipGetErrorString(e));
     return 0;
+}
+
+// A second stream of the current device for learner kernels that run beside the main chain (forked and joined with
+// the events; one stream and four events per device, created on first use, never destroyed). nullptr on failure.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+inline SideStream* side_stream() {
+    static SideStream side[64];
+    static std::mutex mu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    SideStream& ss = side[dev];
+    if (!ss.s) {
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        for (auto& e : ss.ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    }
+    return &ss;
+}
+// event `k` recorded on `from`, waited for by `to`
+inline bool fork_join(SideStream* ss, int k, hipStream_t from, hipStream_t to) {
+    return hipEventRecord(ss->ev[k], from) == hipSuccess && hipStreamWaitEvent(to, ss->ev[k], 0) == hipSuccess;
 }
 
 }  // namespace mlg

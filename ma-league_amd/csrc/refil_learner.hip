@@ -20,8 +20,6 @@
 //   finish      clip_grad_norm_ (10), RMSprop, stats (:211-231)
 // Agent rows: r = (c * B + b) * NA + n for copy c (0 plain, 1 within, 2 interact); target rows r = b * NA + n.
 // Items i = b * T + t. Mixer items use t < T - 1 (the other kernels write zeros for t = T - 1).
-#include <mutex>
-
 #include "mlg_host.h"
 #include "gru4_device.h"
 #include "refil_device.h"
@@ -1602,26 +1600,7 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
 
 // The mixer's hypernetwork kernels run on a second stream beside the agent path: hyper_fwd needs only the
 // prologue's outputs (beside ent_fwd -> rec4 -> q), hyper_bwd only mix_td's dX (beside rec_bwd4 -> ent_bwd); the
-// sequential recurrences leave most CUs idle. One side stream and four events per device, created on first use.
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-};
-SideStream* side_stream() {
-    static SideStream side[64];
-    static std::mutex mu;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    SideStream& ss = side[dev];
-    if (!ss.s) {
-        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        for (auto& e : ss.ev)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    }
-    return &ss;
-}
-
+// sequential recurrences leave most CUs idle (mlg::side_stream, mlg_host.h).
 int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs* bufs, hipStream_t s) {
     const RCfg& c = p.c;
     const bool s8 = is_s8(c);  // the refil_8 shape: static instantiations of the per-item kernels
@@ -1691,11 +1670,10 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     P.nb_e = (int)(((int64_t)c.I * NE * c.K1 + 255) / 256);
     hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)prologue_blocks(P)), dim3(256), 0, s, P);
     static const bool one_stream = getenv("MLG_REFIL_ONE_STREAM") != nullptr;
-    SideStream* side = one_stream ? nullptr : side_stream();
+    mlg::SideStream* side = one_stream ? nullptr : mlg::side_stream();
     const hipStream_t sh = side ? side->s : s;  // the hypernet kernels' stream
     if (side) {
-        MLG_REQUIRE(hipEventRecord(side->ev[0], s) == hipSuccess && hipStreamWaitEvent(sh, side->ev[0], 0) == hipSuccess,
-                    "refil learner: side stream fork");
+        MLG_REQUIRE(mlg::fork_join(side, 0, s, sh), "refil learner: side stream fork");
     }
     // ---- agent forward ----
     AgentPtrs on{ws + w.pa_on, ws + w.x1, ws + w.qkv, ws + w.P, ws + w.o, ws + w.x2, ws + w.x3, ws + w.gi_on,
@@ -1736,8 +1714,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
                        bufs->groupA, p.Lh, ws + w.ein, hp,
                        ws + w.msum);
     if (side) {
-        MLG_REQUIRE(hipEventRecord(side->ev[1], sh) == hipSuccess && hipStreamWaitEvent(s, side->ev[1], 0) == hipSuccess,
-                    "refil learner: side stream join");
+        MLG_REQUIRE(mlg::fork_join(side, 1, sh, s), "refil learner: side stream join");
     }
     MixIO io;
     for (int k = 0; k < 4; ++k) {
@@ -1753,8 +1730,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     io.part = ws + w.part;
     hipLaunchKernelGGL(s8 ? mix_td_kernel<1> : mix_td_kernel<0>, dim3((unsigned)c.I), dim3(64), 0, s, c, bt, io);
     if (side) {
-        MLG_REQUIRE(hipEventRecord(side->ev[2], s) == hipSuccess && hipStreamWaitEvent(sh, side->ev[2], 0) == hipSuccess,
-                    "refil learner: side stream fork");
+        MLG_REQUIRE(mlg::fork_join(side, 2, s, sh), "refil learner: side stream fork");
     }
     HypBwd hb;
     for (int k = 0; k < 4; ++k) {

@@ -490,7 +490,29 @@ inline int64_t layout_bjobs(BJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t
     *n_tasks = tasks;
     *n_red = red;
     *slab_part = mlg_align4(slab);
-    return mlg_align4(slab) + mlg_align4((red + 255) / 256);
+    // norm partials: one per reduce block, + 4 for a table reduced as two views (bjob_view: one more block at most)
+    return mlg_align4(slab) + mlg_align4((red + 255) / 256) + 4;
+}
+
+// jobs [q0, q1) of a laid-out table as a table of their own (tasks renumbered from 0, slab positions kept): the
+// wgrad and reduce launches of a view compute exactly the view's dW / db (same chunks, same order), so a table can
+// run as two views on two streams; the view's norm partials go to their own range of the partial array
+template <int MJ>
+inline BJobsT<MJ> bjob_view(const BJobsT<MJ>& J, int q0, int q1, int* n_tasks, int64_t* n_red) {
+    BJobsT<MJ> V;
+    V.n = 0;
+    int tasks = 0;
+    int64_t red = 0;
+    for (int q = q0; q < q1; ++q) {
+        V.j[V.n] = J.j[q];
+        V.j[V.n].task0 = tasks;
+        tasks += J.j[q].mb * J.j[q].nb * J.j[q].chunks;
+        red += (int64_t)J.j[q].mb * J.j[q].nb * BSLAB;
+        ++V.n;
+    }
+    *n_tasks = tasks;
+    *n_red = red;
+    return V;
 }
 
 }  // namespace mlg
