@@ -2,7 +2,7 @@
 # A/B of self-play rollout variants (scripts/bench_sp_rollout.py, one process per library), two passes.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/sp_ab
-for pass in 1 2; do
+for pass in $(seq 1 ${PASSES:-2}); do
   for v in ${VARIANTS:-default}; do
     if [ "$v" = default ]; then lib=""; else lib=ma-league_amd/maleague/_lib/variants/$v.so; fi
     k=${KERNEL:-}
