@@ -120,6 +120,7 @@ class ParallelStepper(EnvStepper):
         # run summaries in flight: one pinned host buffer per run, up to _HOST_RING runs unresolved
         self._info_hosts = [torch.zeros(6 * B, dtype=torch.int32, pin_memory=pin) for _ in range(self._HOST_RING)]
         self._pendings = deque()  # (run_id, event, test_mode, host buffer): summary copies in flight
+        self._last_end_ev = None  # end event of the last timed launch (bench.py): reused as its summary event
         self._post = []       # resolved runs awaiting host post-processing (logger, env_infos)
         self._runs = {}       # run_id -> (last_run dict, EnvInfos), the latest two
         self._run_id = 0
@@ -234,13 +235,19 @@ class ParallelStepper(EnvStepper):
         """Zero-copy: the kernel already wrote the summary into the reserved pinned buffer; an event marks its
         completion. Else async D2H of the device summary into a pinned buffer of the ring (stream-ordered before
         the next run's kernel rewrites the device copy), then the event."""
+        ev = None
         if self._zero_copy():
             host = self._host_slot
+            # the run's timing end event (bench.py) already marks the kernel's completion: no second event record
+            # (each costs a few us of queue time between the rollout and the learner)
+            ev = self._last_end_ev
         else:
             host = self._reserve_host()
             host.copy_(self._info, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        self._last_end_ev = None
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record()
         self._run_id += 1
         self._pendings.append((self._run_id, ev, test_mode, host))
 
@@ -346,6 +353,7 @@ class ParallelStepper(EnvStepper):
 
     def _launch_mb(self, mb, epsilon: float, test_mode: bool):
         run_info = self._run_info()
+        self.home_mac.agent.packed()  # a re-pack (parameters changed) runs before the timed window
         ev = None
         if self._timed_launch():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -354,6 +362,7 @@ class ParallelStepper(EnvStepper):
         if ev is not None:
             ev[1].record()
             self.timing.append(ev)
+            self._last_end_ev = ev[1]
 
     def run(self, test_mode=False):
         if self.home_mac is None:

@@ -97,17 +97,19 @@ class SelfPlayParallelStepper(ParallelStepper):
             raise ValueError("home and away agents must have the same architecture")
         st = self.envs.to_c()
         run_info = self._run_info()
+        p_h, p_a = h_agent.packed(), a_agent.packed()  # re-packs (parameters changed) before the timed window
         ev = None
         if self._timed_launch():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         _native.call("mlg_rollout_selfplay", _native.byref(self._cspec), _native.byref(st), _native.byref(d),
-                     _native.ptr(h_agent.packed()), _native.ptr(a_agent.packed()), _native.byref(mb_h),
+                     _native.ptr(p_h), _native.ptr(p_a), _native.byref(mb_h),
                      _native.byref(mb_a), _native.byref(run_info), float(eps_h), float(eps_a),
                      int(bool(test_mode)), _native.stream_ptr(self.device))
         if ev is not None:
             ev[1].record()
             self.timing.append(ev)
+            self._last_end_ev = ev[1]
         del keep
         self._queue_summary(test_mode)
         self._finish_post()
