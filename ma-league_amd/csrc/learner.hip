@@ -1555,6 +1555,34 @@ __global__ void __launch_bounds__(512) agent_bwd4_kernel(LCfg c, MlgBatch bt, Ag
     lst.flush(1);
 }
 
+// The reverse recurrence (blocks < nbwd, H = 64: 4 waves each) and, as the launch's remaining workgroups, the weight
+// gradients whose deltas are final after the mixer kernel (fc2 and the mixer's jobs: table view JA). The
+// recurrence keeps 40 CUs busy for its 101 sequential steps; the wgrad workgroups fill the others, with no second
+// stream and no events (each event record costs a few us of queue time). Same per-job arithmetic as the separate
+// launches.
+template <int H>
+__global__ void __launch_bounds__(256, 2) bwd4_wgrad_kernel(LCfg c, MlgBatch bt, AgentLayout L, const float* __restrict__ P,
+                                                         const float* __restrict__ ws_hs, const float* __restrict__ ws_gr,
+                                                         const float* __restrict__ ws_gz, const float* __restrict__ ws_gn,
+                                                         const float* __restrict__ ws_ghn, const float* __restrict__ dqv,
+                                                         float* __restrict__ dgi, float* __restrict__ dgh,
+                                                         const float* __restrict__ msum, WJobs JA,
+                                                         float* __restrict__ slab, int nbwd) {
+    if ((int)blockIdx.x >= nbwd) {
+        mlg::wgrad_block_body<16>(JA, slab, (int)blockIdx.x - nbwd);
+        return;
+    }
+    LStamps lst;
+    lst.init();
+    const int r = blockIdx.x * 4 + ((threadIdx.x & 63) & 3);
+    const bool valid = r < c.R;
+    const int b = valid ? r / c.N : 0, n = valid ? r % c.N : 0;
+    const mlg::Gru4Bwd a{c.R, c.T, c.A, c.N, P + L.whh, P + L.w2, ws_hs, ws_gr, ws_gz, ws_gn, ws_ghn, dqv,
+                         bt.actions, dgi, dgh};
+    mlg::gru4_bwd<H>(a, blockIdx.x, t_eff(msum), bslot(bt, b) * bt.T1 * c.N + n, lst);
+    lst.flush(1);
+}
+
 // dA = (W_ih^T dGI) * (x > 0) for every (t, row): grid (ntiles, T), HC waves (wave = feature chunk).
 template <int H>
 __global__ void __launch_bounds__(512) agent_dx_kernel(LCfg c, const float* __restrict__ wihT,
@@ -1887,40 +1915,41 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     else
         hipLaunchKernelGGL((mix_td_kernel<64, 32>), dim3(p.w.n_mix_tiles), dim3(128), 0, s, c, bt, Mon, Mtg, p.mp,
                            ws + p.w.mac, ws + p.w.tmac, ws + p.w.msum, mo);
-    // weight gradients as two job views: fc2 and the mixer's (their deltas are final after the mixer kernel) on a side
-    // stream beside the reverse recurrence, then fc1 / W_ih / W_hh after agent_dx (same dW / db as one table)
+    // weight gradients: fc2 and the mixer's jobs (final after the mixer kernel, table view JA) run as extra
+    // workgroups of the reverse-recurrence launch (H = 64, bwd4_wgrad_kernel); fc1 / W_ih / W_hh (view JB) after
+    // agent_dx; one reduce over the whole table
     int64_t slab_floats, n_red;
     int n_tasks;
     WJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
-    static const bool one_stream = getenv("MLG_LEARNER_ONE_STREAM") != nullptr;
-    mlg::SideStream* side = one_stream ? nullptr : mlg::side_stream();
-    const hipStream_t se = side ? side->s : s;
     int ta, tb;
     int64_t ra, rb;
     const WJobs JA = mlg::bjob_view(J, 3, J.n, &ta, &ra), JB = mlg::bjob_view(J, 0, 3, &tb, &rb);
-    const int nra = (int)((ra + 255) / 256), nrb = (int)((rb + 255) / 256);
-    if (side) {
-        MLG_REQUIRE(mlg::fork_join(side, 0, s, se), "qlearner: side stream fork");
-    }
-    hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((ta + 3) / 4)), dim3(256), 0, se, JA, ws + p.w.slab);
-    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)nra), dim3(256), 0, se, JA, ws + p.w.slab,
-                       ws + p.w.nrm);
-    if (side) MLG_REQUIRE(hipEventRecord(side->ev[1], se) == hipSuccess, "qlearner: side stream record");
-    if (rec16)
+    const bool fused = !rec16 && H == 64 && threads == 256;
+    if (fused) {
+        const int nbwd = (c.R + 3) / 4;
+        hipLaunchKernelGGL((bwd4_wgrad_kernel<H>), dim3((unsigned)(nbwd + (ta + 3) / 4)), dim3(256), 0, s, c, bt, p.L,
+                           ws + p.w.p_on, ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq,
+                           ws + p.w.dgi, ws + p.w.dgh, ws + p.w.msum, JA, ws + p.w.slab, nbwd);
+    } else if (rec16) {
         hipLaunchKernelGGL((agent_bwd_kernel<H>), dim3(ntiles), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                            ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi,
                            ws + p.w.dgh, ws + p.w.msum);
-    else
+    } else {
         hipLaunchKernelGGL((agent_bwd4_kernel<H>), dim3((c.R + 3) / 4), dim3(threads), 0, s, c, bt, p.L, ws + p.w.p_on,
                            ws + p.w.hs, ws + p.w.gr, ws + p.w.gz, ws + p.w.gn, ws + p.w.ghn, ws + p.w.dq, ws + p.w.dgi,
                            ws + p.w.dgh, ws + p.w.msum);
+    }
     hipLaunchKernelGGL((agent_dx_kernel<H>), dim3(ntiles, c.T), dim3(threads), 0, s, c, ws + p.w.wihT, ws + p.w.x,
                        ws + p.w.dgi, ws + p.w.da, ws + p.w.msum);
-    hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((tb + 3) / 4)), dim3(256), 0, s, JB, ws + p.w.slab);
-    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)nrb), dim3(256), 0, s, JB, ws + p.w.slab,
-                       ws + p.w.nrm + nra);
-    if (side) MLG_REQUIRE(hipStreamWaitEvent(s, side->ev[1], 0) == hipSuccess, "qlearner: side stream join");
-    const int n_red_blocks = nra + nrb;
+    if (fused)
+        hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((tb + 3) / 4)), dim3(256), 0, s, JB,
+                           ws + p.w.slab);
+    else
+        hipLaunchKernelGGL(mlg::wgrad_block_kernel<16>, dim3((unsigned)((n_tasks + 3) / 4)), dim3(256), 0, s, J,
+                           ws + p.w.slab);
+    const int n_red_blocks = (int)((n_red + 255) / 256);
+    hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<16>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J,
+                       ws + p.w.slab, ws + p.w.nrm);
     const int64_t n_par = p.n_agent + p.n_mixer;
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + p.w.part,
                        p.w.n_mix_tiles, ws + p.w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr,

@@ -273,10 +273,12 @@ __device__ __forceinline__ int find_bjob(const BJobsT<MJ>& J, int task) {
     return k;
 }
 
+// the work of workgroup `bid` (4 waves = 4 consecutive tasks) of a wgrad launch; a __device__ function so that
+// a learner can run it as extra workgroups of another launch (learner.hip bwd4_wgrad_kernel)
 template <int MJ>
-__global__ void __launch_bounds__(256, 2) wgrad_block_kernel(BJobsT<MJ> J, float* __restrict__ slab) {
+__device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __restrict__ slab, int bid) {
     const int lane = threadIdx.x & 63;
-    const int task = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int task = bid * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const BJob& last = J.j[J.n - 1];
     if (task >= last.task0 + last.mb * last.nb * last.chunks) return;
     const BJob jb = J.j[find_bjob(J, task)];
@@ -418,6 +420,11 @@ __global__ void __launch_bounds__(256, 2) wgrad_block_kernel(BJobsT<MJ> J, float
 }
 
 // fixed-order sum over chunks -> dW / db (bias from the nbi == 0 blocks); per-block sums of squares -> nrm_part
+template <int MJ>
+__global__ void __launch_bounds__(256, 2) wgrad_block_kernel(BJobsT<MJ> J, float* __restrict__ slab) {
+    wgrad_block_body<MJ>(J, slab, (int)blockIdx.x);
+}
+
 template <int MJ>
 __global__ void __launch_bounds__(256) wgrad_block_reduce_kernel(BJobsT<MJ> J, const float* __restrict__ slab,
                                                                  float* __restrict__ nrm_part) {
