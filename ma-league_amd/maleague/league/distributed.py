@@ -90,13 +90,16 @@ class DistributedLeague:
         if self._delta.is_cuda:
             from .. import _native
             B = int(won.shape[0])
-            # the kernel reads int32 rows: [B, 2] won (policy team first) and [B] draw
+            # the kernel reads int32 rows: [B, 2] won (policy team first) and [B] draw, from device memory or from a
+            # pinned (device-accessible) summary slot written by the rollout (zero-copy, ParallelStepper)
+            reach = lambda x: x.is_cuda or (x.device.type == "cpu" and x.is_pinned())  # noqa: E731
             if won.dtype != torch.int32 or draw.dtype != torch.int32 or tuple(won.shape) != (B, 2) or \
-                    tuple(draw.shape) != (B,) or not won.is_cuda or not draw.is_cuda:
-                raise ValueError(f"record_runs: won must be int32 [B, 2] and draw int32 [B] on the device, got "
-                                 f"{won.dtype} {tuple(won.shape)} / {draw.dtype} {tuple(draw.shape)}")
+                    tuple(draw.shape) != (B,) or not reach(won) or not reach(draw):
+                raise ValueError(f"record_runs: won must be int32 [B, 2] and draw int32 [B] on the device or pinned, "
+                                 f"got {won.dtype} {tuple(won.shape)} / {draw.dtype} {tuple(draw.shape)}")
             entry = self._delta[home, away]
-            _native.call("mlg_league_record_runs", _native.ptr(won.contiguous()), _native.ptr(draw.contiguous()),
+            dptr = lambda x: _native.ptr(x) if x.is_cuda else x.data_ptr()  # noqa: E731  (pinned: device-accessible)
+            _native.call("mlg_league_record_runs", dptr(won.contiguous()), dptr(draw.contiguous()),
                          int(won.shape[0]), entry.data_ptr(), int(not self.payoff.reference_compat),
                          _native.stream_ptr(self.device))
             return

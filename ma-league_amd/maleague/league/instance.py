@@ -127,7 +127,7 @@ class LeagueInstance:
         B = st.batch_size
         for _ in range(iterations):
             exp._train_episode(self.episode)
-            info = st._info
+            info = st.last_run_info() if hasattr(st, "last_run_info") else st._info
             self.league.record_runs(self.pid, self.opponent, info[B:3 * B].view(B, 2), info[3 * B:4 * B])
             self.episode += B
 

@@ -121,6 +121,7 @@ class ParallelStepper(EnvStepper):
         self._info_hosts = [torch.zeros(6 * B, dtype=torch.int32, pin_memory=pin) for _ in range(self._HOST_RING)]
         self._pendings = deque()  # (run_id, event, test_mode, host buffer): summary copies in flight
         self._last_end_ev = None  # end event of the last timed launch (bench.py): reused as its summary event
+        self._host_slot = None  # zero-copy: the pinned ring slot of the last launched run
         self._post = []       # resolved runs awaiting host post-processing (logger, env_infos)
         self._runs = {}       # run_id -> (last_run dict, EnvInfos), the latest two
         self._run_id = 0
@@ -335,6 +336,12 @@ class ParallelStepper(EnvStepper):
         mb, keep = self._to_mlg(batch)
         self._launch_mb(mb, epsilon, test_mode)
         del keep
+
+    def last_run_info(self) -> torch.Tensor:
+        """The int32 [6 B] summary the last launched run writes (ep_len | won [B, 2] | draw | ret | ...): its pinned
+        ring slot in zero-copy mode (device-accessible, read by stream-ordered kernels such as the league's
+        record_runs), else the device buffer."""
+        return self._host_slot if self._zero_copy() and self._host_slot is not None else self._info
 
     def _run_info(self):
         B = self.batch_size

@@ -21,7 +21,8 @@ from .parallel_stepper import LazyEnvInfos, ParallelStepper
 
 
 class SelfPlayParallelStepper(ParallelStepper):
-    _ZERO_COPY = False  # the league reads each run's wins on the device (LeagueInstance.play)
+    # zero-copy run summaries as ParallelStepper: the league's record_runs kernel reads each run's wins straight from
+    # the pinned summary slot (LeagueInstance.play -> last_run_info)
 
     def __init__(self, args, logger, log_start_t=0):
         super().__init__(args, logger, log_start_t)

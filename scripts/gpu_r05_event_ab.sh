@@ -1,6 +1,6 @@
 #!/bin/bash
 # bench legs with the rollout's timing end event reused as the run-summary event (default) vs an event of its own
-# (MLG_AB_OWN_EVENT=1), alternating.
+# (MLG_AB_OWN_EVENT=1: an A/B switch in ParallelStepper._queue_summary, removed after the run), alternating.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/event_ab
 for rep in 1 2 3; do
