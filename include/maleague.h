@@ -301,6 +301,9 @@ typedef struct {
     float *stats;                /* [8] out: loss, im_loss, grad_norm, td_error_abs, q_taken_mean, target_mean,
                                     mask_sum, 0 */
     double *trained_steps;       /* optional [1] += mask_sum (Agent.trained_steps, refil_learner.py:176) */
+    float *target_sync;          /* optional (NULL = off) [n_agent + n_mixer] receives the updated parameters in the
+                                    optimizer launch: the target update when due after this step
+                                    (refil_learner.py:181-183 -> _update_targets; usually target_params) */
 } MlgRefilLearnerBufs;
 
 int64_t mlg_refil_param_counts(const MlgRefilLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);

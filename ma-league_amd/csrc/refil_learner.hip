@@ -1517,7 +1517,7 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
                                                       float lr, float alpha, float eps, float max_norm, int NA,
                                                       float lmbda, float* __restrict__ stats,
                                                       const float* __restrict__ nrm_part, int n_nrm,
-                                                      double* __restrict__ trained) {
+                                                      double* __restrict__ trained, float* __restrict__ tsync) {
     __shared__ float red[1024];
     const int tid = threadIdx.x;
     float s = 0.f;
@@ -1530,7 +1530,9 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
         grads[i] = gi;
         const float a = alpha * sq[i] + (1.f - alpha) * gi * gi;
         sq[i] = a;
-        params[i] -= lr * gi / (sqrtf(a) + eps);
+        const float pn = params[i] - lr * gi / (sqrtf(a) + eps);
+        params[i] = pn;
+        if (tsync) tsync[i] = pn;  // the target update due after this step (refil_learner.py:181-183), same launch
     }
     if (blockIdx.x == 0) {
         float s5[5];
@@ -1775,7 +1777,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + w.part, c.I,
                        ws + w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr, cfg->optim_alpha,
                        cfg->optim_eps, cfg->grad_norm_clip, c.NA, c.lmbda, bufs->stats, ws + p.w.nrm, n_red_blocks,
-                       bufs->trained_steps);
+                       bufs->trained_steps, bufs->target_sync);
     return mlg::check_launch("refil_train");
 }
 

@@ -115,19 +115,23 @@ class REFILLearner(Learner):
                          groupA.data_ptr(), _native.stream_ptr(self.device))
         groupA = groupA.reshape(B, NE).to(device=self.device, dtype=torch.uint8).contiguous()
         mb, keep = mlg_entity_batch(batch)
-        # trained steps accumulate on the device inside the optimizer launch (no separate add)
+        # trained steps accumulate on the device inside the optimizer launch (no separate add); the target update
+        # due after this step (refil_learner.py:181-183) is written by that launch too (no separate copy)
         counter = self.mac.agent.trained_counter(self.device)
+        sync = (episode_num - self.last_target_update_episode) / self.args.target_update_interval >= 1.0
         bufs = _native.MlgRefilLearnerBufs(mb, groupA.data_ptr(), self._flat.flat.data_ptr(), self._grads.data_ptr(),
                                            self._sq.data_ptr(), self._tflat.flat.data_ptr(), self._ws.data_ptr(),
-                                           self._stats.data_ptr(), counter.data_ptr())
+                                           self._stats.data_ptr(), counter.data_ptr(),
+                                           self._tflat.flat.data_ptr() if sync else None)
         _native.call("mlg_refil_train", _native.byref(cfg), _native.byref(bufs), _native.stream_ptr(self.device))
         del keep
         self._groupA = groupA
         self._step += 1
         self.mac.agent.mark_dirty()
         self.train_calls += 1
-        if (episode_num - self.last_target_update_episode) / self.args.target_update_interval >= 1.0:
-            self.update_targets()
+        if sync:
+            self.target_mac.agent.mark_dirty()
+            self.logger.info(f"Updated {self.name}target network.")
             self.last_target_update_episode = episode_num
         self._stats_fresh = True
         if callable(t_env):  # lazily resolved t_env: the kernels above are already queued
