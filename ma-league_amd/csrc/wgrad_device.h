@@ -165,8 +165,9 @@ inline int64_t layout_jobs(WJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t*
 
 // ================================================================================================
 // Blocked variant: one wave per (job, 64 x 64 output block, 1024-row chunk); per 4-row step every lane loads 4 delta
-// and 4 x values and issues 16 MFMAs (vs 2 loads per MFMA above), partials [block][chunk][64 * 64 + 64] summed over
-// chunks in a fixed order (deterministic).
+// and 4 x values and issues 16 MFMAs (vs 2 loads per MFMA above); the 4 waves of a workgroup (4 chunks of one block)
+// add their partials in LDS, partials [block][chunk group][64 * 64 + 64] summed over groups in a fixed order
+// (deterministic).
 namespace mlg {
 
 constexpr int BCH = 1024;        // max rows per chunk
@@ -266,6 +267,9 @@ __device__ __forceinline__ bool bjob_row_live(const BJob& jb, int row) {
     return t < (int)jb.mlen[b];
 }
 
+// row chunks are processed (and their partials stored) in groups of 4, one workgroup per group and output block
+__host__ __device__ __forceinline__ int bjob_groups(const BJob& jb) { return (jb.chunks + 3) >> 2; }
+
 template <int MJ>
 __device__ __forceinline__ int find_bjob(const BJobsT<MJ>& J, int task) {
     int k = 0;
@@ -274,22 +278,31 @@ __device__ __forceinline__ int find_bjob(const BJobsT<MJ>& J, int task) {
 }
 
 // the work of workgroup `bid` (4 waves = 4 consecutive tasks) of a wgrad launch; a __device__ function so that
-// a learner can run it as extra workgroups of another launch (learner.hip bwd4_wgrad_kernel)
+// a learner can run it as extra workgroups of another launch (learner.hip bwd4_wgrad_kernel). 256 threads.
 template <int MJ>
 __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __restrict__ slab, int bid) {
-    const int lane = threadIdx.x & 63;
-    const int task = bid * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // partials of the 4 waves summed pairwise in LDS, (c0 + c2) + (c1 + c3), before the one slab store per workgroup
+    // (two 16 KB slots: with the reverse recurrence's LDS, bwd4_wgrad_kernel still fits two workgroups per CU)
+    __shared__ __attribute__((aligned(16))) floatx4 wred[2][16][64];
+    __shared__ float wbred[2][4][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int task = bid * 4 + w;
     const BJob& last = J.j[J.n - 1];
-    if (task >= last.task0 + last.mb * last.nb * last.chunks) return;
+    // job task counts are multiples of 4: the test (and the job) is the same for the whole workgroup
+    if (bid * 4 >= last.task0 + last.mb * last.nb * bjob_groups(last) * 4) return;
     const BJob jb = J.j[find_bjob(J, task)];
     const int local = task - jb.task0;
-    // the output blocks of one row chunk are consecutive tasks (the same workgroup / neighbours): jobs with several
-    // 64-row output blocks (M = 192: in_trans, W_ih, W_hh) then read their x rows from HBM once, the other blocks
-    // hit L2 (block-major order re-read them from HBM per block). Slab positions do not depend on this order.
-    const int ch = local / (jb.mb * jb.nb), blk = local % (jb.mb * jb.nb);
+    // the 4 waves of a workgroup take the row chunks 4 cg .. 4 cg + 3 of one 64 x 64 output block and add their
+    // partials in LDS (chunk order), so the slab holds one partial per chunk group; the output blocks of one chunk
+    // group are consecutive workgroups (jobs with several 64-row output blocks - M = 192: in_trans, W_ih, W_hh - then
+    // read their x rows from HBM about once, the other blocks hit the MALL)
+    const int grp = local >> 2, nblk = jb.mb * jb.nb;
+    const int cg = grp / nblk, blk = grp % nblk;
+    const int ch = 4 * cg + w;
+    const bool act = ch < jb.chunks;  // the last group's spare waves add zeros
     const int mbi = blk / jb.nb, nbi = blk % jb.nb;
     const int col = lane & 15, g = lane >> 4;
-    const int r0 = ch * jb.ch_rows, r1 = min(jb.rows, r0 + jb.ch_rows);
+    const int r0 = ch * jb.ch_rows, r1 = act ? min(jb.rows, r0 + jb.ch_rows) : r0;
     floatx4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -310,7 +323,7 @@ __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __r
     // chunks, ...): the live rows (a prefix of every episode) then spread evenly over the job's waves instead of
     // leaving whole chunks with all the work; other jobs keep contiguous chunks
     const bool strided = jb.skip != 0;
-    const int s0 = strided ? ch : r0 >> 5, s1 = strided ? (jb.rows + 31) >> 5 : (r1 + 31) >> 5;
+    const int s0 = strided ? ch : r0 >> 5, s1 = !act ? s0 : strided ? (jb.rows + 31) >> 5 : (r1 + 31) >> 5;
     const int ds = strided ? jb.chunks : 1, rend = strided ? jb.rows : r1;
     for (int s = s0; s < s1; s += ds) {
         const int rr = s << 5;
@@ -401,7 +414,36 @@ __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __r
         }
     }
 #endif
-    float* out = slab + jb.slab0 + ((int64_t)blk * jb.chunks + ch) * BSLAB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        bsum[i] += __shfl_xor(bsum[i], 16);
+        bsum[i] += __shfl_xor(bsum[i], 32);
+    }
+    auto put = [&](int v) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wred[v][4 * i + j][lane] = acc[i][j];
+        if (g == 0)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wbred[v][i][col] = bsum[i];
+    };
+    auto add = [&](int v) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] += wred[v][4 * i + j][lane];
+            bsum[i] += wbred[v][i][col];
+        }
+    };
+    if (w >= 2) put(w - 2);
+    __syncthreads();
+    if (w < 2) add(w);
+    if (w == 1) put(1);  // slot 1 was read by this wave only
+    __syncthreads();
+    if (w != 0) return;
+    add(1);
+    float* out = slab + jb.slab0 + ((int64_t)blk * bjob_groups(jb) + cg) * BSLAB;
     // D layout: acc[i][j] reg q -> MFMA row 4g + q, i.e. the A values of lane col' = 4g + q (block row
     // m = 4 col' + i), and MFMA column col (block column k = 4 col + j)
 #pragma unroll
@@ -410,16 +452,12 @@ __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __r
         for (int q = 0; q < 4; ++q)
             *reinterpret_cast<floatx4*>(out + (4 * (4 * g + q) + i) * 64 + 4 * col) =
                 floatx4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+    if (g == 0)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float s = bsum[i];
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if (g == 0) out[4096 + 4 * col + i] = s;
-    }
+        for (int i = 0; i < 4; ++i) out[4096 + 4 * col + i] = bsum[i];
 }
 
-// fixed-order sum over chunks -> dW / db (bias from the nbi == 0 blocks); per-block sums of squares -> nrm_part
+// fixed-order sum over chunk groups -> dW / db (bias from the nbi == 0 blocks); per-block sums of squares -> nrm_part
 template <int MJ>
 __global__ void __launch_bounds__(256, 2) wgrad_block_kernel(BJobsT<MJ> J, float* __restrict__ slab) {
     wgrad_block_body<MJ>(J, slab, (int)blockIdx.x);
@@ -440,28 +478,29 @@ __global__ void __launch_bounds__(256) wgrad_block_reduce_kernel(BJobsT<MJ> J, c
             const int blk = (int)(loc / BSLAB), e = (int)(loc % BSLAB);
             const int mbi = blk / jb.nb, nbi = blk % jb.nb;
             float s = 0.f;
-            const float* base = slab + jb.slab0 + (int64_t)blk * jb.chunks * BSLAB + e;
+            const int ng = bjob_groups(jb);
+            const float* base = slab + jb.slab0 + (int64_t)blk * ng * BSLAB + e;
             int ch = 0;
 #ifndef MLG_WRED_DEPTH
 #define MLG_WRED_DEPTH 64
 #endif
             // MLG_WRED_DEPTH loads in flight (the slab partials were just written by other CUs: each round trip is an
-            // L2 / MALL miss), summed in chunk order
-            for (; ch + MLG_WRED_DEPTH <= jb.chunks; ch += MLG_WRED_DEPTH) {
+            // L2 / MALL miss), summed in group order
+            for (; ch + MLG_WRED_DEPTH <= ng; ch += MLG_WRED_DEPTH) {
                 float v[MLG_WRED_DEPTH];
 #pragma unroll
                 for (int u = 0; u < MLG_WRED_DEPTH; ++u) v[u] = base[(int64_t)(ch + u) * BSLAB];
 #pragma unroll
                 for (int u = 0; u < MLG_WRED_DEPTH; ++u) s += v[u];
             }
-            for (; ch + 8 <= jb.chunks; ch += 8) {
+            for (; ch + 8 <= ng; ch += 8) {
                 float v[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(ch + u) * BSLAB];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) s += v[u];
             }
-            for (; ch < jb.chunks; ++ch) s += base[(int64_t)ch * BSLAB];
+            for (; ch < ng; ++ch) s += base[(int64_t)ch * BSLAB];
             if (e < 4096) {
                 const int m = mbi * 64 + e / 64, k = nbi * 64 + e % 64;
                 if (m < jb.M && k < jb.K) {
@@ -490,8 +529,8 @@ inline int64_t layout_bjobs(BJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t
     for (int q = 0; q < J.n; ++q) {
         J.j[q].task0 = tasks;
         J.j[q].slab0 = slab;
-        tasks += J.j[q].mb * J.j[q].nb * J.j[q].chunks;
-        slab += (int64_t)J.j[q].mb * J.j[q].nb * J.j[q].chunks * BSLAB;
+        tasks += J.j[q].mb * J.j[q].nb * bjob_groups(J.j[q]) * 4;
+        slab += (int64_t)J.j[q].mb * J.j[q].nb * bjob_groups(J.j[q]) * BSLAB;
         red += (int64_t)J.j[q].mb * J.j[q].nb * BSLAB;
     }
     *n_tasks = tasks;
@@ -513,7 +552,7 @@ inline BJobsT<MJ> bjob_view(const BJobsT<MJ>& J, int q0, int q1, int* n_tasks, i
     for (int q = q0; q < q1; ++q) {
         V.j[V.n] = J.j[q];
         V.j[V.n].task0 = tasks;
-        tasks += J.j[q].mb * J.j[q].nb * J.j[q].chunks;
+        tasks += J.j[q].mb * J.j[q].nb * bjob_groups(J.j[q]) * 4;
         red += (int64_t)J.j[q].mb * J.j[q].nb * BSLAB;
         ++V.n;
     }

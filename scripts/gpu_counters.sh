@@ -3,7 +3,7 @@
 # refil = refil_rollout), separate rocprofv3 --pmc passes, counters only (no trace domains):
 #   FETCH_SIZE | WRITE_SIZE (HBM bytes; they cannot share a pass) | 3 SQ passes (<= 8 SQ + 1 GRBM counters each)
 # then scripts/parse_counters.py -> gpurun_out/counters/counters.json (copied to profiles/counters.json).
-# COMMIT names the profiled commit (the box has no .git).
+# COMMIT names the profiled commit (the box has no .git); HBM_ONLY=1 runs the two HBM passes only.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/counters
@@ -19,6 +19,7 @@ for m in ${MODES:-ai league refil}; do
   mkdir -p $OUT/$m
   pass $m fetch FETCH_SIZE
   pass $m write WRITE_SIZE
+  [ -n "$HBM_ONLY" ] && continue
   pass $m sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE
   pass $m sq2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
   pass $m sq3 SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_FLAT GRBM_GUI_ACTIVE

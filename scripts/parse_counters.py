@@ -17,7 +17,7 @@ from collections import defaultdict
 root, commit = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "unknown")
 # the rollout kernels and the learners' kernels (QMIX learner.hip, REFIL refil_learner.hip, shared wgrad)
 FILT = tuple(os.environ.get("MLG_CNT_FILTER", "rollout,agent_,rec4_mixpre,mix_td,wgrad_block,finish_kernel,prep_kernel,"
-                            "hyper_fwd,hyper_bwd,ent_fwd,ent_bwd,rec_kernel,rec4_kernel,rec_bwd,q_kernel,prologue_kernel").split(","))
+                            "hyper_fwd,hyper_bwd,ent_fwd,ent_bwd,rec_kernel,rec4_kernel,rec_bwd,q_kernel,prologue_kernel,bwd4_wgrad").split(","))
 
 
 def short(name):
