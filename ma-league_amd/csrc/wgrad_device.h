@@ -269,6 +269,13 @@ __device__ __forceinline__ bool bjob_row_live(const BJob& jb, int row) {
 
 // row chunks are processed (and their partials stored) in groups of 4, one workgroup per group and output block
 __host__ __device__ __forceinline__ int bjob_groups(const BJob& jb) { return (jb.chunks + 3) >> 2; }
+// workgroups of a job: jobs with several output blocks take the groups in stripes of 8 (see wgrad_block_body), the
+// last stripe padded with idle workgroups
+__host__ __device__ __forceinline__ int bjob_stripe(const BJob& jb) { return jb.mb * jb.nb > 1 ? 8 : 1; }
+__host__ __device__ __forceinline__ int bjob_wgs(const BJob& jb) {
+    const int st = bjob_stripe(jb);
+    return jb.mb * jb.nb * ((bjob_groups(jb) + st - 1) / st * st);
+}
 
 template <int MJ>
 __device__ __forceinline__ int find_bjob(const BJobsT<MJ>& J, int task) {
@@ -289,15 +296,19 @@ __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __r
     const int task = bid * 4 + w;
     const BJob& last = J.j[J.n - 1];
     // job task counts are multiples of 4: the test (and the job) is the same for the whole workgroup
-    if (bid * 4 >= last.task0 + last.mb * last.nb * bjob_groups(last) * 4) return;
+    if (bid * 4 >= last.task0 + bjob_wgs(last) * 4) return;
     const BJob jb = J.j[find_bjob(J, task)];
-    const int local = task - jb.task0;
+    const int wg = (task - jb.task0) >> 2;
     // the 4 waves of a workgroup take the row chunks 4 cg .. 4 cg + 3 of one 64 x 64 output block and add their
-    // partials in LDS (chunk order), so the slab holds one partial per chunk group; the output blocks of one chunk
-    // group are consecutive workgroups (jobs with several 64-row output blocks - M = 192: in_trans, W_ih, W_hh - then
-    // read their x rows from HBM about once, the other blocks hit the MALL)
-    const int grp = local >> 2, nblk = jb.mb * jb.nb;
-    const int cg = grp / nblk, blk = grp % nblk;
+    // partials in LDS, so the slab holds one partial per chunk group. Jobs with several output blocks (M = 192:
+    // in_trans, W_ih, W_hh; K > 64) take the groups in stripes of 8: workgroup wg of a stripe has group
+    // stripe * 8 + wg % 8 and block wg / 8, so the blocks of one group are 8 workgroups apart - dispatched at about
+    // the same time to the same XCD (round-robin over the 8 XCDs), where the first to read a row chunk brings it into
+    // that XCD's L2 for the others
+    const int nblk = jb.mb * jb.nb, st = bjob_stripe(jb);
+    const int sl = wg / (st * nblk), sr = wg % (st * nblk);
+    const int cg = sl * st + sr % st, blk = sr / st;
+    if (cg >= bjob_groups(jb)) return;  // the last stripe's padding (whole workgroup)
     const int ch = 4 * cg + w;
     const bool act = ch < jb.chunks;  // the last group's spare waves add zeros
     const int mbi = blk / jb.nb, nbi = blk % jb.nb;
@@ -529,7 +540,7 @@ inline int64_t layout_bjobs(BJobsT<MJ>& J, int* n_tasks, int64_t* n_red, int64_t
     for (int q = 0; q < J.n; ++q) {
         J.j[q].task0 = tasks;
         J.j[q].slab0 = slab;
-        tasks += J.j[q].mb * J.j[q].nb * bjob_groups(J.j[q]) * 4;
+        tasks += bjob_wgs(J.j[q]) * 4;
         slab += (int64_t)J.j[q].mb * J.j[q].nb * bjob_groups(J.j[q]) * BSLAB;
         red += (int64_t)J.j[q].mb * J.j[q].nb * BSLAB;
     }
@@ -552,7 +563,7 @@ inline BJobsT<MJ> bjob_view(const BJobsT<MJ>& J, int q0, int q1, int* n_tasks, i
     for (int q = q0; q < q1; ++q) {
         V.j[V.n] = J.j[q];
         V.j[V.n].task0 = tasks;
-        tasks += J.j[q].mb * J.j[q].nb * bjob_groups(J.j[q]) * 4;
+        tasks += bjob_wgs(J.j[q]) * 4;
         red += (int64_t)J.j[q].mb * J.j[q].nb * BSLAB;
         ++V.n;
     }
