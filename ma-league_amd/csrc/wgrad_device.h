@@ -284,13 +284,72 @@ __device__ __forceinline__ int find_bjob(const BJobsT<MJ>& J, int task) {
     return k;
 }
 
+#if !defined(MLG_WGRAD_F32)
+// the 8 rows rr + 8g .. rr + 8g + 7 of a lane: delta columns m0 .. m0 + 3 into a, x columns k0 .. k0 + 3 into b
+// (zeros for a dead group / rows past rend / columns past M, K)
+__device__ __forceinline__ void wgrad_load_step(const BJob& jb, int rr, int g, bool glive, int rend, int m0, int k0,
+                                                bool va, bool vb, float (&a)[8][4], float (&b)[8][4]) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const int row = rr + 8 * g + t;
+        const bool rv = glive && row < rend;
+        const float* dr = jb.delta + (int64_t)row * jb.ldd + m0;
+        const float* xr = jb.x + (int64_t)row * jb.ldx + k0;
+        if (rv && va) {
+            const floatx4 v = ld4(dr);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[t][i] = v[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[t][i] = (rv && m0 + i < jb.M) ? dr[i] : 0.f;
+        }
+        if (rv && vb) {
+            const floatx4 v = ld4(xr);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[t][i] = v[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[t][i] = (rv && k0 + i < jb.K) ? xr[i] : 0.f;
+        }
+    }
+}
+
+// one 32-row step's products: tile i's A operand is element i of the 8 delta vectors, tile j's B operand element j
+// of the 8 x vectors; x tiles split one at a time (12 VGPRs live instead of 48); every accumulator sees the same
+// product sequence as with all four split up front
+__device__ __forceinline__ void wgrad_split_a(const float (&a)[8][4], Split3 (&as)[4], float (&bsum)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        as[i] = split3(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]});
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bsum[i] += a[t][i];
+    }
+}
+__device__ __forceinline__ void wgrad_mfma_b(const Split3 (&as)[4], const float (&b)[8][4], floatx4 (&acc)[4][4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const Split3 bs = split3(floatx4{b[0][j], b[1][j], b[2][j], b[3][j]}, floatx4{b[4][j], b[5][j], b[6][j], b[7][j]});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma_x6(as[i], bs, acc[i][j]);
+    }
+}
+__device__ __forceinline__ void wgrad_mfma_step(const float (&a)[8][4], const float (&b)[8][4], floatx4 (&acc)[4][4],
+                                                float (&bsum)[4]) {
+    Split3 as[4];
+    wgrad_split_a(a, as, bsum);
+    wgrad_mfma_b(as, b, acc);
+}
+#endif
+
 // the work of workgroup `bid` (4 waves = 4 consecutive tasks) of a wgrad launch; a __device__ function so that
 // a learner can run it as extra workgroups of another launch (learner.hip bwd4_wgrad_kernel). 256 threads.
-template <int MJ>
+template <int MJ, bool GLDS = false>
 __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __restrict__ slab, int bid) {
     // partials of the 4 waves summed pairwise in LDS, (c0 + c2) + (c1 + c3), before the one slab store per workgroup
-    // (two 16 KB slots: with the reverse recurrence's LDS, bwd4_wgrad_kernel still fits two workgroups per CU)
-    __shared__ __attribute__((aligned(16))) floatx4 wred[2][16][64];
+    // (two 16 KB slots: with the reverse recurrence's LDS, bwd4_wgrad_kernel still fits two workgroups per CU). GLDS:
+    // 16 KB of row staging per wave, the slots in waves 2 and 3's staging (their loops are over when they fill them)
+    __shared__ __attribute__((aligned(16))) floatx4 lbuf[GLDS ? 4 : 2][16][64];
+    floatx4(*wred)[16][64] = GLDS ? lbuf + 2 : lbuf;
     __shared__ float wbred[2][4][16];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int task = bid * 4 + w;
@@ -336,54 +395,106 @@ __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __r
     const bool strided = jb.skip != 0;
     const int s0 = strided ? ch : r0 >> 5, s1 = !act ? s0 : strided ? (jb.rows + 31) >> 5 : (r1 + 31) >> 5;
     const int ds = strided ? jb.chunks : 1, rend = strided ? jb.rows : r1;
-    for (int s = s0; s < s1; s += ds) {
-        const int rr = s << 5;
-        // rows with zero deltas add exactly zero: a lane's 8-row group of them loads nothing (zeros), a step with no
-        // live group is skipped
-        bool glive = rr + 8 * g < rend;
+    // rows with zero deltas add exactly zero: a lane's 8-row group of them loads nothing (zeros), a step with no live
+    // group is skipped. The wave's steps are indexed i = 0 .. nst - 1 (step s0 + i ds); their liveness is evaluated
+    // 64 steps at a time, lane l taking step index 64 win + l for the 4 row groups (four ballots), so the loop itself
+    // does no integer division. With <= 64 episodes the episode lengths sit in a register (episode e in lane e).
+    const int nst = act ? (s1 - s0 + ds - 1) / ds : 0;
+    const int nep = jb.skip == 1 ? jb.I / jb.T : jb.B;
+    const bool mreg = jb.skip && nep <= 64;
+    const float mlv = (mreg && lane < nep) ? jb.mlen[lane] : 0.f;
+    int win = -1;
+    uint64_t any = 0, mg = 0;  // steps of the window with a live group; this lane's group's live steps
+    auto group_live = [&](int row) -> bool {
+        bool gv = row < rend;
         if (jb.skip) {
-            glive = glive && bjob_row_live(jb, rr + 8 * g);
-            if (__ballot(glive) == 0) continue;
+            int eb, et;
+            if (jb.skip == 1) {
+                const int item = (row / jb.rpi) % jb.I;
+                eb = item / jb.T;
+                et = item % jb.T;
+            } else {
+                et = row / jb.R;
+                eb = ((row % jb.R) / jb.NA) % jb.B;
+            }
+            const float ml = mreg ? __shfl(mlv, eb & 63) : (gv ? jb.mlen[eb] : 0.f);
+            gv = gv && et < (int)ml;
         }
+        return gv;
+    };
+    auto next_live = [&](int i) -> int {  // first step index >= i with a live group (nst: none)
+        while (i < nst) {
+            if ((i >> 6) != win) {
+                win = i >> 6;
+                const int li = (win << 6) + lane;
+                const int rl = (s0 + li * ds) << 5;
+                const bool inr = li < nst;
+                // group_live first: its lane shuffle runs with every lane active
+                const uint64_t b0 = __ballot(group_live(rl) && inr), b1 = __ballot(group_live(rl + 8) && inr),
+                               b2 = __ballot(group_live(rl + 16) && inr), b3 = __ballot(group_live(rl + 24) && inr);
+                any = b0 | b1 | b2 | b3;
+                mg = g == 0 ? b0 : g == 1 ? b1 : g == 2 ? b2 : b3;
+            }
+            const uint64_t rem = any & (~0ull << (i & 63));
+            if (rem) return (win << 6) + __builtin_ctzll(rem);
+            i = (win + 1) << 6;
+        }
+        return nst;
+    };
+    auto live_of = [&](int i) -> bool { return (mg >> (i & 63)) & 1; };  // i in the current window
+    int i = next_live(0);
+    bool gl = i < nst && live_of(i);
+    if constexpr (GLDS) {
+        // one step ahead through LDS: the next live step's 16 row loads go global -> LDS (global_load_lds, 16 bytes
+        // per lane, this wave's 16 KB of `lbuf`) while this step's products run from VGPRs (a register copy of the
+        // next step does not fit in 256 VGPRs). Lanes whose rows are dead or past the end load row 0 and are zeroed
+        // after the read (columns past M / K are loaded as in the register path: they only reach discarded output
+        // rows / columns).
+        if (__all(va && vb)) {
+            floatx4(*stg)[64] = lbuf[w];
+            auto issue = [&](int ii, bool gv) {
+                const int rr = (s0 + ii * ds) << 5;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int row = rr + 8 * g + t;
+                    const int64_t rs = (gv && row < rend) ? row : 0;
+                    __builtin_amdgcn_global_load_lds((const void*)(jb.delta + rs * jb.ldd + m0),
+                                                     (__attribute__((address_space(3))) void*)&stg[t][0], 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void*)(jb.x + rs * jb.ldx + k0),
+                                                     (__attribute__((address_space(3))) void*)&stg[8 + t][0], 16, 0, 0);
+                }
+            };
+            if (i < nst) issue(i, gl);
+            while (i < nst) {
+                const int in = next_live(i + 1);
+                const bool gn = in < nst && live_of(in);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int rr = (s0 + i * ds) << 5;
+                float a[8][4], b[8][4];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const bool rv = gl && rr + 8 * g + t < rend;
+                    const floatx4 va4 = stg[t][lane], vb4 = stg[8 + t][lane];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        a[t][q] = rv ? va4[q] : 0.f;
+                        b[t][q] = rv ? vb4[q] : 0.f;
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads are done before the buffer refills
+                if (in < nst) issue(in, gn);
+                wgrad_mfma_step(a, b, acc, bsum);
+                i = in;
+                gl = gn;
+            }
+        }
+    }
+    while (i < nst) {
         float a[8][4], b[8][4];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int row = rr + 8 * g + t;
-            const bool rv = glive && row < rend;
-            const float* dr = jb.delta + (int64_t)row * jb.ldd + m0;
-            const float* xr = jb.x + (int64_t)row * jb.ldx + k0;
-            if (rv && va) {
-                const floatx4 v = ld4(dr);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) a[t][i] = v[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) a[t][i] = (rv && m0 + i < jb.M) ? dr[i] : 0.f;
-            }
-            if (rv && vb) {
-                const floatx4 v = ld4(xr);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) b[t][i] = v[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) b[t][i] = (rv && k0 + i < jb.K) ? xr[i] : 0.f;
-            }
-        }
-        Split3 as[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            as[i] = split3(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]});
-#pragma unroll
-            for (int t = 0; t < 8; ++t) bsum[i] += a[t][i];
-        }
-        // x tiles split one at a time (12 VGPRs live instead of 48: 256 registers, two waves per SIMD); every
-        // accumulator sees the same product sequence as with all four split up front
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const Split3 bs = split3(floatx4{b[0][j], b[1][j], b[2][j], b[3][j]}, floatx4{b[4][j], b[5][j], b[6][j], b[7][j]});
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i][j] = mfma_x6(as[i], bs, acc[i][j]);
-        }
+        wgrad_load_step(jb, (s0 + i * ds) << 5, g, gl, rend, m0, k0, va, vb, a, b);
+        wgrad_mfma_step(a, b, acc, bsum);
+        i = next_live(i + 1);
+        gl = i < nst && live_of(i);
     }
 #else
     // two 4-row steps per iteration: both steps' loads are issued before the first step's MFMAs (same
@@ -471,7 +582,11 @@ __device__ __forceinline__ void wgrad_block_body(const BJobsT<MJ>& J, float* __r
 // fixed-order sum over chunk groups -> dW / db (bias from the nbi == 0 blocks); per-block sums of squares -> nrm_part
 template <int MJ>
 __global__ void __launch_bounds__(256, 2) wgrad_block_kernel(BJobsT<MJ> J, float* __restrict__ slab) {
-    wgrad_block_body<MJ>(J, slab, (int)blockIdx.x);
+#if defined(MLG_WGRAD_NOGLDS)
+    wgrad_block_body<MJ, false>(J, slab, (int)blockIdx.x);
+#else
+    wgrad_block_body<MJ, true>(J, slab, (int)blockIdx.x);
+#endif
 }
 
 template <int MJ>
