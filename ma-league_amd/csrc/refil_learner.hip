@@ -38,6 +38,7 @@ struct RCfg {
     float gamma, lmbda;
 };
 
+constexpr int REFIL_HYPER_JOBS = 16;  // weight-gradient jobs of the 4 hypernets (make_jobs)
 constexpr int64_t REFIL_HSP = 12 * 2 * 3 * 64 * 4;  // split hypernet in_trans (hyper_split_kernel)
 struct WsR {
     int64_t pa_on, pa_tg, ph_on[4], ph_tg[4];
@@ -1581,7 +1582,7 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
     J.j[J.n++] = steps(mlg::bjob(at(p.w.dgh), 3 * EMB, at(p.w.hs_on), EMB, gp(a.c_whh), gp(a.c_bhh), 3 * EMB, EMB, TR));
     J.j[J.n++] = steps(mlg::bjob(at(p.w.d2), c.A, ws ? ws + p.w.hs_on + (int64_t)c.Ron * EMB : nullptr, EMB,
                                  gp(a.c_w3), gp(a.c_b3), c.A, EMB, TR));
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 4; ++k) {  // REFIL_HYPER_JOBS jobs, the table's last
         const RHyper& h = p.Lh;
         const int64_t G0 = p.n_agent + (int64_t)k * h.c_total;
         const int rows = nvar(k) * c.I * NAS;
@@ -1594,6 +1595,7 @@ RJobs make_jobs(Plan& p, float* ws, float* grads, int64_t* slab_floats, int* n_t
         J.j[J.n++] = items(mlg::bjob(at(p.w.dX[k]), EM, at(p.w.x2m[k]), EMB, gp(G0 + h.c_w2), gp(G0 + h.c_b2), EM, EMB,
                                      rows), NAS);
     }
+    static_assert(REFIL_HYPER_JOBS == 4 * 4, "four jobs per hypernet");
     int64_t slab_part;
     *slab_floats = mlg::layout_bjobs(J, n_tasks, n_red, &slab_part);
     p.w.nrm = p.w.slab + slab_part;
@@ -1751,6 +1753,16 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     }
     hipLaunchKernelGGL(s8 ? hyper_bwd_kernel<1> : hyper_bwd_kernel<0>, dim3((unsigned)c.I, 4), dim3(64), 0, sh, c, bt, hb,
                        ws + w.msum);
+    // weight gradients: the hypernets' jobs (the table's last REFIL_HYPER_JOBS, final after hyper_bwd) run on the side
+    // stream beside ent_bwd, the agent's after it; one reduce over the whole table (same chunk sums as one launch)
+    int64_t slab_floats, n_red;
+    int n_tasks;
+    RJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
+    int tH, tE;
+    int64_t rH, rE;
+    const RJobs JH = mlg::bjob_view(J, J.n - REFIL_HYPER_JOBS, J.n, &tH, &rH),
+               JE = mlg::bjob_view(J, 0, J.n - REFIL_HYPER_JOBS, &tE, &rE);
+    hipLaunchKernelGGL(mlg::wgrad_block_kernel<MJ>, dim3((unsigned)((tH + 3) / 4)), dim3(256), 0, sh, JH, ws + w.slab);
     if (side) MLG_REQUIRE(hipEventRecord(side->ev[3], sh) == hipSuccess, "refil learner: side stream record");
     // ---- agent backward ----
     if (rec16)
@@ -1764,12 +1776,9 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
               ws + w.dgi, ws + w.dfc2, ws + w.dout, ws + w.dqkv, ws + w.dfc1};
     hipLaunchKernelGGL(s8 ? ent_bwd_kernel<1> : ent_bwd_kernel<0>, dim3((unsigned)((c.I + 1) / 2)), dim3(64), 0, s, c, bt,
                        eb, ws + w.msum);
-    if (side) MLG_REQUIRE(hipStreamWaitEvent(s, side->ev[3], 0) == hipSuccess, "refil learner: side stream join");
     // ---- weight gradients, clip, RMSprop ----
-    int64_t slab_floats, n_red;
-    int n_tasks;
-    RJobs J = make_jobs(p, ws, bufs->grads, &slab_floats, &n_tasks, &n_red);
-    hipLaunchKernelGGL(mlg::wgrad_block_kernel<MJ>, dim3((unsigned)((n_tasks + 3) / 4)), dim3(256), 0, s, J, ws + w.slab);
+    hipLaunchKernelGGL(mlg::wgrad_block_kernel<MJ>, dim3((unsigned)((tE + 3) / 4)), dim3(256), 0, s, JE, ws + w.slab);
+    if (side) MLG_REQUIRE(hipStreamWaitEvent(s, side->ev[3], 0) == hipSuccess, "refil learner: side stream join");
     const int n_red_blocks = (int)((n_red + 255) / 256);
     hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<MJ>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + w.slab,
                        ws + p.w.nrm);
