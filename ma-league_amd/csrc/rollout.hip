@@ -2026,7 +2026,14 @@ __device__ __forceinline__ void rollout_v2_body(const MlgEnvSpec& spec, const Ml
         env_lane_step1(Ce, E, t, hl);
         sp.mark(4);
         env_lane_step2(Ce, E, t, hl, sp);
+#if defined(MLG_V7_TAIL_MIXED)
         if (!E.stepped && (t & 1)) env_lane_tail(Ce, E, 8, hl);
+#else
+        // a finished env's half-wave zeroes its slot's tail only while its partner half is idle too: in a wave whose
+        // other env still steps, the zeroing would run after that env's step (one instruction stream) and lengthen
+        // the step of the whole workgroup (barrier-bound); deferred rows are zeroed once the wave is idle or at the end
+        if (__ballot(E.stepped) == 0 && (t & 1)) env_lane_tail(Ce, E, 8, hl);
+#endif
         sp.mark(8);
         lds_barrier();
         sp.mark(10);
