@@ -304,6 +304,8 @@ typedef struct {
     float *target_sync;          /* optional (NULL = off) [n_agent + n_mixer] receives the updated parameters in the
                                     optimizer launch: the target update when due after this step
                                     (refil_learner.py:181-183 -> _update_targets; usually target_params) */
+    const int32_t *host_rows;    /* optional (NULL = off) HOST copy of the slot map (B <= mlg_qlearner_inline_rows()):
+                                    travels as a kernel argument, batch.rows is then ignored */
 } MlgRefilLearnerBufs;
 
 int64_t mlg_refil_param_counts(const MlgRefilLearnerCfg *c, int64_t *n_agent, int64_t *n_mixer);

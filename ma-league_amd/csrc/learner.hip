@@ -202,7 +202,6 @@ __device__ void mask_sum_block(const MlgBatch& bt, int B, int T, float* __restri
 // Fused learner prologue (one launch instead of eight): block 0 sums the mask (mask_sum_block); the other blocks
 // pack the online / target agent weights (pack_agent_elem), transpose W_ih (dX pass), pack the online / target
 // QMixer hypernets (pack_mixer_elem) and zero the sparse delta buffers d2 and dq.
-constexpr int MLG_INLINE_ROWS = 64;  // largest batch whose slot map travels as a kernel argument
 struct PrepJob {
     AgentLayout L;
     MlgAgentParams ap_on, ap_tg;

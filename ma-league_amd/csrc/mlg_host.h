@@ -7,6 +7,10 @@
 #include <mutex>
 #include <string>
 
+// largest batch (episodes) whose learner slot map travels as a kernel argument (MlgLearnerBufs / MlgRefilLearnerBufs
+// .host_rows; mlg_qlearner_inline_rows)
+constexpr int MLG_INLINE_ROWS = 64;
+
 namespace mlg {
 
 inline std::string& last_error() {

@@ -46,7 +46,7 @@ struct WsR {
     int64_t h_wsp[10], h_wspT[5];  // + in_trans^T split for hyper_bwd (hypernet k) / ent_bwd (agent: [4])  // in_trans as split-bf16 A operands: hypernet k of net at [k + 4 net], agent net at [8 + net]
     int64_t ein, x1, qkv, P, o, x2, x3, gi_on, gi_tg, hs_on, hs_tg, gr, gz, gn, ghn, mac, tmac;
     int64_t x1m[4], qkvm[4], Pm[4], om[4], x2m[4], X[4], Xtg[4], dX[4], doutm[4], dqkvm[4], dfc1m[4];
-    int64_t dq, d2, part, msum, dgi, dgh, dfc2, dout, dqkv, dfc1;
+    int64_t dq, d2, part, msum, dgi, dgh, dfc2, dout, dqkv, dfc1, rows;
     int64_t slab, nrm, total;
 };
 
@@ -164,6 +164,7 @@ Plan make_plan(const MlgRefilLearnerCfg* cfg, int T1) {
     w.dout = take(T * Ron * EMB);
     w.dqkv = take(I * NE * 3 * EMB);
     w.dfc1 = take(I * NE * EMB);
+    w.rows = take(MLG_INLINE_ROWS);  // int32 slot map (host_rows)
     w.slab = o;
     w.nrm = 0;
     w.total = o;
@@ -498,6 +499,9 @@ struct Prologue {
     MlgEntityBatch bt;
     float *ein, *msum;
     int nb_a, nb_h, nb_s, nb_t, nb_e;  // blocks per agent pack, hypernet pack, split block, transpose job; ein blocks
+    int n_rows_in;                     // > 0: the slot map travels here (host_rows); block 0 stores it to rows_dst
+    int32_t* rows_dst;
+    int32_t rows_in[MLG_INLINE_ROWS];
 };
 static_assert(sizeof(Prologue) <= 4096, "prologue kernel arguments over 4 KB");
 inline int prologue_blocks(const Prologue& P) {
@@ -505,9 +509,19 @@ inline int prologue_blocks(const Prologue& P) {
 }
 __global__ void __launch_bounds__(256) prologue_kernel(Prologue P) {
     __shared__ float red[256];
+    __shared__ int32_t srows[MLG_INLINE_ROWS];
+    MlgEntityBatch bt = P.bt;
+    if (P.n_rows_in > 0) {  // this launch reads the slot map from LDS, the later launches from rows_dst
+        if ((int)threadIdx.x < P.n_rows_in) {
+            srows[threadIdx.x] = P.rows_in[threadIdx.x];
+            if (blockIdx.x == 0) P.rows_dst[threadIdx.x] = P.rows_in[threadIdx.x];
+        }
+        __syncthreads();
+        bt.rows = srows;
+    }
     int blk = blockIdx.x;
     if (blk == 0) {
-        mask_sum_body(P.bt, P.c.B, P.c.T, P.msum, red);
+        mask_sum_body(bt, P.c.B, P.c.T, P.msum, red);
         return;
     }
     blk -= 1;
@@ -521,7 +535,7 @@ __global__ void __launch_bounds__(256) prologue_kernel(Prologue P) {
     blk -= 5 * P.nb_s;
     if (blk < P.tj.n * P.nb_t) return transpose_body(P.tj, blk % P.nb_t, blk / P.nb_t);
     blk -= P.tj.n * P.nb_t;
-    ein_body(P.c, P.bt, P.ein, blk);
+    ein_body(P.c, bt, P.ein, blk);
 }
 
 // ---- masks -----------------------------------------------------------------------------------------------
@@ -1609,10 +1623,12 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     const RCfg& c = p.c;
     const bool s8 = is_s8(c);  // the refil_8 shape: static instantiations of the per-item kernels
     float* ws = bufs->workspace;
-    const MlgEntityBatch& bt = bufs->batch;
+    const WsR& w = p.w;
+    MlgEntityBatch bt = bufs->batch;
+    // host slot map: the prologue's argument, stored by it to the workspace for the later launches
+    if (bufs->host_rows) bt.rows = reinterpret_cast<const int32_t*>(ws + w.rows);
     const float* params = bufs->params;
     const float* tparams = bufs->target_params;
-    const WsR& w = p.w;
     // ---- prologue, one launch: mask sum, parameter packs, in_trans splits, transposes, entity inputs ----
     Prologue P{};
     P.aj = agent_jobs(p.La);
@@ -1665,6 +1681,11 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     P.hsT.dst[4] = ws + w.h_wspT[4];
     P.c = c;
     P.bt = bt;
+    if (bufs->host_rows) {
+        P.n_rows_in = c.B;
+        P.rows_dst = reinterpret_cast<int32_t*>(ws + w.rows);
+        for (int b = 0; b < c.B; ++b) P.rows_in[b] = bufs->host_rows[b];
+    }
     P.ein = ws + w.ein;
     P.msum = ws + w.msum;
     P.nb_a = (int)((P.aj.total + 255) / 256);
@@ -1839,6 +1860,8 @@ extern "C" int mlg_refil_train(const MlgRefilLearnerCfg* c, const MlgRefilLearne
     MLG_REQUIRE(bt.entities && bt.obs_mask && bt.entity_mask && bt.actions && bt.avail && bt.reward && bt.terminated &&
                     bt.actions_onehot && bt.filled, "refil_train: batch has null tensors");
     MLG_REQUIRE(bt.B == c->B && bt.T1 >= c->T, "refil_train: batch B=%d T1=%d vs cfg B=%d T=%d", bt.B, bt.T1, c->B, c->T);
+    MLG_REQUIRE(!b->host_rows || c->B <= MLG_INLINE_ROWS, "refil_train: host_rows needs B <= %d (got %d)",
+                MLG_INLINE_ROWS, c->B);
     Plan p = make_plan(c, bt.T1);
     return run_train(p, c, b, (hipStream_t)stream);
 }

@@ -104,7 +104,8 @@ class MlgRefilLearnerCfg(ctypes.Structure):
 class MlgRefilLearnerBufs(ctypes.Structure):
     _fields_ = [("batch", MlgEntityBatch)] + [(n, ctypes.c_void_p) for n in ["groupA", "params", "grads", "square_avg",
                                                                            "target_params", "workspace", "stats",
-                                                                           "trained_steps", "target_sync"]]
+                                                                           "trained_steps", "target_sync",
+                                                                           "host_rows"]]
 
 
 _P = ctypes.c_void_p

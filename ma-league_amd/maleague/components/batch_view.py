@@ -73,11 +73,12 @@ ENTITY_DTYPES = {"entities": torch.float32, "obs_mask": torch.uint8, "entity_mas
                  "terminated": torch.uint8, "actions_onehot": torch.float32, "filled": torch.int64}
 
 
-def mlg_entity_batch(batch):
-    """Entity-scheme EpisodeBatch (REFIL, config 5) -> MlgEntityBatch. Returns (MlgEntityBatch, keepalive)."""
+def mlg_entity_batch(batch, device_rows=True):
+    """Entity-scheme EpisodeBatch (REFIL, config 5) -> MlgEntityBatch. Returns (MlgEntityBatch, keepalive).
+    device_rows=False: a sampled view's slot map is left out (rows = NULL), as in mlg_batch."""
     rows = None
     if _sampled_view(batch):
-        rows = batch.rows
+        rows = batch.rows if device_rows else None
         data = batch.ring.data.transition_data
     else:
         data = batch.data.transition_data

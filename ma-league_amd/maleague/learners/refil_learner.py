@@ -114,7 +114,11 @@ class REFILLearner(Learner):
             _native.call("mlg_refil_draw_groups", B, NE, self._group_seed, self.train_calls & 0xFFFFFFFF,
                          groupA.data_ptr(), _native.stream_ptr(self.device))
         groupA = groupA.reshape(B, NE).to(device=self.device, dtype=torch.uint8).contiguous()
-        mb, keep = mlg_entity_batch(batch)
+        # a sampled view's slot map travels as a kernel argument (no pinned host copy + H2D copy per call)
+        host_rows = getattr(batch, "host_rows", None)
+        if host_rows is not None and (B > lib.mlg_qlearner_inline_rows() or getattr(batch, "_data", None) is not None):
+            host_rows = None
+        mb, keep = mlg_entity_batch(batch, device_rows=host_rows is None)
         # trained steps accumulate on the device inside the optimizer launch (no separate add); the target update
         # due after this step (refil_learner.py:181-183) is written by that launch too (no separate copy)
         counter = self.mac.agent.trained_counter(self.device)
@@ -122,7 +126,8 @@ class REFILLearner(Learner):
         bufs = _native.MlgRefilLearnerBufs(mb, groupA.data_ptr(), self._flat.flat.data_ptr(), self._grads.data_ptr(),
                                            self._sq.data_ptr(), self._tflat.flat.data_ptr(), self._ws.data_ptr(),
                                            self._stats.data_ptr(), counter.data_ptr(),
-                                           self._tflat.flat.data_ptr() if sync else None)
+                                           self._tflat.flat.data_ptr() if sync else None,
+                                           None if host_rows is None else host_rows.ctypes.data)
         _native.call("mlg_refil_train", _native.byref(cfg), _native.byref(bufs), _native.stream_ptr(self.device))
         del keep
         self._groupA = groupA

@@ -187,3 +187,41 @@ def test_refil_learner_matches_oracle_config5_batch(device):
     for k, v in L.mixer.named_parameters():
         np.testing.assert_allclose(v.detach().cpu().numpy(), ref.mixer[k].detach().numpy(), atol=2e-5, rtol=0,
                                    err_msg=f"mixer {k}")
+
+
+def test_refil_learner_sampled_view_matches_copy(device):
+    """The bench's path: 32 episodes sampled as an in-place view of a device replay buffer (slot map handed to the
+    kernels as a kernel argument, MlgRefilLearnerBufs.host_rows) train exactly like the gathered copy of the same
+    episodes (no slot map)."""
+    from maleague.components.replay_buffer import ReplayBuffer
+    from test_gpu_refil import _rollout
+    from helpers import entity_scheme_for
+    spec, ag, a0, nb, summ, _ = _rollout(device, B=64, T=100, seed=23, eps=0.05, test_mode=False)
+    arrs = {k: np.ascontiguousarray(v) for k, v in nb.items()}
+    eb = _batch_from(arrs, device)
+    B, T1 = arrs["entities"].shape[:2]
+    info = {"n_agents": 8, "n_actions": 21, "n_entities": 16, "entity_shape": 8, "episode_limit": T1 - 1}
+    scheme, groups, pre = entity_scheme_for(info, torch)
+    buf = ReplayBuffer(scheme, groups, 80, T1, preprocess=pre, device=device)
+    buf.insert_episode_batch(eb)
+    np.random.seed(1)
+    view = buf.sample(32, view=True)
+    assert view.host_rows is not None and view.host_rows.dtype == np.int32
+    copy_ = buf[view.ep_ids]
+    a = refil_args(device="cuda")
+    torch.manual_seed(8)
+    from maleague.modules.mixers import FlexQMixer
+    mixer_p = {k: v.detach().cpu().numpy() for k, v in FlexQMixer(refil_args(device="cpu")).state_dict().items()}
+    agent_p = {k: v.detach().cpu().numpy() for k, v in ag.state_dict().items()}
+    L1, _ = _learner(eb, agent_p, mixer_p, a)
+    L2, _ = _learner(eb, agent_p, mixer_p, a)
+    g = torch.Generator().manual_seed(12)
+    for call in range(2):
+        groupA = torch.bernoulli(torch.rand(32, 1, 1, generator=g).repeat(1, 1, 16), generator=g).to(torch.uint8)
+        L1.train(view, 0, episode_num=call, groupA=groupA.to(device))
+        L2.train(copy_, 0, episode_num=call, groupA=groupA.to(device))
+        s1, s2 = L1.last_stats, L2.last_stats
+        for k in s1:
+            assert s1[k] == s2[k], (call, k, s1[k], s2[k])
+        assert torch.equal(L1._flat.flat, L2._flat.flat), call
+    assert view._rows is None  # the slot map never went to the device
