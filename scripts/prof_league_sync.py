@@ -19,7 +19,11 @@ from maleague.league import DistributedLeague, LeagueInstance  # noqa: E402
 a = types.SimpleNamespace(envs=4096, episode_limit=100, plan=None)
 args, _ = bench.make_args("league", a, 0, 0)
 lg = DistributedLeague(n_players=1, device=torch.device("cuda:0"), seed=0, max_historical=4)
-inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="matchmaking", seed=0)
+if os.environ.get("MODE", "bench") == "bench":  # the bench's N = 1 league (AlphaStar roles, bench.league_setup)
+    lmode, roles = bench.league_setup(1, args)
+    inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode=lmode, role=roles, seed=0)
+else:
+    inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode="matchmaking", seed=0)
 inst.experiment.stepper.t_env = 10 ** 6
 for _ in range(3):
     inst.sync()
