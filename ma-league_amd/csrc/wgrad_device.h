@@ -317,27 +317,21 @@ __device__ __forceinline__ void wgrad_load_step(const BJob& jb, int rr, int g, b
 // one 32-row step's products: tile i's A operand is element i of the 8 delta vectors, tile j's B operand element j
 // of the 8 x vectors; x tiles split one at a time (12 VGPRs live instead of 48); every accumulator sees the same
 // product sequence as with all four split up front
-__device__ __forceinline__ void wgrad_split_a(const float (&a)[8][4], Split3 (&as)[4], float (&bsum)[4]) {
+__device__ __forceinline__ void wgrad_mfma_step(const float (&a)[8][4], const float (&b)[8][4], floatx4 (&acc)[4][4],
+                                                float (&bsum)[4]) {
+    Split3 as[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         as[i] = split3(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]});
 #pragma unroll
         for (int t = 0; t < 8; ++t) bsum[i] += a[t][i];
     }
-}
-__device__ __forceinline__ void wgrad_mfma_b(const Split3 (&as)[4], const float (&b)[8][4], floatx4 (&acc)[4][4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const Split3 bs = split3(floatx4{b[0][j], b[1][j], b[2][j], b[3][j]}, floatx4{b[4][j], b[5][j], b[6][j], b[7][j]});
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][j] = mfma_x6(as[i], bs, acc[i][j]);
     }
-}
-__device__ __forceinline__ void wgrad_mfma_step(const float (&a)[8][4], const float (&b)[8][4], floatx4 (&acc)[4][4],
-                                                float (&bsum)[4]) {
-    Split3 as[4];
-    wgrad_split_a(a, as, bsum);
-    wgrad_mfma_b(as, b, acc);
 }
 #endif
 
