@@ -57,8 +57,12 @@ for k, cs in vals.items():
     if m.get("SQ_INSTS_MFMA"):
         d["valu_per_mfma"] = m.get("SQ_INSTS_VALU", 0.0) / m["SQ_INSTS_MFMA"]
     out[k] = d
+# annotations that are not counters (bench.py's latency floor reads them): kept when a kernel is re-collected
+KEEP = ("one_env_step_cycles", "one_env_step_source")
 if len(sys.argv) > 3 and os.path.exists(sys.argv[3]):  # merge into an existing counters.json (other kernels kept)
     prev = json.load(open(sys.argv[3])).get("kernels", {})
+    for k, d in out.items():
+        d.update({a: prev[k][a] for a in KEEP if a in prev.get(k, {}) and a not in d})
     prev.update(out)
     out = prev
 print(json.dumps({"kernels": out, "note": __doc__.strip().splitlines()[0]}, indent=1))
