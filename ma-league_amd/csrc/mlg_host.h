@@ -48,7 +48,12 @@ inline SideStream* side_stream() {
     std::lock_guard<std::mutex> lk(mu);
     SideStream& ss = side[dev];
     if (!ss.s) {
-        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        // the least priority (1 on this image; the caller's stream has the default 0): the side stream carries the
+        // work off the critical path, so the main chain's workgroups are dispatched first when both have work
+        // (REFIL learner 0.663 -> 0.658 ms; the greatest priority measured 0.677, profiles/r05/s47_side_prio_ab/)
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
+        if (hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, least) != hipSuccess) return nullptr;
         for (auto& e : ss.ev)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
