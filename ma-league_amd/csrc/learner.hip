@@ -1637,25 +1637,25 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
         params[i] = pn;
         if (tsync) tsync[i] = pn;  // target update due after this step (q_learner.py:127-128), same launch
     }
-    if (blockIdx.x == 0) {
-        float s4[4];
-        for (int k = 0; k < 4; ++k) {
-            float v = 0.f;
-            for (int j = tid; j < n_part; j += blockDim.x) v += part[(int64_t)j * 4 + k];
-            s4[k] = block_sum_1024(v, red);
-        }
+    // the four stat sums on blocks 0..3 (one each, same order as one block doing all four: bit-identical), so no
+    // block runs four block reductions after its parameter slice
+    const float ms = msum_p[0];
+    for (int k = blockIdx.x; k < 4; k += gridDim.x) {
+        float v = 0.f;
+        for (int j = tid; j < n_part; j += blockDim.x) v += part[(int64_t)j * 4 + k];
+        const float sk = block_sum_1024(v, red);
         if (tid == 0) {
-            const float ms = msum_p[0];
-            stats[0] = s4[0] / ms;
-            stats[1] = norm;
-            stats[2] = s4[1] / ms;
-            stats[3] = s4[2] / (ms * N);
-            stats[4] = s4[3] / (ms * N);
-            stats[5] = ms;
-            stats[6] = ms;
-            stats[7] = 0.f;
-            if (trained) trained[0] += (double)ms;  // Agent.trained_steps (q_learner.py:104)
+            if (k == 0) stats[0] = sk / ms;
+            else if (k == 1) stats[2] = sk / ms;
+            else stats[k + 1] = sk / (ms * N);  // k = 2, 3: stats[3], stats[4] (per agent)
         }
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+        stats[1] = norm;
+        stats[5] = ms;
+        stats[6] = ms;
+        stats[7] = 0.f;
+        if (trained) trained[0] += (double)ms;  // Agent.trained_steps (q_learner.py:104)
     }
 }
 

@@ -1549,26 +1549,32 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
         params[i] = pn;
         if (tsync) tsync[i] = pn;  // the target update due after this step (refil_learner.py:181-183), same launch
     }
-    if (blockIdx.x == 0) {
-        float s5[5];
-        for (int k = 0; k < 5; ++k) {
+    // the stat sums spread over blocks 0..3 (block 0: loss and im_loss, which combine; blocks 1..3 one each; same
+    // order as one block doing all five: bit-identical)
+    const float ms = msum_p[0];
+    for (int q = blockIdx.x; q < 4; q += gridDim.x) {
+        auto sum = [&](int k) {
             float v = 0.f;
             for (int j = tid; j < n_items; j += blockDim.x) v += part[(int64_t)j * 8 + k];
-            s5[k] = mlg::block_sum_1024(v, red);
+            return mlg::block_sum_1024(v, red);
+        };
+        if (q == 0) {
+            const float s0 = sum(0), s1 = sum(1);
+            if (tid == 0) {
+                const float loss = s0 / ms, im = s1 / ms;
+                stats[0] = (1.f - lmbda) * loss + lmbda * im;
+                stats[1] = im;
+            }
+        } else {
+            const float sk = sum(q + 1);
+            if (tid == 0) stats[q + 2] = q == 1 ? sk / ms : sk / (ms * NA);
         }
-        if (tid == 0) {
-            const float ms = msum_p[0];
-            const float loss = s5[0] / ms, im = s5[1] / ms;
-            stats[0] = (1.f - lmbda) * loss + lmbda * im;
-            stats[1] = im;
-            stats[2] = norm;
-            stats[3] = s5[2] / ms;
-            stats[4] = s5[3] / (ms * NA);
-            stats[5] = s5[4] / (ms * NA);
-            stats[6] = ms;
-            stats[7] = 0.f;
-            if (trained) trained[0] += (double)ms;
-        }
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+        stats[2] = norm;
+        stats[6] = ms;
+        stats[7] = 0.f;
+        if (trained) trained[0] += (double)ms;
     }
 }
 
