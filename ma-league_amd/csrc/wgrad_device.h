@@ -71,16 +71,17 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WJobsT<MJ> J, float* __restr
 
 // fixed-order sum over chunks -> dW, db
 __device__ __forceinline__ float block_sum_1024(float v, float* red) {
-    // deterministic tree sum over blockDim.x (power of two <= 1024) threads; result in every thread
-    const int tid = threadIdx.x;
-    red[tid] = v;
+    // deterministic sum over blockDim.x (a multiple of 64, <= 1024) threads, result in every thread: a butterfly
+    // within each wave (lane 0's fixed association), then the waves' partials in wave order -- two barriers instead
+    // of one per tree level
+    const int tid = threadIdx.x, nw = (int)(blockDim.x >> 6);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    if ((tid & 63) == 0) red[tid >> 6] = v;
     __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (tid < w) red[tid] += red[tid + w];
-        __syncthreads();
-    }
-    const float r = red[0];
-    __syncthreads();
+    float r = 0.f;
+    for (int i = 0; i < nw; ++i) r += red[i];
+    __syncthreads();  // red reusable by the caller
     return r;
 }
 
