@@ -180,7 +180,9 @@ def run_league_leg(ctx: Ctx, inst, steps: int, warmup: int, match_len: int) -> d
               "historical_matches_rank0": sum(1 for h in inst.history if h[2]),
               "historical_matches_timed_rank0": sum(1 for h in inst.history[-len(ex):] if h[2]) if ex else 0,
               "evictions": lg.evictions,
-              "payoff_games": float(lg.payoff.tensor[..., 0].sum().item())})
+              "payoff_games": float(lg.payoff.tensor[..., 0].sum().item()),
+              "teams": ([t.codes() for t in inst.teams] if getattr(inst, "teams", None) is not None else None),
+              "away_teams_rank0": sorted(set(getattr(inst, "away_teams", None) or [])) or None})
     return r
 
 
@@ -218,16 +220,31 @@ def league_setup(world: int, args):
     return "rolebased", ["main"] * world
 
 
-def league_workload(world, plan, a, roles=None):
+def league_teams(world: int, a):
+    """Every league player's team (central_worker.py:44-50, 84-93): ``n_teams`` compositions sampled by the
+    TeamComposer with the forced unit (force-unit --role HEALER --attack RANGED, unique, sorted first), one per
+    main player; at N >= 4 each team fields a main player and a main exploiter (alpha_star_league.py:23-40: player p
+    and p + N/2 share team p). ``--league-teams mirror``: every player plays the env plan mirrored (round 5)."""
+    if a.league_teams == "mirror":
+        return None, 0
+    from maleague.league.teams import compose_league_teams
+    n_teams = world if world < 4 else world // 2
+    teams = compose_league_teams(5, n_teams, "HEALER", "RANGED", unique=True, seed=0)
+    return [teams[p % n_teams] for p in range(world)], n_teams
+
+
+def league_workload(world, plan, a, roles=None, n_teams=0):
+    comp = f"composed{n_teams}teams_forceHR" if n_teams else plan
     if world >= 4:
         n_main = roles.count("main")
-        return (f"pfsp_league_{n_main}main_{world - n_main}exploiter_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
-                "BASELINE config 4 (PFSP league: main players + main exploiters, historical snapshots, RCCL)")
+        return (f"pfsp_league_{n_main}main_{world - n_main}exploiter_qmix_5v5_{comp}_{a.envs}envs_ep{a.episode_limit}",
+                "BASELINE config 4 (PFSP league: main players + main exploiters, one composed team per main / exploiter "
+                "pair, historical snapshots, RCCL)")
     if world > 1:
-        return (f"selfplay_pfsp_{world}learners_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
-                f"BASELINE config 3 (self-play QMIX, {world} learners as main players: self-play + PFSP over "
-                f"historical snapshots, opponent swap via RCCL)")
-    return (f"league_player_vs_own_snapshots_qmix_5v5_{plan}_{a.envs}envs_ep{a.episode_limit}",
+        return (f"selfplay_pfsp_{world}learners_qmix_5v5_{comp}_{a.envs}envs_ep{a.episode_limit}",
+                f"BASELINE config 3 (self-play QMIX, {world} learners as main players with their own composed teams: "
+                f"self-play + PFSP over historical snapshots, opponent swap via RCCL)")
+    return (f"league_player_vs_own_snapshots_qmix_5v5_{comp}_{a.envs}envs_ep{a.episode_limit}",
             "1-GPU league player (self-play vs its own snapshots): the per-GPU league cost, scaling denominator")
 
 
@@ -379,7 +396,8 @@ def leg_summary(L, a):
                     **{k: L[k] for k in ("league_iterations", "exchange_ms_mean", "exchange_ms_max", "exchange_frac",
                                          "collective_backend", "world_size", "opponents_rank0",
                                          "historical_snapshots", "snapshots_taken", "historical_matches_rank0",
-                                         "historical_matches_timed_rank0", "evictions", "payoff_games")},
+                                         "historical_matches_timed_rank0", "evictions", "payoff_games", "teams",
+                                         "away_teams_rank0")},
                     "note": "league scaling = league.value at N / league.value at N = 1 (same leg, same per-GPU "
                             "workload: weak scaling)"})
     return out
@@ -398,6 +416,8 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--episode-limit", type=int, default=100)
     ap.add_argument("--plan", default=None, help="match_build_plan (default medium_1h_4t; refil: refil_8)")
+    ap.add_argument("--league-teams", dest="league_teams", default="composed", choices=["composed", "mirror"],
+                    help="league leg: per-player TeamComposer compositions (default) or the plan mirrored")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-every", type=int, default=1,
@@ -488,8 +508,10 @@ def main():
             from maleague.league import DistributedLeague, LeagueInstance
             lg = DistributedLeague(n_players=world, device=dev, seed=0, max_historical=4 * world)
             lmode, roles = league_setup(world, args)
-            inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode=lmode, role=roles, seed=0)
-            workload, cfg_name = league_workload(world, plan, a, roles)
+            pteams, n_teams = league_teams(world, a)
+            inst = LeagueInstance(args, MainLogger(log_interval=10 ** 12), lg, mode=lmode, role=roles, seed=0,
+                                  teams=pteams)
+            workload, cfg_name = league_workload(world, plan, a, roles, n_teams)
             exp = inst.experiment
             parallelism = f"league{world}_{lg.backend}"
         stepper = exp.stepper
@@ -539,7 +561,7 @@ def main():
                                                "exchange_frac", "collective_backend", "world_size",
                                                "opponents_rank0", "historical_snapshots", "snapshots_taken",
                                                "historical_matches_rank0", "historical_matches_timed_rank0",
-                                               "evictions")}
+                                               "evictions", "teams", "away_teams_rank0")}
         if "league" in results and head != "league":
             out["league"] = leg_summary(results["league"], a)
         if "refil" in results and head != "refil":

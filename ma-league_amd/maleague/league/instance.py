@@ -24,6 +24,7 @@ from ..runs.sp_ma_experiment import agent_vector, load_agent_vector
 from .distributed import DistributedLeague
 from .matchmaking import REGISTRY as matchmaking_REGISTRY
 from .roles import ROLES, Historical, LeagueView, alphastar_roles
+from .teams import match_plan
 
 
 class LeagueInstance:
@@ -31,10 +32,20 @@ class LeagueInstance:
     learner) or "rolebased" (``role`` in simple/main/main_exploiter/league_exploiter)."""
 
     def __init__(self, args, logger, league: DistributedLeague, mode="matchmaking", role=None, seed=0,
-                 experiment=None):
+                 experiment=None, teams=None):
+        """``teams``: the league's Team of every player (index = pid; league.teams.compose_league_teams, one team
+        per player as CentralWorker assigns them, central_worker.py:84-93). Each match then puts this player's team
+        against the opponent's (a historical snapshot plays its parent's team). None: every player plays the
+        env config's own plan, mirrored."""
         self.args, self.logger, self.league = args, logger, league
         self.pid = league.player()
         self.mode = mode
+        if teams is not None and len(teams) != league.n:
+            raise ValueError(f"{len(teams)} teams for a league of {league.n} players (one team per player)")
+        self.teams = list(teams) if teams is not None else None
+        self.home_team = self.teams[self.pid] if self.teams is not None else None
+        self.away_team = None
+        self.away_teams = []  # the away roster (codes) of every match, in order
         rng = np.random.RandomState(seed * 1000 + self.pid)
         if mode == "rolebased":
             roles = role if isinstance(role, (list, tuple)) else [role or "simple"] * league.n
@@ -52,8 +63,7 @@ class LeagueInstance:
         if experiment is None:
             sp_args = copy.deepcopy(args)
             sp_args.env_args = dict(args.env_args)
-            sp_args.env_args["match_build_plan"] = mirror_plan(args.env_args["match_build_plan"], ai=False,
-                                                                config_dir=getattr(args, "config_dir", None))
+            sp_args.env_args["match_build_plan"] = self._plan(ai=False)
             experiment = LeagueExperiment(sp_args, logger)
             experiment._init_stepper()
         self.experiment = experiment
@@ -61,18 +71,39 @@ class LeagueInstance:
         self.history = []  # (league iteration, opponent pid, historical?)
         self.episode = 0
 
+    def _plan(self, ai: bool):
+        """The home team mirrored (league_experiment_process.py:57-62 with away=None): this player's league team,
+        or the env config's own plan when the league has no team compositions."""
+        if self.home_team is not None:
+            return match_plan(self.home_team, ai=ai)
+        return mirror_plan(self.args.env_args["match_build_plan"], ai=ai, config_dir=getattr(self.args, "config_dir", None))
+
+    def team_of(self, pid: int):
+        """The Team a league pid plays: a player's own, a historical snapshot its parent's (None without teams)."""
+        if self.teams is None:
+            return None
+        if pid < self.league.n:
+            return self.teams[pid]
+        parents = [p for h, p, _ in self.league.historical_meta if h == pid]
+        if not parents:
+            raise KeyError(f"league pid {pid} is neither a player nor a stored historical snapshot")
+        return self.teams[parents[0]]
+
     # ---- phases -------------------------------------------------------------------------------------------
-    def pretrain_vs_ai(self, iterations: int):
-        """matchmaking_league_instance.py:21-25: initial play against the mirrored scripted AI."""
-        if iterations <= 0:
+    def pretrain_vs_ai(self, iterations: int = 0, play_time_seconds: float = None):
+        """matchmaking_league_instance.py:21-25: initial play against the mirrored scripted AI, for ``iterations``
+        training iterations or ``play_time_seconds`` of wall time (the reference's play_time_mins)."""
+        if iterations <= 0 and not play_time_seconds:
             return
         ai_args = copy.deepcopy(self.args)
         ai_args.env_args = dict(self.args.env_args)
-        ai_args.env_args["match_build_plan"] = mirror_plan(self.args.env_args["match_build_plan"], ai=True,
-                                                            config_dir=getattr(self.args, "config_dir", None))
+        ai_args.env_args["match_build_plan"] = self._plan(ai=True)
         exp = MultiAgentExperiment(ai_args, self.logger)
         load_agent_vector(exp.home_mac, agent_vector(self.experiment.home_mac))
-        exp.start(max_iterations=iterations)
+        if play_time_seconds:
+            exp.start(play_time_seconds=play_time_seconds)
+        else:
+            exp.start(max_iterations=iterations)
         self.experiment.load_home_agent(exp.home_mac.agent.state_dict())
         del exp
 
@@ -109,6 +140,10 @@ class LeagueInstance:
             return None
         self.opponent = int(opp)
         self.experiment.load_adversary_vector(self.league.params_of(self.opponent))
+        if self.teams is not None:  # the adversary's roster (matchmaking_league_instance.py:52, :61-62)
+            self.away_team = self.team_of(self.opponent)
+            self.away_teams.append(self.away_team.codes())
+            self.experiment.configure_match(self.home_team, self.away_team)
         self.history.append((len(self.history), self.opponent, bool(hist)))
         return self.opponent, hist
 
@@ -130,6 +165,18 @@ class LeagueInstance:
             info = st.last_run_info() if hasattr(st, "last_run_info") else st._info
             self.league.record_runs(self.pid, self.opponent, info[B:3 * B].view(B, 2), info[3 * B:4 * B])
             self.episode += B
+
+    def play_for(self, seconds: float, max_iterations: int = None) -> int:
+        """A match of ``seconds`` wall time (the reference's ``start(play_time_seconds=play_time_mins * 60)``,
+        matchmaking_league_instance.py:64): training iterations until the time is up (at least one), or
+        ``max_iterations``. Returns the iterations played. Ranks play their matches independently; they meet
+        again at the next sync()."""
+        import time
+        t0, n = time.perf_counter(), 0
+        while n == 0 or (time.perf_counter() - t0 < seconds and (max_iterations is None or n < max_iterations)):
+            self.play(1)
+            n += 1
+        return n
 
     def run(self, league_iterations: int, iterations_per_match: int, pretrain_iterations: int = 0):
         self.pretrain_vs_ai(pretrain_iterations)

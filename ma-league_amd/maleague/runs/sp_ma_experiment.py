@@ -115,3 +115,11 @@ class LeagueExperiment(SelfPlayMultiAgentExperiment):
     def load_home_agent(self, agent: OrderedDict):
         self.home_mac.load_state_dict(agent=agent)
         del agent
+
+    def configure_match(self, home, away=None):
+        """LeagueExperimentInstance._configure_experiment(home, away, ai=False) (league_experiment_process.py:57-62):
+        plan team 0 = the home team's roster, team 1 = the adversary's (the home roster mirrored when ``away`` is
+        None). ``home`` / ``away``: league Teams or match_build_plan unit lists. The reference builds a new
+        LeagueExperiment (env, buffer, optimizer) per match; here the stepper swaps the env spec in place."""
+        from ..league.teams import match_plan
+        self.stepper.set_match_build_plan(match_plan(home, away))

@@ -148,6 +148,27 @@ class ParallelStepper(EnvStepper):
     def _build_spec(self, env_args, config_dir):
         return TeamsEnvSpec.from_env_args(env_args, config_dir)
 
+    def set_match_build_plan(self, plan):
+        """Swap the env's team rosters between runs (a league match: home team vs the adversary's team,
+        league_experiment_process.py:57-62, where the reference rebuilds the whole experiment and its env). The new
+        plan must keep the env's shape (units, agents, actions, policy team) -- the batches, replay buffer and MACs
+        stay valid; the roles / attack types of every unit follow the plan. The spec travels by value as a kernel
+        argument, so runs already queued keep the rosters they were launched with."""
+        env_args = dict(self.args.env_args)
+        env_args["match_build_plan"] = plan
+        env_args.setdefault("seed", getattr(self.args, "seed", 0))
+        spec = self._build_spec(env_args, getattr(self.args, "config_dir", None))
+        old = self.spec
+        if (spec.U, spec.n_agents, spec.n_actions, spec.policy_team, spec.n_policy_teams) != \
+                (old.U, old.n_agents, old.n_actions, old.policy_team, old.n_policy_teams):
+            raise ValueError(f"match_build_plan changes the env shape (U {old.U} -> {spec.U}, agents {old.n_agents} -> "
+                             f"{spec.n_agents}, policy teams {old.n_policy_teams} -> {spec.n_policy_teams}): a "
+                             "roster swap keeps the team sizes")
+        self.args.env_args = env_args
+        self.spec = spec
+        self.envs.spec = spec
+        self._cspec = spec.to_c()
+
     def _to_mlg(self, batch):
         return mlg_batch(batch)
 

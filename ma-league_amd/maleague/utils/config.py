@@ -58,6 +58,18 @@ BUILTIN = {
         "test_greedy": True, "test_nepisode": 32, "test_interval": 10000, "log_interval": 10000,
         "runner_log_interval": 10000, "learner_log_interval": 10000, "t_max": 2050000, "show_exp_parameters": True,
     },
+    # src/config/leagues/matchmaking.yaml (the league layer: per-match play time, league run time, matchmaking)
+    "leagues/matchmaking": {
+        "play_time_mins": 120, "league_runtime_hours": 24, "n_league_evaluation_episodes": 100,
+        "show_exp_parameters": True, "buffer_cpu_only": False, "mac": "basic", "headless_controls": False,
+        "use_cuda": True, "use_tensorboard": True, "matchmaking": "pfsp",
+    },
+    # src/config/leagues/test.yaml (a short league: 1-minute matches, 6 minutes in all)
+    "leagues/test": {
+        "team_size": 5, "play_time_mins": 1, "league_runtime_hours": 0.1, "n_league_evaluation_episodes": 1,
+        "show_exp_parameters": True, "env_args": {"record": False, "fps": 60}, "buffer_cpu_only": True,
+        "mac": "basic", "headless_controls": False, "use_cuda": True, "use_tensorboard": True, "matchmaking": "pfsp",
+    },
     "algs/vdn": {
         "action_selector": "epsilon_greedy", "epsilon_start": 1.0, "epsilon_finish": 0.05,
         "epsilon_anneal_time": 50000, "runner": "episode", "buffer_size": 5000, "target_update_interval": 200,

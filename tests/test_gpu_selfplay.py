@@ -26,8 +26,9 @@ SP7_MAX_DIVERGING = {"medium_1h_4t": 2, "small": 2, "medium": 2}  # measured 0 /
 
 def _sp_args(B, episode_limit, seed, plan="medium_1h_4t", **kw):
     from maleague.envs.plans import builtin_plan
+    mbp = builtin_plan(plan, self_play=True) if isinstance(plan, str) else plan
     return qmix_args(batch_size_run=B, seed=seed,
-                     env_args={"match_build_plan": builtin_plan(plan, self_play=True), "grid_size": 20,
+                     env_args={"match_build_plan": mbp, "grid_size": 20,
                                "stochastic_spawns": True, "episode_limit": episode_limit}, **kw)
 
 
@@ -212,7 +213,7 @@ def test_selfplay_headline_shape_properties(device):
 
 def test_selfplay_headline_shape_agent_parity(device):
     """config 3 at its full shape (5v5 self-play, 4096 envs, episode_limit 100, train mode at the
-    steady-state epsilon 0.05 on both sides, the sp7 kernel): 64 envs spread over the launch, BOTH sides, replayed
+    steady-state epsilon 0.05 on both sides, the sp8 kernel -- the default for this shape): 64 envs spread over the launch, BOTH sides, replayed
     through the oracle self-play stepper + C env (both batches and returns bit-exact) and the fp32 oracle MAC of each
     side -- every epsilon draw bit-exact vs the counter RNG, every greedy pick the oracle's argmax (near ties within
     Q_TOL). self_play_stepper.py:44-147, basic_controller.py:29-36."""
@@ -225,6 +226,82 @@ def test_selfplay_headline_shape_agent_parity(device):
     n = _check_sides(stepper, (home, away), args, (hb, ab), infos, episode=0, test_mode=False, eps=eps, envs=sub)
     print(f"config-3 full-shape agent parity: {n}")
     assert n["greedy"] > 10000 and n["epsilon_draws"] > 0
+
+
+def _composed_teams(k=2, seed=0):
+    from maleague.league.teams import compose_league_teams
+    teams = compose_league_teams(5, k, "HEALER", "RANGED", seed=seed)
+    assert len({t.codes() for t in teams}) == k
+    return teams
+
+
+def test_selfplay_composed_teams_headline_shape_parity(device):
+    """a league match between two DIFFERENT composed 5-unit teams (TeamComposer, force-unit HEALER /
+    RANGED; team_composer.py:82-181, matchmaking_league_instance.py:52-62) at the config-3 shape: 4096 envs, train
+    mode at epsilon 0.05, the sp8 kernel. 64 envs of BOTH sides teacher-forced through the oracle self-play stepper +
+    C env (batches and returns bit-exact) and each side's fp32 oracle MAC (epsilon draws bit-exact, greedy picks
+    within Q_TOL); the env spec carries the home roster in team 0 and the adversary's in team 1."""
+    from maleague.envs.teams_env import ATTACK_IDS, ROLE_IDS
+    from maleague.league.teams import match_plan
+    home_t, away_t = _composed_teams()
+    stepper, home, away, args = _build(device, plan=match_plan(home_t, away_t), B=4096, episode_limit=100, seed=0)
+    sp = stepper.spec
+    for side, t in ((0, home_t), (1, away_t)):
+        assert sp.role[5 * side:5 * side + 5] == [ROLE_IDS[u["role"].name] for u in t.units]
+        assert sp.melee[5 * side:5 * side + 5] == [ATTACK_IDS[u["attack_type"].name] for u in t.units]
+    assert sp.role[:5] != sp.role[5:] or sp.melee[:5] != sp.melee[5:]
+    stepper.t_env = 10 ** 6
+    hb, ab, infos = stepper.run(test_mode=False)
+    sub = np.linspace(0, 4095, 64).astype(int)
+    eps = tuple(float(e) for e in stepper.epsilons)
+    n = _check_sides(stepper, (home, away), args, (hb, ab), infos, episode=0, test_mode=False, eps=eps, envs=sub)
+    print(f"composed teams {home_t.codes()} vs {away_t.codes()}: {n}")
+    assert n["greedy"] > 10000 and n["epsilon_draws"] > 0
+
+
+def test_selfplay_roster_swap_between_runs(device):
+    """ParallelStepper.set_match_build_plan (the league's opponent swap): the next run plays the new away roster --
+    bit-exact against the C env built from the new spec -- while the batches, MACs and env state stay in place; a
+    plan that changes the env's shape is refused."""
+    from maleague.league.teams import match_plan
+    t = _composed_teams(3, seed=4)
+    stepper, home, away, args = _build(device, plan=match_plan(t[0], t[1]), B=256, episode_limit=40, seed=6)
+    hb, ab, infos = stepper.run(test_mode=True)
+    _check_sides(stepper, (home, away), args, (hb, ab), infos, episode=0, test_mode=True, eps=(0.0, 0.0))
+    stepper.set_match_build_plan(match_plan(t[0], t[2]))
+    assert stepper.spec.role[5:] == [{"TANK": 0, "HEALER": 1, "ADC": 2}[u["role"].name] for u in t[2].units]
+    hb, ab, infos = stepper.run(test_mode=True)
+    _check_sides(stepper, (home, away), args, (hb, ab), infos, episode=1, test_mode=True, eps=(0.0, 0.0))
+    from maleague.league.teams import compose_league_teams
+    small = compose_league_teams(3, 1, "HEALER", "RANGED", seed=0)[0]
+    with pytest.raises(ValueError):
+        stepper.set_match_build_plan(match_plan(t[0], small))
+
+
+def test_league_instance_composed_teams_gpu(device):
+    """A league player with its own composed team on the GPU (player 1 of a 2-player league whose player 0 is a fixed
+    replica with another team): every match puts the adversary's roster into the self-play env spec's away units."""
+    from maleague.custom_logging import MainLogger
+    from maleague.league import DistributedLeague, LeagueInstance, PayoffEntry
+    from maleague.runs.sp_ma_experiment import agent_vector
+    teams = _composed_teams(2, seed=1)
+    lg = DistributedLeague(n_players=2, device=device, max_historical=3, player_id=1)
+    inst = LeagueInstance(_league_args(1024, 60), MainLogger(), lg, mode="rolebased",
+                          role=["main", "main_exploiter"], seed=1, teams=teams)
+    ex = inst.experiment
+    assert ex.stepper.spec.role[:5] == ex.stepper.spec.role[5:]  # mirrored before the first match
+    lg.set_player_params(0, agent_vector(ex.home_mac).clone() * 0.5)
+    for _ in range(2):
+        assert inst.sync() == (0, False)
+        sp = ex.stepper.spec
+        assert inst.away_team == teams[0] and inst.home_team == teams[1]
+        assert sp.role[5:] == [u["role"].value["id"] for u in teams[0].units]
+        assert sp.role[:5] == [u["role"].value["id"] for u in teams[1].units]
+        inst.play(1)
+    lg.sync_payoff()
+    torch.cuda.synchronize()
+    assert float(lg.payoff.tensor[1, 0, PayoffEntry.GAMES]) == 2 * 1024
+    assert inst.away_teams == [teams[0].codes()] * 2
 
 
 def test_selfplay_episode_stepper(device):

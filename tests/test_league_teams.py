@@ -1,0 +1,257 @@
+"""The team-composition league on CPU:
+
+* every league player owns its own composed team, and at every opponent swap the self-play env spec's away
+  units take the opponent's roster (a historical snapshot: its parent's) -- matchmaking_league_instance.py:44-62,
+  league_experiment_process.py:57-62 -- over gloo at world size 4 (matchmaking) and 8 (the exact config-4 shape:
+  AlphaStar roles, a main player and a main exploiter per team);
+* the league entry point (maleague/league/main.py, central_worker_main.py:28-111): argument parsing, player layout
+  and a gloo world-4 dry run (teams composed identically on every rank, one exchange).
+
+The learner is a stand-in (no GPU here); the env spec is the product's (TeamsEnvSpec from the match plan).
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Agent(torch.nn.Module):
+    def __init__(self, rank):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.full((6,), float(rank)))
+        self.trained_steps = 0
+
+
+class _MAC:
+    def __init__(self, rank):
+        self.agent = _Agent(rank)
+
+
+class _Stepper:
+    def __init__(self, B):
+        self.batch_size = B
+        self._info = torch.zeros(6 * B, dtype=torch.int32)
+        self.t_env = 0
+
+
+class _TeamExperiment:
+    """LeagueExperiment stand-in whose configure_match builds the product's env spec from the match plan (what
+    ParallelStepper.set_match_build_plan installs) and records it per match."""
+
+    def __init__(self, rank, B=16):
+        self.home_mac, self.away_mac = _MAC(rank), _MAC(-1)
+        self.stepper = _Stepper(B)
+        self.rng = np.random.RandomState(rank)
+        self.specs = []
+
+    def load_adversary_vector(self, vec):
+        with torch.no_grad():
+            self.away_mac.agent.w.copy_(vec)
+
+    def configure_match(self, home, away=None):
+        from maleague.envs.teams_env import TeamsEnvSpec
+        from maleague.league.teams import match_plan
+        spec = TeamsEnvSpec.from_env_args({"match_build_plan": match_plan(home, away)})
+        parents = {h: p for h, p, _ in self.league.historical_meta}  # the snapshot -> parent map at match time
+        self.specs.append((list(spec.role), list(spec.melee), list(spec.team), spec.n_agents, parents))
+
+    def _train_episode(self, episode):
+        B = self.stepper.batch_size
+        self.stepper._info[B:3 * B] = torch.from_numpy(self.rng.randint(0, 2, 2 * B).astype(np.int32))
+        self.stepper._info[3 * B:4 * B] = torch.from_numpy(self.rng.randint(0, 2, B).astype(np.int32))
+        self.home_mac.agent.trained_steps += B * 10
+        with torch.no_grad():
+            self.home_mac.agent.w.add_(1.0)
+
+
+def _worker(rank, world, port, experiment, league_size, out, iters, staged=None):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, os.path.join(ROOT, "ma-league_amd"))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from types import SimpleNamespace
+    from maleague.league import DistributedLeague, LeagueInstance
+    from maleague.league.main import player_layout
+    from maleague.league.teams import compose_league_teams
+    if staged is not None:  # force the collective branch: host-staged (gloo + GPU) or in place (RCCL's)
+        DistributedLeague._host_staged = lambda self: staged
+    args = SimpleNamespace(matchmaking="pfsp", league_checkpoint_min_steps=300, league_checkpoint_max_steps=600,
+                           env_args={})
+    teams = compose_league_teams(5, league_size, "HEALER", "RANGED", seed=11)
+    roles, team_idx = player_layout(experiment, league_size)
+    lg = DistributedLeague(n_players=world, device="cpu", seed=0, max_historical=3)
+    exp = _TeamExperiment(rank)
+    exp.league = lg
+    inst = LeagueInstance(args, None, lg, mode="matchmaking" if roles[0] is None else "rolebased",
+                          role=None if roles[0] is None else roles, seed=0, experiment=exp,
+                          teams=[teams[i] for i in team_idx])
+    hist = inst.run(league_iterations=iters, iterations_per_match=2)
+    # every match's away team, resolved from the replicated metadata as it stood at that match
+    out.put((rank, hist, exp.specs, [t.to_json() for t in teams], team_idx, roles,
+             lg.payoff.tensor.numpy().tolist(), list(lg.historical_meta), lg.evictions,
+             [(p.pid, p.trained_steps) for p in inst.players] if roles[0] else None))
+    dist.destroy_process_group()
+
+
+def _run(world, experiment, league_size, iters=6, staged=None):
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, experiment, league_size, q, iters, staged))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _roster(team_json):
+    from maleague.envs.teams_env import ATTACK_IDS, ROLE_IDS
+    roles = [ROLE_IDS[u["role"]["__enum__"].split(".")[1]] for u in team_json["units"]]
+    melee = [ATTACK_IDS[u["attack_type"]["__enum__"].split(".")[1]] for u in team_json["units"]]
+    return roles, melee
+
+
+def _check_rosters(res, world, n_players):
+    teams = res[0][3]
+    n_hist = 0
+    for rank, hist, specs, tj, team_idx, roles, pay, meta, _, _ in res:
+        assert tj == teams  # identical composition on every rank
+        assert len(specs) == len(hist)
+        home_roles, home_melee = _roster(teams[team_idx[rank]])
+        for (_, opp, is_hist), (role, melee, team, n_agents, parents) in zip(hist, specs):
+            assert n_agents == 10 and team == [0] * 5 + [1] * 5
+            assert role[:5] == home_roles and melee[:5] == home_melee  # home = this player's team
+            assert is_hist == (opp >= n_players)
+            parent = parents[opp] if is_hist else opp  # a snapshot plays its parent's team
+            n_hist += is_hist
+            away_roles, away_melee = _roster(teams[team_idx[parent]])
+            assert role[5:] == away_roles and melee[5:] == away_melee, (rank, opp, parent)
+        np.testing.assert_array_equal(np.array(pay), np.array(res[0][6]))
+        assert meta == res[0][7]
+    return teams, n_hist
+
+
+def test_league_rosters_gloo_world4_matchmaking():
+    """4 learners, 4 composed teams, PFSP matchmaking: every match's env spec = (own team, opponent's team)."""
+    res = _run(4, "matchmaking", 4)
+    teams, _ = _check_rosters(res, 4, 4)
+    assert len({json.dumps(t) for t in teams}) == 4  # four different compositions
+    opps = {opp for r in res for _, opp, _ in r[1]}
+    assert len(opps) > 1  # different opponents -> different away rosters across the league
+
+
+def test_league_config4_gloo_world8_alphastar():
+    """the exact config-4 shape -- 8 ranks, 4 teams, each with a main player and a main exploiter
+    (alpha_star_league.py:23-40) -- run past the historical capacity (3 slots): payoff, historical metadata and
+    evictions identical on every rank; exploiters face main players (or their snapshots) only; every match's
+    env spec holds the opponent's (parent's) roster."""
+    res = _run(8, "alphastar", 4, iters=10)
+    roles = res[0][5]
+    assert roles == ["main", "main_exploiter"] * 4 and res[0][4] == [0, 0, 1, 1, 2, 2, 3, 3]
+    _, n_hist = _check_rosters(res, 8, 8)
+    assert n_hist > 0  # historical snapshots were played with their parents' rosters
+    meta0, ev0 = res[0][7], res[0][8]
+    assert len(meta0) == 3 and ev0 > 0, (meta0, ev0)  # pool filled, snapshots evicted
+    for r in res:
+        assert r[7] == meta0 and r[8] == ev0
+    mains = [p for p, role in enumerate(roles) if role == "main"]
+    for rank, hist, *_ in res:
+        if roles[rank] == "main_exploiter":
+            for _, opp, is_hist in hist:
+                assert opp in mains or is_hist
+
+
+def test_collective_branches_agree_gloo_world4():
+    """DistributedLeague's in-place collective branch (the one RCCL takes: all_reduce / all_gather on
+    the league's own tensors) and its host-staged branch (gloo with GPU tensors) give the same league -- payoff,
+    historical pool, matches -- on every rank (CPU tensors over gloo, the branch forced each way)."""
+    a = _run(4, "alphastar", 2, iters=6, staged=False)
+    b = _run(4, "alphastar", 2, iters=6, staged=True)
+    for ra, rb in zip(a, b):
+        assert ra[1] == rb[1]  # matches (iteration, opponent, historical?)
+        np.testing.assert_array_equal(np.array(ra[6]), np.array(rb[6]))
+        assert ra[7] == rb[7] and ra[8] == rb[8]
+        assert [x[:4] for x in ra[2]] == [x[:4] for x in rb[2]]
+
+
+def test_parse_reference_command_line():
+    """SURVEY §3.1's command line parses (force-unit after the config overrides and vice versa)."""
+    from maleague.league.main import parse, player_layout
+    a, ov = parse(["--config=qmix", "--env-config=ma", "--league-config=matchmaking", "--experiment=matchmaking",
+                   "--matchmaking=pfsp", "--league_size=8", "--team_size=5", "--batch_size_run=4096",
+                   "--env_args.episode_limit=100", "force-unit", "--role=HEALER", "--attack=RANGED"])
+    assert (a.league_size, a.team_size, a.experiment, a.matchmaking) == (8, 5, "matchmaking", "pfsp")
+    assert (a.role, a.attack, a.unique) == ("HEALER", "RANGED", True)
+    assert ov == ["--batch_size_run=4096", "--env_args.episode_limit=100"]
+    a, ov = parse(["--config=qmix", "--env-config=ma", "--league-config=test", "--experiment=alphastar",
+                   "--league_size=4", "force-unit", "--role=healer", "--attack=melee", "--runner=parallel"])
+    assert (a.role, a.attack) == ("HEALER", "MELEE") and ov == ["--runner=parallel"]
+    a, _ = parse(["--config=qmix", "--env-config=ma", "--league-config=matchmaking"])
+    assert a.role is None and a.cmd is None
+    with pytest.raises(SystemExit):
+        parse(["--config=qmix", "--env-config=ma", "--league-config=matchmaking", "stray"])
+    assert player_layout("alphastar", 2, 1, 1)[0] == ["main", "main_exploiter", "league_exploiter"] * 2
+    assert player_layout("rolebased", 3) == (["simple"] * 3, [0, 1, 2])
+
+
+def test_league_configs_layered():
+    from maleague.utils.config import build_config
+    cfg = build_config("qmix", "ma", league="matchmaking", overrides=["--play_time_mins=0.5"], cuda_available=False)
+    assert cfg["play_time_mins"] == 0.5 and cfg["league_runtime_hours"] == 24 and cfg["matchmaking"] == "pfsp"
+    assert cfg["buffer_cpu_only"] is False  # league layer over the env layer, under the algorithm layer
+
+
+def _main_worker(rank, world, port, argv, out):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    sys.path.insert(0, os.path.join(ROOT, "ma-league_amd"))
+    os.chdir(out[1])
+    from maleague.league.main import main
+    s = main(argv)
+    out[0].put((rank, s))
+
+
+def test_league_main_dry_run_gloo_world4(tmp_path):
+    """The entry point at world 4 (alphastar, 2 teams x (main + main exploiter)): every rank composes the same teams,
+    rank 0 writes league_config.json with every player's role and roster, one exchange ran over gloo."""
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    argv = ["--config=qmix", "--env-config=ma", "--league-config=matchmaking", "--experiment=alphastar",
+            "--league_size=2", "--team_size=5", "--dry-run", "--seed=3", f"--local_results_path={tmp_path}",
+            "force-unit", "--role=HEALER", "--attack=RANGED"]
+    procs = [ctx.Process(target=_main_worker, args=(r, 4, port, argv, (q, str(tmp_path)))) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s0 = res[0][1]
+    assert all(s["team_tids"] == s0["team_tids"] for _, s in res)
+    assert [p["role"] for p in s0["players"]] == ["main", "main_exploiter"] * 2
+    assert [p["team"]["tid"] for p in s0["players"]] == [s0["team_tids"][0]] * 2 + [s0["team_tids"][1]] * 2
+    assert all(p["codes"].startswith("HR") for p in s0["players"])
+    assert s0["params_of"] == [float(p["team"]["tid"]) for p in s0["players"]]
+    assert s0["payoff_wins"] == 1 + 2 + 3 + 4 and s0["collective_backend"] == "gloo"
+    with open(os.path.join(s0["log_dir"], "league_config.json")) as f:
+        saved = json.load(f)
+    assert saved["team_tids"] == s0["team_tids"] and saved["force_unit"] == ["HEALER", "RANGED", True]
