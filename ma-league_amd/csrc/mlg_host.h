@@ -34,17 +34,21 @@ inline int check_launch(const char* what) {
     return 0;
 }
 
-// A second stream of the current device for learner kernels that run beside the main chain (forked and joined with
-// the events; one stream and four events per device, created on first use, never destroyed). nullptr on failure.
+// A second stream on the device of the caller's stream `s`, for learner kernels that run beside the main chain (forked
+// and joined with the events; one stream and four events per device, created on first use, never destroyed).
+// nullptr -- the caller then runs everything on `s` -- when `s`'s device is not the current device (the side stream
+// would land on the wrong device) or when creating the stream or its events fails (nothing half-built is published).
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
-inline SideStream* side_stream() {
+inline SideStream* side_stream(hipStream_t caller) {
     static SideStream side[64];
     static std::mutex mu;
     int dev = 0;
+    hipDevice_t sdev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (hipStreamGetDevice(caller, &sdev) != hipSuccess || (int)sdev != dev) return nullptr;
     std::lock_guard<std::mutex> lk(mu);
     SideStream& ss = side[dev];
     if (!ss.s) {
@@ -53,9 +57,18 @@ inline SideStream* side_stream() {
         // (REFIL learner 0.663 -> 0.658 ms; the greatest priority measured 0.677, profiles/r05/s47_side_prio_ab/)
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
-        if (hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, least) != hipSuccess) return nullptr;
-        for (auto& e : ss.ev)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        SideStream fresh;
+        for (auto& e : fresh.ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                for (auto& x : fresh.ev)
+                    if (x) (void)hipEventDestroy(x);
+                return nullptr;
+            }
+        if (hipStreamCreateWithPriority(&fresh.s, hipStreamNonBlocking, least) != hipSuccess) {
+            for (auto& x : fresh.ev) (void)hipEventDestroy(x);
+            return nullptr;
+        }
+        ss = fresh;  // published only once complete
     }
     return &ss;
 }

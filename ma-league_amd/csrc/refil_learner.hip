@@ -1700,8 +1700,9 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     P.nb_t = (3 * EMB * EMB + 255) / 256;
     P.nb_e = (int)(((int64_t)c.I * NE * c.K1 + 255) / 256);
     hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)prologue_blocks(P)), dim3(256), 0, s, P);
-    static const bool one_stream = getenv("MLG_REFIL_ONE_STREAM") != nullptr;
-    mlg::SideStream* side = one_stream ? nullptr : mlg::side_stream();
+    // read per call: a test can compare the one-stream and side-stream forms within one process
+    const bool one_stream = getenv("MLG_REFIL_ONE_STREAM") != nullptr;
+    mlg::SideStream* side = one_stream ? nullptr : mlg::side_stream(s);
     const hipStream_t sh = side ? side->s : s;  // the hypernet kernels' stream
     if (side) {
         MLG_REQUIRE(mlg::fork_join(side, 0, s, sh), "refil learner: side stream fork");

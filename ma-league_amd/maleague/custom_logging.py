@@ -134,8 +134,14 @@ class _Series:
         self._n += 1
 
     def extend_array(self, a):
-        a = np.asarray(a)
-        self._items.append(_Chunk(a.reshape(-1)))
+        """Arrays are copied (a caller changing its array in place later must not change unlogged stats); lists and
+        tuples stay Python values, extended as the reference's list.extend does (no dtype coercion)."""
+        if isinstance(a, (list, tuple)):
+            self._items.extend(a)
+            self._n += len(a)
+            return
+        a = np.array(a, copy=True).reshape(-1)
+        self._items.append(_Chunk(a))
         self._n += a.size
 
     def clear(self):

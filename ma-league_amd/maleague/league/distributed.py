@@ -56,6 +56,7 @@ class DistributedLeague:
         self.historical_meta: List[tuple] = []  # (pid, parent pid, trained_steps), oldest first
         self.evictions = 0  # snapshots evicted to make room for newer ones (pool full)
         self.payoff_host = None  # host copy of the payoff taken by host_snapshot() (what matchmaking reads)
+        self._installed = set()  # players whose parameters set_player_params installed (no process group)
 
     def player(self) -> int:
         return self.rank % self.n if self._pid is None else self._pid
@@ -67,6 +68,7 @@ class DistributedLeague:
         flat = flat.detach().reshape(-1).to(torch.float32)
         self._alloc_pool(flat.numel(), flat.device)
         self.current[pid].copy_(flat)
+        self._installed.add(pid)
 
     def _alloc_pool(self, n_p: int, device):
         if self.current is None:
@@ -182,6 +184,10 @@ class DistributedLeague:
             meta = allm[:, n_p:].detach().cpu().numpy().astype(np.int64)
         else:  # nothing to gather: the message stays on the host, the parameters on the device; the other players
             # (player_id leagues) keep their installed replicas and never ask for checkpoints
+            missing = [p for p in range(self.n) if p != self.player() and p not in self._installed]
+            if missing:  # their pool rows would silently be zeros
+                raise ValueError(f"league exchange without a process group: players {missing} have no parameters "
+                                 "(DistributedLeague(player_id=...) + set_player_params for every other player)")
             meta = np.zeros((self.n, 4), dtype=np.int64)
             meta[self.player()] = np.asarray(meta_in, dtype=np.float32).astype(np.int64)
             params = None

@@ -225,3 +225,136 @@ def test_refil_learner_sampled_view_matches_copy(device):
             assert s1[k] == s2[k], (call, k, s1[k], s2[k])
         assert torch.equal(L1._flat.flat, L2._flat.flat), call
     assert view._rows is None  # the slot map never went to the device
+
+
+def _synthetic_entity_batch(B, T1, NA, NE, ED, A, lens, seed):
+    """A random entity-scheme batch of any shape (the env variant only produces NA = 8): episode b holds lens[b]
+    transitions (filled t <= lens[b], terminated at lens[b] - 1 for even b), a random number of active entities
+    (the rest padded: entity_mask 1, zero features), random observability, availability (>= 1 per agent row) and
+    actions among the available ones. Keys as EpisodeBatch.transition_data."""
+    rng = np.random.RandomState(seed)
+    ent = (0.5 * rng.randn(B, T1, NE, ED)).astype(np.float32)
+    emask = np.zeros((B, T1, NE), np.uint8)
+    omask = (rng.rand(B, T1, NE, NE) < 0.3).astype(np.uint8)
+    avail = (rng.rand(B, T1, NA, A) < 0.5).astype(np.int32)
+    avail[..., 0] = np.maximum(avail[..., 0], (avail.sum(-1) == 0).astype(np.int32))
+    acts = np.zeros((B, T1, NA, 1), np.int64)
+    filled = np.zeros((B, T1, 1), np.int64)
+    term = np.zeros((B, T1, 1), np.uint8)
+    rew = rng.randn(B, T1, 1).astype(np.float32)
+    for b in range(B):
+        k = rng.randint(max(1, NA - 3), NA + 1)  # active agents
+        kn = rng.randint(k, NE + 1)               # active entities
+        emask[b, :, kn:] = 1
+        emask[b, :, k:NA] = 1
+        L = int(lens[b])
+        filled[b, :L + 1] = 1
+        if b % 2 == 0:
+            term[b, L - 1] = 1
+        for t in range(T1):
+            dead = rng.rand(NE) < 0.1
+            emask[b, t, dead] = 1
+            for n in range(NA):
+                ok = np.nonzero(avail[b, t, n])[0]
+                acts[b, t, n, 0] = ok[rng.randint(len(ok))]
+        emask[b, L + 1:] = 0
+    ent[emask.astype(bool)] = 0.0
+    omask = np.maximum(omask, emask[:, :, None, :])
+    omask = np.maximum(omask, emask[:, :, :, None])
+    for x in (ent, rew, avail, acts):
+        for b in range(B):
+            x[b, int(lens[b]) + 1:] = 0
+    omask[filled[..., 0] == 0] = 0
+    emask[filled[..., 0] == 0] = 0
+    onehot = np.zeros((B, T1, NA, A), np.float32)
+    np.put_along_axis(onehot, acts, 1.0, axis=-1)
+    onehot[filled[..., 0] == 0] = 0
+    return {"entities": ent, "obs_mask": omask, "entity_mask": emask, "actions": acts, "avail_actions": avail,
+            "reward": rew, "terminated": term, "actions_onehot": onehot, "filled": filled}
+
+
+@pytest.mark.parametrize("NA,NE", [(5, 12), (3, 7)])
+def test_refil_learner_na_not_multiple_of_8_matches_oracle(device, NA, NE):
+    """the learner's NA % 8 != 0 branch (generic instantiations; no t-major skipping, conditional zeroing
+    of d2 / dfc2 / dout) against the oracle: two train calls on a random batch of NA agents among NE entities."""
+    A = 5 + NE
+    B, T1 = 8, 25
+    lens = np.random.RandomState(NA).randint(4, T1 - 1, size=B)
+    arrs = _synthetic_entity_batch(B, T1, NA, NE, 8, A, lens, seed=NA * 10 + NE)
+    T = int(lens.max()) + 1
+    arrs = {k: np.ascontiguousarray(v[:, :T]) for k, v in arrs.items()}
+    a_dev = refil_args(device="cuda", n_agents=NA, n_entities=NE, n_actions=A)
+    a_cpu = refil_args(device="cpu", n_agents=NA, n_entities=NE, n_actions=A)
+    eb = _batch_from(arrs, device, NE=NE, NA=NA, A=A)
+    torch.manual_seed(NA)
+    from maleague.modules.agents import REGISTRY as agent_REGISTRY
+    from maleague.modules.mixers import FlexQMixer
+    mixer_p = {k: v.detach().cpu().numpy() for k, v in FlexQMixer(a_cpu).state_dict().items()}
+    ag = agent_REGISTRY["imagine_entity_attend_rnn"](8 + A, a_cpu)
+    agent_p = {k: v.detach().cpu().numpy() for k, v in ag.state_dict().items()}
+    L, _ = _learner(eb, agent_p, mixer_p, a_dev)
+    ref = RR.REFILLearnerRef(agent_p, mixer_p, a_cpu)
+    batch = {k: torch.from_numpy(v) for k, v in arrs.items()}
+    g = torch.Generator().manual_seed(9)
+    for call in range(2):
+        groupA = torch.bernoulli(torch.rand(B, 1, 1, generator=g).repeat(1, 1, NE), generator=g).to(torch.uint8)
+        want = ref.train(batch, groupA, episode_num=call)
+        L.train(eb, 0, episode_num=call, groupA=groupA.to(device))
+        got = L.last_stats
+        for k in want:
+            np.testing.assert_allclose(got[k], want[k], rtol=2e-4, atol=1e-5, err_msg=f"NA={NA} call {call} {k}")
+        for k, v in L.mac.agent.named_parameters():
+            np.testing.assert_allclose(v.detach().cpu().numpy(), ref.agent[k].detach().numpy(), atol=2e-5, rtol=0,
+                                       err_msg=f"NA={NA} call {call} agent {k}")
+        for k, v in L.mixer.named_parameters():
+            np.testing.assert_allclose(v.detach().cpu().numpy(), ref.mixer[k].detach().numpy(), atol=2e-5, rtol=0,
+                                       err_msg=f"NA={NA} call {call} mixer {k}")
+
+
+@pytest.mark.parametrize("NA,NE", [(8, 16), (5, 12)])
+def test_refil_learner_no_stale_rows_across_calls(device, NA, NE, monkeypatch):
+    """rows the backward kernels skip (items past an episode's live steps) must not carry data from an
+    earlier call. One learner trains on a batch of LONG episodes, then on one of SHORT episodes (same buffer length,
+    so the same workspace layout); a fresh learner holding the first learner's parameters, RMSprop state and targets
+    trains on the short batch alone. Both must end bit-identical (parameters, gradients, stats). Run for the
+    side-stream and the one-stream form; those two must agree bit for bit as well."""
+    A = 5 + NE
+    B, T1 = 8, 41
+    long_b = _synthetic_entity_batch(B, T1, NA, NE, 8, A, np.full(B, T1 - 2), seed=1)
+    short_b = _synthetic_entity_batch(B, T1, NA, NE, 8, A, np.random.RandomState(2).randint(3, 9, size=B), seed=2)
+    a_dev = refil_args(device="cuda", n_agents=NA, n_entities=NE, n_actions=A)
+    a_cpu = refil_args(device="cpu", n_agents=NA, n_entities=NE, n_actions=A)
+    torch.manual_seed(3)
+    from maleague.modules.agents import REGISTRY as agent_REGISTRY
+    from maleague.modules.mixers import FlexQMixer
+    mixer_p = {k: v.detach().cpu().numpy() for k, v in FlexQMixer(a_cpu).state_dict().items()}
+    agent_p = {k: v.detach().cpu().numpy() for k, v in
+               agent_REGISTRY["imagine_entity_attend_rnn"](8 + A, a_cpu).state_dict().items()}
+    g = torch.Generator().manual_seed(5)
+    gA = [torch.bernoulli(torch.rand(B, 1, 1, generator=g).repeat(1, 1, NE), generator=g).to(torch.uint8).to(device)
+          for _ in range(2)]
+    results = {}
+    for mode in ("side", "one"):
+        if mode == "one":
+            monkeypatch.setenv("MLG_REFIL_ONE_STREAM", "1")
+        else:
+            monkeypatch.delenv("MLG_REFIL_ONE_STREAM", raising=False)
+        e_long = _batch_from(long_b, device, NE=NE, NA=NA, A=A)
+        e_short = _batch_from(short_b, device, NE=NE, NA=NA, A=A)
+        L1, _ = _learner(e_long, agent_p, mixer_p, a_dev)
+        L1.train(e_long, 0, episode_num=0, groupA=gA[0])
+        torch.cuda.synchronize()
+        L2, _ = _learner(e_short, agent_p, mixer_p, a_dev)
+        with torch.no_grad():
+            L2._flat.flat.copy_(L1._flat.flat)
+            L2._sq.copy_(L1._sq)
+            L2._tflat.flat.copy_(L1._tflat.flat)
+        L1.train(e_short, 0, episode_num=1, groupA=gA[1])
+        L2.train(e_short, 0, episode_num=1, groupA=gA[1])
+        torch.cuda.synchronize()
+        assert torch.equal(L1._flat.flat, L2._flat.flat), mode
+        assert torch.equal(L1._grads, L2._grads), mode
+        assert L1.last_stats == L2.last_stats, mode
+        results[mode] = (L1._flat.flat.clone(), L1._grads.clone(), L1.last_stats)
+    assert torch.equal(results["side"][0], results["one"][0]) and torch.equal(results["side"][1], results["one"][1])
+    assert results["side"][2] == results["one"][2]

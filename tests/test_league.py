@@ -394,3 +394,36 @@ def test_agent_vector_flat_view_and_reflatten():
     assert agent_vector(mac).data_ptr() == fp2.flat.data_ptr()
     with pytest.raises(ValueError):
         load_agent_vector(mac, torch.zeros(3))
+
+
+def test_exchange_without_group_requires_installed_players():
+    """a multi-player league without a process group must not exchange with other players' rows silently
+    zero: the exchange raises until every other player's parameters are installed."""
+    from maleague.league import DistributedLeague
+    flat = torch.arange(4, dtype=torch.float32)
+    lg = DistributedLeague(n_players=3, device="cpu", player_id=1)
+    with pytest.raises(ValueError):
+        lg.exchange(flat, 0, False)
+    lg.set_player_params(0, flat + 1)
+    with pytest.raises(ValueError):
+        lg.exchange(flat, 0, False)
+    lg.set_player_params(2, flat + 2)
+    lg.exchange(flat, 0, False)
+    assert torch.equal(lg.params_of(1), flat) and torch.equal(lg.params_of(2), flat + 2)
+    with pytest.raises(ValueError):
+        DistributedLeague(n_players=3, device="cpu").exchange(flat, 0, False)
+    DistributedLeague(n_players=1, device="cpu").exchange(flat, 0, False)  # a one-player league needs nothing else
+
+
+def test_logger_series_snapshots_arrays():
+    """collected arrays are copied (a later in-place change of the caller's array does not change
+    unlogged statistics); lists are extended as Python values (no dtype coercion)."""
+    import numpy as np
+    from maleague.custom_logging import _Series
+    s = _Series()
+    a = np.array([1.0, 2.0, 3.0], dtype=np.float32)
+    s.extend_array(a)
+    a[:] = 0
+    s.extend_array([True, 2, 3.5])
+    v = s.values()
+    assert v[:3] == [1.0, 2.0, 3.0] and v[3:] == [True, 2, 3.5] and type(v[3]) is bool and type(v[4]) is int
