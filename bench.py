@@ -311,6 +311,7 @@ def roofline(mode, stepper, r, steps, B):
         floor_ms = (r["longest_episode_mean"] + 1) * step_cyc / CLOCK_HZ * 1e3
         out.update({"latency_floor_ms": floor_ms, "latency_floor_frac": floor_ms / r["avg_kernel_ms"],
                     "one_env_step_cycles": step_cyc, "one_env_step_source": cnt.get("one_env_step_source"),
+                    "one_env_step_commit": cnt.get("one_env_step_commit"),
                     "longest_episode_mean": r["longest_episode_mean"], "latency_floor_clock_ghz": CLOCK_HZ / 1e9})
     if mode == "ai":
         issued = fl / N * r["rows_per_launch"] / avg_s

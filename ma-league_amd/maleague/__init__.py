@@ -5,3 +5,5 @@ mixers, env) so YAML configs select the same keys; every hot-path op runs in lib
 (hand-written HIP kernels, C ABI in include/maleague.h). See DESIGN.md.
 """
 __version__ = "0.1.0"
+
+from . import ops  # noqa: E402,F401  (registers torch.ops.maleague.*)

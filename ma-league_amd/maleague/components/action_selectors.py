@@ -10,7 +10,6 @@ from __future__ import annotations
 
 import torch
 
-from .. import _native
 from .epsilon_schedules import DecayThenFlatSchedule
 
 
@@ -31,14 +30,11 @@ class EpsilonGreedyActionSelector:
         q = agent_inputs.float().contiguous()
         B, N, A = q.shape
         av = avail_actions.to(device=q.device, dtype=torch.int32).contiguous()
-        actions = torch.empty(B, N, dtype=torch.int64, device=q.device)
-        greedy = torch.empty(B, N, dtype=torch.int64, device=q.device)
         keys = (torch.arange(B, dtype=torch.int64, device=q.device) + (self.seed << 32)).contiguous()
         episodes = torch.full((B,), self._calls & 0x7FFFFFFF, dtype=torch.int32, device=q.device)
         self._calls += 1
-        _native.call("mlg_select_actions", _native.ptr(q), _native.ptr(av), B * N, A, N, _native.ptr(keys),
-                     _native.ptr(episodes), 0, eps, _native.ptr(actions), _native.ptr(greedy), _native.stream_ptr())
-        return actions, greedy
+        from ..ops import select_actions
+        return select_actions(q, av, keys, episodes, 0, eps)
 
 
 class MultinomialActionSelector:

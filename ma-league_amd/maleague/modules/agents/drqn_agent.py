@@ -125,10 +125,5 @@ class DRQNAgentNetwork(AgentNetwork):
         H = self.args.rnn_hidden_dim
         x = inputs.float().contiguous()
         h_in = hidden_state.reshape(-1, H).float().contiguous()
-        R = x.shape[0]
-        q = torch.empty(R, self.args.n_actions, device=x.device)
-        h_out = torch.empty(R, H, device=x.device)
-        d = self.dims()
-        _native.call("mlg_agent_forward", _native.byref(d), _native.ptr(self.packed()), _native.ptr(x),
-                     _native.ptr(h_in), _native.ptr(q), _native.ptr(h_out), R, _native.stream_ptr())
-        return q, h_out
+        from ...ops import struct_fields
+        return torch.ops.maleague.agent_forward(self.packed(), x, h_in, struct_fields(self.dims()))

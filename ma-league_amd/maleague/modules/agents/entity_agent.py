@@ -103,13 +103,11 @@ class EntityAttentionRNNAgent(AgentNetwork):
         hs = torch.empty(bs, ts, na, H, device=dev)
         d = self.dims()
         P = self.packed()
+        from ...ops import refil_agent_step, struct_fields
+        dl = struct_fields(d)
         for t in range(ts):
             et, ot, mt = ent[:, t].contiguous(), om[:, t].contiguous(), em[:, t].contiguous()
-            qt = torch.empty(bs, na, A, device=dev)
-            ht = torch.empty(bs, na, H, device=dev)
-            _native.call("mlg_refil_agent_forward", _native.byref(d), _native.ptr(P), _native.ptr(et), _native.ptr(ot),
-                         _native.ptr(mt), _native.ptr(h), _native.ptr(qt), _native.ptr(ht), int(bs),
-                         _native.stream_ptr())
+            qt, ht = refil_agent_step(P, et, ot, mt, h, dl)
             q[:, t] = qt
             hs[:, t] = ht
             h = ht

@@ -9,7 +9,6 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ... import _native
 
 
 class EntityAttentionLayer(nn.Module):
@@ -36,11 +35,8 @@ class EntityAttentionLayer(nn.Module):
         x = entities.float().contiguous()
         pre = pre_mask[:, :nq, :ne].to(torch.uint8).contiguous()
         post = post_mask.to(torch.uint8).contiguous()
-        y = torch.empty(bs, nq, self.out_dim, device=dev)
         w_in = self.in_trans.weight.detach().float().contiguous()
         w_out = self.out_trans.weight.detach().float().contiguous()
         b_out = self.out_trans.bias.detach().float().contiguous()
-        _native.call("mlg_refil_attention", _native.ptr(w_in), _native.ptr(w_out), _native.ptr(b_out), _native.ptr(x),
-                     _native.ptr(pre), _native.ptr(post), int(bs), int(ne), int(nq), int(self.n_heads),
-                     _native.ptr(y), None, None, None, None, None, _native.stream_ptr())
-        return y
+        from ...ops import refil_attention
+        return refil_attention(w_in, w_out, b_out, x, pre, post, int(self.n_heads))

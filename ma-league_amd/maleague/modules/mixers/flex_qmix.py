@@ -68,8 +68,7 @@ class FlexQMixer(nn.Module):
         if imagine_groups is not None:
             wm = imagine_groups[0].reshape(R, ne, ne).to(torch.uint8).contiguous()
             im = imagine_groups[1].reshape(R, ne, ne).to(torch.uint8).contiguous()
-        out = torch.empty(R, device=dev)
-        _native.call("mlg_refil_mixer_forward", _native.byref(d), _native.ptr(packed), _native.ptr(qs),
-                     _native.ptr(ent), _native.ptr(em), _native.ptr(wm), _native.ptr(im),
-                     int(bool(self.args.softmax_mixing_weights)), _native.ptr(out), R, _native.stream_ptr())
+        from ...ops import refil_mixer_forward, struct_fields
+        out = refil_mixer_forward(packed, qs, ent, em, wm, im, int(bool(self.args.softmax_mixing_weights)),
+                                  struct_fields(d))
         return out.view(bs, T, 1)

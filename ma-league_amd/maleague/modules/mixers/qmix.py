@@ -58,9 +58,9 @@ class QMixer(nn.Module):
         bs = agent_qs.size(0)
         qs = agent_qs.reshape(-1, self.n_agents).float().contiguous()
         st = states.reshape(-1, self.state_dim).float().contiguous()
-        out = torch.empty(qs.shape[0], device=qs.device)
         p, keep = self._cparams()
-        _native.call("mlg_qmix_forward", _native.byref(p), _native.ptr(qs), _native.ptr(st), _native.ptr(out),
-                     qs.shape[0], _native.stream_ptr())
-        del keep
+        from ...ops import qmix_forward
+        empty = qs.new_empty(0)
+        out = qmix_forward([empty if t is None else t for t in keep], qs, st,
+                           [p.n_agents, p.state_dim, p.embed_dim, p.hypernet_embed, p.hypernet_layers])
         return out.view(bs, -1, 1)
