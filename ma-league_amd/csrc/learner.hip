@@ -1923,8 +1923,7 @@ int run_train(Plan& p, const MlgLearnerCfg* cfg, const MlgLearnerBufs* bufs, hip
     int ta, tb;
     int64_t ra, rb;
     const WJobs JA = mlg::bjob_view(J, 3, J.n, &ta, &ra), JB = mlg::bjob_view(J, 0, 3, &tb, &rb);
-    // MLG_LEARNER_BWD_NOFUSE=1 (A/B): the reverse recurrence alone, every wgrad job after agent_dx
-    const bool fused = !rec16 && H == 64 && threads == 256 && !getenv("MLG_LEARNER_BWD_NOFUSE");
+    const bool fused = !rec16 && H == 64 && threads == 256;
     if (fused) {
         const int nbwd = (c.R + 3) / 4;
         hipLaunchKernelGGL((bwd4_wgrad_kernel<H>), dim3((unsigned)(nbwd + (ta + 3) / 4)), dim3(256), 0, s, c, bt, p.L,
