@@ -255,3 +255,32 @@ def test_league_main_dry_run_gloo_world4(tmp_path):
     with open(os.path.join(s0["log_dir"], "league_config.json")) as f:
         saved = json.load(f)
     assert saved["team_tids"] == s0["team_tids"] and saved["force_unit"] == ["HEALER", "RANGED", True]
+
+
+def test_league_main_dry_run_with_config_tree(tmp_path):
+    """The entry point reads a reference-layout config tree (--config-dir: default.yaml < envs/ < leagues/ < algs/,
+    teams/*.json in the enum-encoded format) and applies --key=value overrides on top, like ConfigBuilder
+    (config_builder.py:19-55); one process, no launcher (world size 1)."""
+    import yaml
+    from maleague.envs.plans import builtin_plan
+    d = tmp_path / "config"
+    for sub in ("envs", "leagues", "algs", "teams"):
+        (d / sub).mkdir(parents=True)
+    (d / "default.yaml").write_text(yaml.safe_dump({"runner": "episode", "batch_size_run": 1, "test_nepisode": 20,
+                                                   "use_cuda": True, "t_max": 10000, "seed": 5}))
+    (d / "envs" / "ma.yaml").write_text(yaml.safe_dump({"env": "ma", "env_args": {"grid_size": 20,
+                                                                                  "match_build_plan": "medium_1h_4t"}}))
+    (d / "leagues" / "matchmaking.yaml").write_text(yaml.safe_dump({"play_time_mins": 120, "league_runtime_hours": 24,
+                                                                    "matchmaking": "pfsp", "buffer_cpu_only": False}))
+    (d / "algs" / "qmix.yaml").write_text(yaml.safe_dump({"learner": "q", "mixer": "qmix", "buffer_size": 5000}))
+    (d / "teams" / "medium_1h_4t.json").write_text(json.dumps(builtin_plan("medium_1h_4t")))
+    from maleague.league.main import main
+    s = main(["--config=qmix", "--env-config=ma", "--league-config=matchmaking", "--experiment=rolebased",
+              "--league_size=1", "--team_size=3", "--dry-run", f"--config-dir={d}", f"--local_results_path={tmp_path}",
+              "--play_time_mins=0.5", "force-unit", "--role=TANK", "--attack=MELEE"])
+    assert s["seed"] == 5 and s["matchmaking"] == "pfsp" and s["world_size"] == 1
+    assert s["players"][0]["role"] == "simple" and s["players"][0]["codes"].split()[0] == "TM"
+    assert len(s["players"][0]["codes"].split()) == 3
+    with open(os.path.join(s["log_dir"], "league_config.json")) as f:
+        saved = json.load(f)
+    assert "--play_time_mins=0.5" in saved["overrides"]
