@@ -2,7 +2,8 @@
 # Alternating A/B of library variants (VARIANTS="name:path/to/lib.so[:ENV=V,ENV2=W] ...", "base:" = the default library,
 # "name::ENV=V" = the default library with environment settings) over ROUNDS
 # rounds: the learner microbenchmark (LRN_MODES, scripts/bench_learner.py: mean ms per train()) and bench legs
-# (BENCH_MODES, bench.py --mode M: value and the rollout kernel's HIP-event average). Optional TESTS run first with
+# (BENCH_MODES, bench.py --mode M: value and the rollout kernel's HIP-event average), microbenchmark scripts (SCRIPTS,
+# last output line). Optional TESTS run first with
 # every variant to check parity.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -25,6 +26,11 @@ for r in $(seq 1 ${ROUNDS:-2}); do
       out=$( ( setenv; MODE=$m REPS=${REPS:-40} timeout -k 10 300 python scripts/bench_learner.py ) 2> gpurun_out/ab/lrn_${name}_$m.err ) \
           || { echo "learner $name $m failed"; tail -20 gpurun_out/ab/lrn_${name}_$m.err; exit 1; }
       echo "r$r lrn $m $name $out"
+    done
+    for sc in ${SCRIPTS:-}; do
+      out=$( ( setenv; timeout -k 10 300 python $sc ) 2> gpurun_out/ab/script_${name}.err | tail -1 ) \
+          || { echo "script $sc $name failed"; tail -20 gpurun_out/ab/script_${name}.err; exit 1; }
+      echo "r$r script $(basename $sc) $name $out"
     done
     for m in ${BENCH_MODES:-}; do
       ( setenv; timeout -k 10 300 python bench.py --mode $m --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline ) \
