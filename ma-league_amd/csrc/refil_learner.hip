@@ -21,6 +21,7 @@
 // Agent rows: r = (c * B + b) * NA + n for copy c (0 plain, 1 within, 2 interact); target rows r = b * NA + n.
 // Items i = b * T + t. Mixer items use t < T - 1 (the other kernels write zeros for t = T - 1).
 #include "mlg_host.h"
+#include "batch_mask_device.h"
 #include "gru4_device.h"
 #include "refil_device.h"
 #include "wgrad_device.h"
@@ -521,7 +522,12 @@ __global__ void __launch_bounds__(256) prologue_kernel(Prologue P) {
     }
     int blk = blockIdx.x;
     if (blk == 0) {
-        mask_sum_body(bt, P.c.B, P.c.T, P.msum, red);
+        __shared__ mlg::MaskStatsLds ms;
+        if (mlg::mask_stats_fits(P.c.B, P.c.T))  // one pass of independent loads (batch_mask_device.h)
+            mlg::batch_mask_stats(bt.filled, bt.terminated, bt.T1, [&](int b) { return eslot(bt, b); }, P.c.B, P.c.T,
+                                  P.msum, P.msum + 4, ms);
+        else
+            mask_sum_body(bt, P.c.B, P.c.T, P.msum, red);
         return;
     }
     blk -= 1;
