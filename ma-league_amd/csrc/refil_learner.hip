@@ -1532,7 +1532,7 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
 }
 
 // ---- clip_grad_norm_ + RMSprop + stats -------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ part, int n_items,
+__global__ void __launch_bounds__(1024) refil_finish_kernel(const float* __restrict__ part, int n_items,
                                                       const float* __restrict__ msum_p, float* __restrict__ params,
                                                       float* __restrict__ grads, float* __restrict__ sq, int64_t n_params,
                                                       float lr, float alpha, float eps, float max_norm, int NA,
@@ -1817,7 +1817,7 @@ int run_train(Plan& p, const MlgRefilLearnerCfg* cfg, const MlgRefilLearnerBufs*
     hipLaunchKernelGGL(mlg::wgrad_block_reduce_kernel<MJ>, dim3((unsigned)n_red_blocks), dim3(256), 0, s, J, ws + w.slab,
                        ws + p.w.nrm);
     const int64_t n_par = p.n_agent + p.n_mixer;
-    hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + w.part, c.I,
+    hipLaunchKernelGGL(refil_finish_kernel, dim3((unsigned)((n_par + 1023) / 1024)), dim3(1024), 0, s, ws + w.part, c.I,
                        ws + w.msum, bufs->params, bufs->grads, bufs->square_avg, n_par, cfg->lr, cfg->optim_alpha,
                        cfg->optim_eps, cfg->grad_norm_clip, c.NA, c.lmbda, bufs->stats, ws + p.w.nrm, n_red_blocks,
                        bufs->trained_steps, bufs->target_sync);
