@@ -58,7 +58,7 @@ for k, cs in vals.items():
         d["valu_per_mfma"] = m.get("SQ_INSTS_VALU", 0.0) / m["SQ_INSTS_MFMA"]
     out[k] = d
 # annotations that are not counters (bench.py's latency floor reads them): kept when a kernel is re-collected
-KEEP = ("one_env_step_cycles", "one_env_step_source")
+KEEP = ("one_env_step_cycles", "one_env_step_source", "one_env_step_commit")
 if len(sys.argv) > 3 and os.path.exists(sys.argv[3]):  # merge into an existing counters.json (other kernels kept)
     prev = json.load(open(sys.argv[3])).get("kernels", {})
     for k, d in out.items():
