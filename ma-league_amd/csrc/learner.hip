@@ -1293,6 +1293,33 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
         b1[cc] = ld4(h + NE + E + cc * 16 + 4 * g);
     }
     const float vv = h[NE + 2 * E];
+    // operands of the backward that depend on nothing computed here, requested now so that their L2 / HBM round
+    // trips overlap the gather and the mixing (wave 1 only: wave 0 leaves after the target mix): agent 0's W_a2^T
+    // block, W_f2^T, V's output row and this row's layer-1 activations (stored by mix_pre_tile)
+    const float* la = hy.la + (int64_t)(valid ? rm : 0) * L1;
+    floatx4 aTb[2][TE][T1H], f2w[T1H][TE], wvb[TE], lab[T1H * 2 + TE];
+    auto load_aT = [&](int n, floatx4 (&d)[TE][T1H]) {
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc)
+#pragma unroll
+            for (int mt = 0; mt < T1H; ++mt) d[cc][mt] = ld4(Mon.a2T + (int64_t)(mt * 16 + col) * NE + n * E + cc * 16 + 4 * g);
+    };
+    if (wv == 1) {
+        load_aT(0, aTb[0]);
+#pragma unroll
+        for (int mt = 0; mt < T1H; ++mt)
+#pragma unroll
+            for (int cc = 0; cc < TE; ++cc) f2w[mt][cc] = ld4(Mon.f2T + (int64_t)(mt * 16 + col) * E + cc * 16 + 4 * g);
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) wvb[cc] = ld4(Mon.v2p + cc * 16 + 4 * g);
+#pragma unroll
+        for (int mt = 0; mt < T1H; ++mt) {
+            lab[mt] = ld4(la + (Mx::OW1 + mt) * 16 + 4 * g);
+            lab[T1H + mt] = ld4(la + (Mx::OWF + mt) * 16 + 4 * g);
+        }
+#pragma unroll
+        for (int cc = 0; cc < TE; ++cc) lab[2 * T1H + cc] = ld4(la + (Mx::OVH + cc) * 16 + 4 * g);
+    }
     float cq[MAXN], tq[MAXN];
     for (int n = 0; n < N; ++n) cq[n] = tq[n] = 0.f;
     gather_q_rows<MIXPF_A>(c, bt, mac, tmac, b, t, valid, g, cq, tq);
@@ -1344,20 +1371,15 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
 #pragma unroll
     for (int mt = 0; mt < T1H; ++mt) dw1h[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
     float dq[MAXN];
-    for (int n = 0; n < N; ++n) {
+#pragma unroll
+    for (int n = 0; n < MIXPF_N; ++n) {  // N <= MIXPF_N (the FAST shapes): static ping-pong buffers
+        if (n >= N) break;
+        if (n + 1 < MIXPF_N && n + 1 < N) load_aT(n + 1, aTb[(n + 1) & 1]);
+        const floatx4(&aT)[TE][T1H] = aTb[n & 1];
         float part = 0.f;
-        floatx4 aT[TE][T1H];
-#pragma unroll
-        for (int cc = 0; cc < TE; ++cc)
-#pragma unroll
-            for (int mt = 0; mt < T1H; ++mt)
-                aT[cc][mt] = ld4(Mon.a2T + (int64_t)(mt * 16 + col) * NE + n * E + cc * 16 + 4 * g);
 #pragma unroll
         for (int cc = 0; cc < TE; ++cc) {
-            floatx4 wp = w1c[0][cc];  // w1c[n][cc] without dynamic register indexing
-#pragma unroll
-            for (int k = 1; k < MIXPF_N; ++k)
-                if (k == n) wp = w1c[k][cc];
+            const floatx4 wp = w1c[n][cc];
             floatx4 dlt;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1378,17 +1400,15 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
     for (int mt = 0; mt < T1H; ++mt) {
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int cc = 0; cc < TE; ++cc)
-            acc = mfma_chunk(ld4(Mon.f2T + (int64_t)(mt * 16 + col) * E + cc * 16 + 4 * g), dwf[cc], acc);
+        for (int cc = 0; cc < TE; ++cc) acc = mfma_chunk(f2w[mt][cc], dwf[cc], acc);
         dwfh[mt] = acc;
     }
     if (valid) {
-        // layer-1 activations (stored by mix_pre_tile) for the ReLU masks
-        const float* la = hy.la + (int64_t)rm * L1;
+        // layer-1 activations (stored by mix_pre_tile, loaded above) for the ReLU masks
         float* d1 = o.d1 + (int64_t)rm * L1;
 #pragma unroll
         for (int mt = 0; mt < T1H; ++mt) {  // w1h
-            const floatx4 l = ld4(la + (Mx::OW1 + mt) * 16 + 4 * g);
+            const floatx4 l = lab[mt];
             floatx4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = l[q] > 0.f ? dw1h[mt][q] : 0.f;
@@ -1396,7 +1416,7 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
         }
 #pragma unroll
         for (int mt = 0; mt < T1H; ++mt) {  // wfh
-            const floatx4 l = ld4(la + (Mx::OWF + mt) * 16 + 4 * g);
+            const floatx4 l = lab[T1H + mt];
             floatx4 acc = dwfh[mt];
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] = l[q] > 0.f ? acc[q] : 0.f;
@@ -1405,8 +1425,8 @@ __global__ void __launch_bounds__(128) mix_td2_kernel(LCfg c, MlgBatch bt, MixPt
 #pragma unroll
         for (int cc = 0; cc < TE; ++cc) {  // b1, vh
             *reinterpret_cast<floatx4*>(d1 + 2 * HE + cc * 16 + 4 * g) = dpre[cc];
-            const floatx4 wv = ld4(Mon.v2p + cc * 16 + 4 * g);
-            const floatx4 l = ld4(la + (Mx::OVH + cc) * 16 + 4 * g);
+            const floatx4 wv = wvb[cc];
+            const floatx4 l = lab[2 * T1H + cc];
             floatx4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = l[q] > 0.f ? dy * wv[q] : 0.f;
