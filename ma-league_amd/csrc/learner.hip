@@ -1620,12 +1620,12 @@ __global__ void __launch_bounds__(512) agent_dx_kernel(LCfg c, const float* __re
     const int64_t row = (int64_t)t * c.R + (valid ? r : 0);
     const float* wrow = wihT + (int64_t)(w * 16 + col) * 3 * H + 4 * g;
     const float* grow = dgi + row * 3 * H + 4 * g;
+    const int64_t o = row * H + w * 16 + 4 * g;
+    const floatx4 xv = ld4(ws_x + o);  // the ReLU mask, requested with the operands (row 0 for padding lanes)
     floatx4 dx = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kc = 0; kc < 3 * H / 16; ++kc) dx = mfma_chunk(ld4(wrow + kc * 16), ld4(grow + kc * 16), dx);
     if (valid) {
-        const int64_t o = row * H + w * 16 + 4 * g;
-        const floatx4 xv = ld4(ws_x + o);
 #pragma unroll
         for (int q = 0; q < 4; ++q) dx[q] = xv[q] > 0.f ? dx[q] : 0.f;
         *reinterpret_cast<floatx4*>(da + o) = dx;
@@ -1643,19 +1643,22 @@ __global__ void __launch_bounds__(1024) finish_kernel(const float* __restrict__ 
                                                       int n_nrm, float* __restrict__ tsync, double* __restrict__ trained) {
     __shared__ float red[1024];
     const int tid = threadIdx.x;
+    // this thread's parameter, gradient and square average, requested before the norm reduction they wait for
+    const int64_t ip = (int64_t)blockIdx.x * blockDim.x + tid;
+    const bool has = ip < n_params;
+    const float g0 = has ? grads[ip] : 0.f, sq0 = has ? sq[ip] : 0.f, p0 = has ? params[ip] : 0.f;
     float s = 0.f;
     for (int i = tid; i < n_nrm; i += blockDim.x) s += nrm_part[i];
     const float norm = sqrtf(block_sum_1024(s, red));
     const float coef = fminf(max_norm / (norm + 1e-6f), 1.f);  // torch clip_grad_norm_ (clamped coef)
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
-    if (i < n_params) {
-        const float gi = grads[i] * coef;
-        grads[i] = gi;
-        const float a = alpha * sq[i] + (1.f - alpha) * gi * gi;  // RMSprop square_avg
-        sq[i] = a;
-        const float pn = params[i] - lr * gi / (sqrtf(a) + eps);
-        params[i] = pn;
-        if (tsync) tsync[i] = pn;  // target update due after this step (q_learner.py:127-128), same launch
+    if (has) {
+        const float gi = g0 * coef;
+        grads[ip] = gi;
+        const float a = alpha * sq0 + (1.f - alpha) * gi * gi;  // RMSprop square_avg
+        sq[ip] = a;
+        const float pn = p0 - lr * gi / (sqrtf(a) + eps);
+        params[ip] = pn;
+        if (tsync) tsync[ip] = pn;  // target update due after this step (q_learner.py:127-128), same launch
     }
     // the four stat sums on blocks 0..3 (one each, same order as one block doing all four: bit-identical), so no
     // block runs four block reductions after its parameter slice

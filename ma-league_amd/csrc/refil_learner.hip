@@ -1541,17 +1541,20 @@ __global__ void __launch_bounds__(1024) refil_finish_kernel(const float* __restr
                                                       double* __restrict__ trained, float* __restrict__ tsync) {
     __shared__ float red[1024];
     const int tid = threadIdx.x;
+    // this thread's parameter, gradient and square average, requested before the norm reduction they wait for
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
+    const bool has = i < n_params;
+    const float g0 = has ? grads[i] : 0.f, sq0 = has ? sq[i] : 0.f, p0 = has ? params[i] : 0.f;
     float s = 0.f;
-    for (int i = tid; i < n_nrm; i += blockDim.x) s += nrm_part[i];
+    for (int k = tid; k < n_nrm; k += blockDim.x) s += nrm_part[k];
     const float norm = sqrtf(mlg::block_sum_1024(s, red));
     const float coef = fminf(max_norm / (norm + 1e-6f), 1.f);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
-    if (i < n_params) {
-        const float gi = grads[i] * coef;
+    if (has) {
+        const float gi = g0 * coef;
         grads[i] = gi;
-        const float a = alpha * sq[i] + (1.f - alpha) * gi * gi;
+        const float a = alpha * sq0 + (1.f - alpha) * gi * gi;
         sq[i] = a;
-        const float pn = params[i] - lr * gi / (sqrtf(a) + eps);
+        const float pn = p0 - lr * gi / (sqrtf(a) + eps);
         params[i] = pn;
         if (tsync) tsync[i] = pn;  // the target update due after this step (refil_learner.py:181-183), same launch
     }
