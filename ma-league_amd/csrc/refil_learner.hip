@@ -1216,6 +1216,26 @@ __global__ void __launch_bounds__(64) mix_td_kernel(RCfg c_arg, MlgEntityBatch b
     }
 }
 
+// One item's q | k | v rows (NE x 3 EMB, row-major in global) into LDS rows of stride LDQ: all of the lane's 24 loads
+// issued before the first LDS write (a loop over them waited for each group of loads in turn, three round trips).
+__device__ __forceinline__ void qkv_to_lds(const float* __restrict__ src, float* dst, int lane) {
+    constexpr int NQ = NE * 3 * EMB / 64;
+    static_assert(NE * 3 * EMB % 64 == 0, "qkv rows: whole 64-lane groups");
+    float v[NQ];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) v[u] = src[lane + 64 * u];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+        const int q = lane + 64 * u;
+        dst[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = v[u];
+    }
+}
+// the relu mask row x[col][0 .. EMB) of a lane (4 quads at 16 q + 4 g)
+__device__ __forceinline__ void load_relu_rows(const float* __restrict__ x, floatx4 (&xv)[4], int lane) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xv[q] = ld4(x + q * 16 + 4 * (lane >> 4));
+}
+
 // ---- hypernet backward: grid (I, 4), one wave ---------------------------------------------------------------
 struct HypBwd {
     const float* wspT[4];
@@ -1248,8 +1268,9 @@ __global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c_arg, MlgEntityBatc
     // masked mixer item: its deltas are zero and only the wgrad jobs read them, which skip its rows
     if (t >= t_eff(msum) - 1 || t >= mix_len(msum, b)) return;
     const uint32_t dead = dead_bits(c, em_bits(c, bt, b, t));
-    for (int q = lane; q < NE * 3 * EMB; q += 64)
-        s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = hb.qkvm[k][(int64_t)i * NE * 3 * EMB + q];
+    floatx4 x1v[4];  // fc1 activations for the final relu mask, requested now (used after the attention backward)
+    load_relu_rows(hb.x1m[k] + ((int64_t)i * NE + col) * EMB, x1v, lane);
+    qkv_to_lds(hb.qkvm[k] + (int64_t)i * NE * 3 * EMB, s_qkv, lane);
     for (int q = lane; q < 32 * LDX; q += 64) s_do[q] = 0.f;
     for (int tile = 0; tile * 16 < V * NAS; ++tile) {
         const int row = tile * 16 + col, v = row >> 3, n = row & 7;
@@ -1292,10 +1313,9 @@ __global__ void __launch_bounds__(64) hyper_bwd_kernel(RCfg c_arg, MlgEntityBatc
 #else
     in_transT_lds_b16(dx1, hb.wspT[k], s_dqkv, lane);
 #endif
-    const float* x1 = hb.x1m[k] + ((int64_t)i * NE + col) * EMB;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const floatx4 xv = ld4(x1 + q * 16 + 4 * g);
+        const floatx4 xv = x1v[q];
 #pragma unroll
         for (int r = 0; r < 4; ++r) dx1[q][r] = xv[r] > 0.f ? dx1[q][r] : 0.f;
         *reinterpret_cast<floatx4*>(hb.dfc1m[k] + ((int64_t)i * NE + col) * EMB + q * 16 + 4 * g) = dx1[q];
@@ -1467,13 +1487,15 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
             }
             continue;
         }
-        // dx3 = W_ih^T dGI, relu'
+        // dx3 = W_ih^T dGI, relu' (the x3 rows requested with the product's operands)
+        floatx4 x3v[4];
+        load_relu_rows(eb.x3 + (valid ? ro : 0) * EMB, x3v, lane);
         floatx4 d3[4];
         bias_init<4>(d3, nullptr, 0, lane);
         mm_ptr<4>(d3, eb.wihT, 3 * EMB, 0, eb.dgi + (valid ? ro : 0) * 3 * EMB, 3 * EMB / 16, lane);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const floatx4 xv = ld4(eb.x3 + (valid ? ro : 0) * EMB + q * 16 + 4 * g);
+            const floatx4 xv = x3v[q];
 #pragma unroll
             for (int r = 0; r < 4; ++r) d3[q][r] = (valid && xv[r] > 0.f) ? d3[q][r] : 0.f;
             if (row_ok) *reinterpret_cast<floatx4*>(eb.dfc2 + ro * EMB + q * 16 + 4 * g) = d3[q];
@@ -1501,8 +1523,9 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
         const int ii = i0 + ee;
         if (ii >= c.I) continue;
         if (!live(ii)) continue;  // past max_t_filled or the episode: zero deltas, skipped by the wgrad jobs
-        for (int q = lane; q < NE * 3 * EMB; q += 64)
-            s_qkv[(q / (3 * EMB)) * LDQ + q % (3 * EMB)] = eb.qkv[(int64_t)ii * NE * 3 * EMB + q];
+        floatx4 x1v[4];  // fc1 activations for the final relu mask, requested now
+        load_relu_rows(eb.x1 + ((int64_t)ii * NE + col) * EMB, x1v, lane);
+        qkv_to_lds(eb.qkv + (int64_t)ii * NE * 3 * EMB, s_qkv, lane);
         wave_sync();
         for (int cc = 0; cc < 3; ++cc) {
             const float* Pv = eb.Pw + ((int64_t)cc * c.I + ii) * 1024;
@@ -1519,10 +1542,9 @@ __global__ void __launch_bounds__(64) ent_bwd_kernel(RCfg c_arg, MlgEntityBatch 
 #else
         in_transT_lds_b16(dx1, eb.wspT, s_dqkv, lane);
 #endif
-        const float* x1 = eb.x1 + ((int64_t)ii * NE + col) * EMB;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const floatx4 xv = ld4(x1 + q * 16 + 4 * g);
+            const floatx4 xv = x1v[q];
 #pragma unroll
             for (int r = 0; r < 4; ++r) dx1[q][r] = xv[r] > 0.f ? dx1[q][r] : 0.f;
             *reinterpret_cast<floatx4*>(eb.dfc1 + ((int64_t)ii * NE + col) * EMB + q * 16 + 4 * g) = dx1[q];
