@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "agent_device.h"
+#include "batch_mask_device.h"
 #include "gru4_device.h"
 #include "mlg_host.h"
 #include "wgrad_device.h"
@@ -226,21 +227,25 @@ struct PrepJob {
 static_assert(sizeof(PrepJob) <= 3072, "PrepJob must fit the kernel-argument segment");
 
 __global__ void __launch_bounds__(1024) prep_kernel(PrepJob J) {
-    __shared__ float red[1024];
     if (blockIdx.x == 0) {
+        __shared__ float red[1024];
+        __shared__ int32_t srows[MLG_INLINE_ROWS];
+        __shared__ mlg::MaskStatsLds ms;
+        MlgBatch b2 = J.bt;
         if (J.n_rows_in > 0) {  // the block reads the slot map from LDS; later launches from rows_dst
-            __shared__ int32_t srows[MLG_INLINE_ROWS];
             if (threadIdx.x < J.n_rows_in) {
                 srows[threadIdx.x] = J.rows_in[threadIdx.x];
                 J.rows_dst[threadIdx.x] = J.rows_in[threadIdx.x];
             }
             __syncthreads();
-            MlgBatch b2 = J.bt;
             b2.rows = srows;
-            mask_sum_block(b2, J.B, J.T, J.msum, red);
-            return;
         }
-        mask_sum_block(J.bt, J.B, J.T, J.msum, red);
+        constexpr int EPW = 4;  // episodes per wave: 16 waves cover batches of up to 64 episodes
+        if (mlg::mask_stats_fits<EPW>(J.B, J.T, blockDim.x / 64))  // one round trip (batch_mask_device.h)
+            mlg::batch_mask_stats<EPW>(b2.filled, b2.terminated, b2.T1, [&](int b) { return bslot(b2, b); }, J.B, J.T,
+                                       J.msum, nullptr, ms);
+        else
+            mask_sum_block(b2, J.B, J.T, J.msum, red);
         return;
     }
     const int64_t na = J.L.gsp,  // the learner reads no pre-split rollout sections (gsp, w1s)

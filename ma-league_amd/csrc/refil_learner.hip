@@ -523,9 +523,10 @@ __global__ void __launch_bounds__(256) prologue_kernel(Prologue P) {
     int blk = blockIdx.x;
     if (blk == 0) {
         __shared__ mlg::MaskStatsLds ms;
-        if (mlg::mask_stats_fits(P.c.B, P.c.T))  // one pass of independent loads (batch_mask_device.h)
-            mlg::batch_mask_stats(bt.filled, bt.terminated, bt.T1, [&](int b) { return eslot(bt, b); }, P.c.B, P.c.T,
-                                  P.msum, P.msum + 4, ms);
+        constexpr int EPW = 8;  // episodes per wave: 4 waves cover the bench's 32-episode batches
+        if (mlg::mask_stats_fits<EPW>(P.c.B, P.c.T, blockDim.x / 64))  // one round trip (batch_mask_device.h)
+            mlg::batch_mask_stats<EPW>(bt.filled, bt.terminated, bt.T1, [&](int b) { return eslot(bt, b); }, P.c.B,
+                                       P.c.T, P.msum, P.msum + 4, ms);
         else
             mask_sum_body(bt, P.c.B, P.c.T, P.msum, red);
         return;
