@@ -211,7 +211,19 @@ __device__ __forceinline__ void gru4_bwd(const Gru4Bwd& a, int tile, int Te, int
     float wt[KQ];  // A operand: W_hh[kq * KQ + kk][fD + i] (i = q)
 #pragma unroll
     for (int kk = 0; kk < KQ; ++kk) wt[kk] = a.whh[(int64_t)(kq * KQ + kk) * H + fD + q];
-    for (int i = tid; i < a.A * H; i += blockDim.x) w2s[i] = a.wq[i];  // output rows for dh += dq W_q[a]
+    {  // output rows for dh += dq W_q[a], staged in LDS: a thread's loads all issued before its first LDS write (the
+       // strided copy loop waited for each load in turn, ahead of the first step)
+        constexpr int PER = 8;
+        const int n = a.A * H, nt = blockDim.x;
+        for (int i0 = tid; i0 < n; i0 += PER * nt) {
+            float v[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) v[u] = i0 + u * nt < n ? a.wq[i0 + u * nt] : 0.f;
+#pragma unroll
+            for (int u = 0; u < PER; ++u)
+                if (i0 + u * nt < n) w2s[i0 + u * nt] = v[u];
+        }
+    }
     {  // steps past max_t_filled: zero deltas (wgrad rows); the tile's rows are contiguous per step
         const int nv = min(4, R - tile * 4) * 3 * H / 4;  // float4s per step and array
         for (int t = Te; t < a.T; ++t) {
