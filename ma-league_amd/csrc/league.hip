@@ -20,12 +20,27 @@ __global__ void __launch_bounds__(kRecThreads) league_record_kernel(const int32_
                                                                     float* __restrict__ entry, int count_games) {
     __shared__ int part[kRecThreads / 64][3];
     int w = 0, l = 0, d = 0;
-    for (int b = threadIdx.x; b < B; b += kRecThreads) {
-        const bool w0 = won[2 * b] != 0, w1 = won[2 * b + 1] != 0;
-        const bool dr = draw[b] != 0 || w0 == w1;
-        w += !dr && w0;
-        l += !dr && !w0;
-        d += dr;
+    // the run summary lives in pinned host memory (zero copy): a thread's loads are all issued before the first is
+    // used -- one host round trip, where the strided loop waited for each element in turn
+    constexpr int PER = 8;
+    for (int b0 = threadIdx.x; b0 < B; b0 += PER * kRecThreads) {
+        int wa[PER], wb[PER], dv[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int b = b0 + u * kRecThreads;
+            wa[u] = b < B ? won[2 * b] : 0;
+            wb[u] = b < B ? won[2 * b + 1] : 0;
+            dv[u] = b < B ? draw[b] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            if (b0 + u * kRecThreads >= B) break;
+            const bool w0 = wa[u] != 0, w1 = wb[u] != 0;
+            const bool dr = dv[u] != 0 || w0 == w1;
+            w += !dr && w0;
+            l += !dr && !w0;
+            d += dr;
+        }
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {

@@ -10,7 +10,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
 split() { name=${1%%:*}; rest=${1#*:}; lib=${rest%%:*}; envs=""; [ "$rest" != "$lib" ] && envs=${rest#*:}; }
-setenv() { [ -n "$lib" ] && export MLG_LIB=$lib; local IFS=,; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done; }
+# variant libraries as absolute paths: tests that start their own processes run them in other directories
+setenv() { [ -n "$lib" ] && case "$lib" in /*) export MLG_LIB=$lib ;; *) export MLG_LIB=$GRAFT_REPO_ROOT/$lib ;; esac
+           local IFS=,; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done; }
 for v in ${VARIANTS}; do
   split "$v"
   if [ -n "$TESTS" ]; then
